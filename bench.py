@@ -1,0 +1,272 @@
+#!/usr/bin/env python3
+"""Benchmark: GiB/s of device-resident shmem_double_sum_to_all, nreduce = 32 Mi.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+A "step" is one pass of the hot path over one batch of synthetic input
+(BASELINE.json metric; DESIGN.md "Measurement"):
+
+* N = 1 (BASELINE.json configs[1], "1 PE = 1 MI355X, local reduce only"): the
+  local element-wise reduction of the reference, write_to[i] =
+  op(write_to[i], pWrk[i]) (reduce-op.c:231-235), as the HIP fold kernel over
+  the whole 32 Mi-element array, called through the C ABI
+  (shmemx_fold_on_stream).  value = nreduce*8 B / step time.
+* N > 1 (configs[2]): the full collective shmemx_double_sum_to_all on all N
+  PEs (one per GPU, RCCL over xGMI), stream-ordered.  value = N * nreduce*8 B
+  / step time (whole job, weak scaling: every PE reduces its own 32 Mi array).
+
+Timing: W untimed warm-up steps, then K steps bracketed by a barrier and a
+device synchronize on both sides; the max over ranks is reported.  The
+kernel's average launch duration comes from HIP events recorded on the stream
+the kernel runs on.  The CPU baseline (rank 0, N = 1 only) times the oracle
+restatement of the reference's src/reduce on the host cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "openshmem-async_amd"))
+import shmem_mi355x as shm  # noqa: E402
+
+GiB = float(1 << 30)
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+XGMI_LINK_GBS = 153.0          # per link, 7 links per GPU
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--nreduce", type=int, default=32 * 1024 * 1024)
+    ap.add_argument("--algo", default="auto", choices=list(shm.ALGOS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-reps", type=int, default=20)
+    ap.add_argument("--extras", type=int, default=1, help="also time the other algorithms / API forms")
+    return ap.parse_args()
+
+
+def pmc_traffic(kernel_key: str):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any
+    (profiles/*pmc*.json written by tools/profile_pmc.py)."""
+    pdir = os.path.join(REPO, "profiles")
+    if not os.path.isdir(pdir):
+        return None
+    for name in sorted(os.listdir(pdir), reverse=True):
+        if "pmc" in name and name.endswith(".json"):
+            try:
+                with open(os.path.join(pdir, name)) as f:
+                    d = json.load(f)
+                v = d.get(kernel_key, {}).get("hbm_bytes_per_launch")
+                if v:
+                    return float(v)
+            except (OSError, ValueError):
+                continue
+    return None
+
+
+def cpu_baseline(n: int, reps: int):
+    """Oracle restatement of reduce-op.c, 2 PEs as 2 forked processes over
+    shared memory (the GASNet smp model), double sum over n elements; per-PE
+    algbw n*8/t of PE 0, median over `reps` warm calls."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # cpu_baseline leg only
+    t0 = time.perf_counter()
+    times, _ = oracle.reduce_fork("double", "sum", 2, 0, 0, 2, n, kind=0, reps=reps, pin_base=0)
+    wall = time.perf_counter() - t0
+    med = statistics.median(times)
+    return {"value": round(n * 8 / med / GiB, 4), "unit": "GiB/s", "cores": 2,
+            "kind": "port",
+            "sample": f"oracle restatement of reduce-op.c (gcc -O2), shmem_double_sum_to_all "
+                      f"nreduce={n} on 2 PEs = 2 processes pinned to 2 cores, shm loopback; "
+                      f"PE 0 per-call time, median of {reps} warm calls "
+                      f"({med * 1e3:.1f} ms/call, {wall:.1f} s wall)"}
+
+
+def time_region(fn, steps, stream, barrier):
+    """Run fn() `steps` times on `stream`; returns (wall_s, event_s)."""
+    barrier()
+    torch.cuda.synchronize()
+    start, stop = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    start.record(stream)
+    for _ in range(steps):
+        fn()
+    stop.record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    return t1 - t0, start.elapsed_time(stop) * 1e-3
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus != world:
+        if world == 1 and a.gpus > 1:
+            sys.exit("bench.py --gpus N>1 must be launched with torch.distributed.run")
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")
+        shm.init_from_torch_distributed(device=local)
+    else:
+        shm.init_attr(0, 1, local, None)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def max_over_ranks(x: float) -> float:
+        if dist is None:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    n = a.nreduce
+    nbytes = n * 8
+    stream = torch.cuda.Stream()
+    sp = stream.cuda_stream
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0x5EED0000 + rank)
+    src = torch.rand(n, dtype=torch.float64, device="cuda", generator=g) + 1.0   # [1, 2)
+    tgt = torch.empty_like(src)
+    torch.cuda.synchronize()
+
+    extras = {}
+    if world == 1:
+        workload = "local reduce (fold acc = acc + in) of shmem_double_sum_to_all, 1 PE"
+        acc = src.clone()
+        inp = torch.rand(n, dtype=torch.float64, device="cuda", generator=g) + 1.0
+
+        def step():
+            shm.fold("double", "sum", acc, inp, n, sp)
+        alg_bytes = 3 * nbytes                 # read acc, read in, write acc
+        algo_used = "fold"
+    else:
+        workload = f"shmem_double_sum_to_all on {world} PEs (one per GPU), RCCL over xGMI"
+        algo_used = a.algo
+
+        def step():
+            shm.reduce_on_stream("double", "sum", tgt, src, n, 0, 0, world, algo_used, sp)
+        alg_bytes = None
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    wall, ev = time_region(step, a.steps, stream, barrier)
+    wall = max_over_ranks(wall)
+    ev = max_over_ranks(ev)
+    ms_per_step = wall / a.steps * 1e3
+    value = world * nbytes * a.steps / wall / GiB
+
+    # correctness guard on what was timed
+    if world == 1:
+        chk = src.clone()
+        torch.cuda.synchronize()          # clone ran on torch's stream, fold runs on sp
+        shm.fold("double", "sum", chk, inp, n, sp)
+        torch.cuda.synchronize()
+        ok = torch.equal(chk, src + inp)
+    else:
+        sample = torch.arange(0, n, max(1, n // 4096), device="cuda")
+        mine = src[sample].cpu()
+        allv = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allv, mine)
+        ref = allv[0].clone()
+        abs_sum = allv[0].abs().clone()
+        for p in range(1, world):
+            ref += allv[p]
+            abs_sum += allv[p].abs()
+        got = tgt[sample].cpu()
+        tol = 2 * (world - 1) * 2.0 ** -53 * abs_sum
+        ok = bool(((got - ref).abs() <= tol).all())
+        ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
+
+    if world == 1:
+        t_launch = ev / a.steps
+        achieved = alg_bytes / t_launch / 1e9
+        traffic = pmc_traffic("fold_double_sum")
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
+                    "avg_launch_us": round(t_launch * 1e6, 2),
+                    "kernel": "fold_kernel<double,SUM,2 inputs>"}
+        if a.extras:
+            # the drop-in call itself at PE_size = 1 (copy semantics, reduce-op.c:213-216)
+            def api_step():
+                shm.reduce_on_stream("double", "sum", tgt, src, n, 0, 0, 1, "auto", sp)
+            for _ in range(3):
+                api_step()
+            w2, e2 = time_region(api_step, max(5, a.steps // 2), stream, barrier)
+            k2 = max(5, a.steps // 2)
+            extras["api_pe_size_1"] = {
+                "GiBps": round(nbytes * k2 / w2 / GiB, 1),
+                "hbm_GBps": round(2 * nbytes / (e2 / k2) / 1e9, 1),
+                "us_per_call": round(e2 / k2 * 1e6, 2)}
+    else:
+        t_call = ev / a.steps
+        xgmi_bytes = 2 * (world - 1) / world * nbytes        # per GPU, RS + AG
+        achieved = xgmi_bytes / t_call / 1e9
+        peak = (world - 1) * XGMI_LINK_GBS
+        roofline = {"bound": "xgmi", "achieved": round(achieved, 1), "peak": peak,
+                    "unit": "GB/s", "frac": round(achieved / peak, 4), "traffic": None,
+                    "alg_bytes_per_launch": int(xgmi_bytes),
+                    "avg_launch_us": round(t_call * 1e6, 2),
+                    "busbw_GBps": round(achieved, 1),
+                    "algbw_GiBps": round(nbytes / t_call / GiB, 2)}
+        if a.extras:
+            for alt in ("rccl", "a2a", "gather"):
+                if alt == algo_used:
+                    continue
+                def alt_step(alt=alt):
+                    shm.reduce_on_stream("double", "sum", tgt, src, n, 0, 0, world, alt, sp)
+                try:
+                    for _ in range(2):
+                        alt_step()
+                    k3 = max(3, a.steps // 4)
+                    w3, _ = time_region(alt_step, k3, stream, barrier)
+                    w3 = max_over_ranks(w3)
+                    extras[f"algo_{alt}_GiBps"] = round(world * nbytes * k3 / w3 / GiB, 2)
+                except shm.ShmemError as e:
+                    extras[f"algo_{alt}_GiBps"] = str(e)
+
+    cpu = None
+    if world == 1 and rank == 0 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(n, a.cpu_reps)
+
+    if rank == 0:
+        line = {
+            "metric": "GiB/s device-resident shmem_double_sum_to_all, nreduce=32Mi, 1/2/4/8 GPUs",
+            "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": workload, "nreduce": n, "type": "double", "op": "sum",
+                       "PE_size": world, "algo": algo_used,
+                       "parallelism": f"one PE per GPU x{world}"},
+            "roofline": roofline, "cpu_baseline": cpu, "correct": ok, "extras": extras,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()

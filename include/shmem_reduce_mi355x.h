@@ -1,0 +1,229 @@
+/*
+ * shmem_reduce_mi355x.h — C ABI of the MI355X-native OpenSHMEM reduction
+ * collectives (libshmem_reduce_mi355x.so).
+ *
+ * Part 1 declares, with the reference's exact prototypes, the 44
+ * shmem_<TYPE>_<OP>_to_all entry points that replace
+ * /root/reference/src/reduce/reduce-op.c:372-431 (declared in the reference at
+ * src/shmem.h:1412-1648, profiling names src/pshmem.h:328-526).  As with the
+ * reference built --enable-pshmem (reduce-op.c:275-364), every pshmem_* name is
+ * the strong symbol and every shmem_* name a weak alias of it, so profilers
+ * (TAU and friends) can still interpose.
+ *
+ * Part 2 is the minimum runtime the path needs: the PE identity that
+ * GET_STATE(mype)/shmem_my_pe() give the reference (utils/state.h,
+ * updown/updown.c:131-184), here one PE = one process = one MI355X.
+ *
+ * Part 3 holds extensions (shmemx_*): stream-ordered (graph-capturable)
+ * forms of the reduction, the local fold kernel on its own, the algorithm
+ * selector, the exchange plan query and error reporting.
+ *
+ * Semantics kept from the reference (see DESIGN.md "Boundary"):
+ *   - blocking collective over the active set PE_start + i*2^logPE_stride,
+ *     i < PE_size; every member calls with the same arguments;
+ *   - target/source may be host memory (as the reference's symmetric heap,
+ *     memory/symmem.c:168-227) or device memory; they may be the same array;
+ *   - pWrk is accepted and never touched; pSync is never written (so it stays
+ *     all SHMEM_SYNC_VALUE, the state barrier-linear.c:75 restores);
+ *   - no return value.  Bad arguments (nreduce < 0, caller not in the active
+ *     set, ...) leave target untouched and set shmemx_reduce_last_error();
+ *     HIP/RCCL failures print a FATAL line and abort, like the reference's
+ *     shmemi_trace(SHMEM_LOG_FATAL) (utils/trace.c:424-427).
+ */
+#ifndef SHMEM_REDUCE_MI355X_H
+#define SHMEM_REDUCE_MI355X_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+#include <complex>
+#define SHMEMX_COMPLEX(T) std::complex<T>
+extern "C" {
+#else
+#include <complex.h>
+#define SHMEMX_COMPLEX(T) T complex
+#endif
+
+/* Constants as the reference defines them on LP64 (shmem.h:1400-1410). */
+#ifndef SHMEM_REDUCE_SYNC_SIZE
+#define SHMEM_REDUCE_SYNC_SIZE        128L
+#define SHMEM_REDUCE_MIN_WRKDATA_SIZE 64L
+#define SHMEM_SYNC_VALUE              (-1L)
+#endif
+
+/* ------------------------------------------------------------------------ */
+/* Part 1: the 44 reduction entry points (shmem.h:1412-1648).               */
+
+#define SHMEMX_DECL_REDUCE(Name, Op, T)                                        \
+    void shmem_##Name##_##Op##_to_all(T *target, T *source, int nreduce,     \
+                                      int PE_start, int logPE_stride,        \
+                                      int PE_size, T *pWrk, long *pSync);    \
+    void pshmem_##Name##_##Op##_to_all(T *target, T *source, int nreduce,    \
+                                       int PE_start, int logPE_stride,       \
+                                       int PE_size, T *pWrk, long *pSync);
+
+#define SHMEMX_DECL_ARITH(Name, T) \
+    SHMEMX_DECL_REDUCE(Name, sum, T) SHMEMX_DECL_REDUCE(Name, prod, T)
+#define SHMEMX_DECL_LOGIC(Name, T)                                             \
+    SHMEMX_DECL_REDUCE(Name, and, T) SHMEMX_DECL_REDUCE(Name, or, T)         \
+    SHMEMX_DECL_REDUCE(Name, xor, T)
+#define SHMEMX_DECL_MINMAX(Name, T) \
+    SHMEMX_DECL_REDUCE(Name, min, T) SHMEMX_DECL_REDUCE(Name, max, T)
+
+/* sum/prod: 9 types (reduce-op.c:388-405) */
+SHMEMX_DECL_ARITH(short, short)
+SHMEMX_DECL_ARITH(int, int)
+SHMEMX_DECL_ARITH(long, long)
+SHMEMX_DECL_ARITH(longlong, long long)
+SHMEMX_DECL_ARITH(float, float)
+SHMEMX_DECL_ARITH(double, double)
+SHMEMX_DECL_ARITH(longdouble, long double)
+SHMEMX_DECL_ARITH(complexd, SHMEMX_COMPLEX(double))
+SHMEMX_DECL_ARITH(complexf, SHMEMX_COMPLEX(float))
+/* and/or/xor: 4 integer types (reduce-op.c:406-417) */
+SHMEMX_DECL_LOGIC(short, short)
+SHMEMX_DECL_LOGIC(int, int)
+SHMEMX_DECL_LOGIC(long, long)
+SHMEMX_DECL_LOGIC(longlong, long long)
+/* min/max: 7 real types (reduce-op.c:418-431) */
+SHMEMX_DECL_MINMAX(short, short)
+SHMEMX_DECL_MINMAX(int, int)
+SHMEMX_DECL_MINMAX(long, long)
+SHMEMX_DECL_MINMAX(longlong, long long)
+SHMEMX_DECL_MINMAX(float, float)
+SHMEMX_DECL_MINMAX(double, double)
+SHMEMX_DECL_MINMAX(longdouble, long double)
+
+/* ------------------------------------------------------------------------ */
+/* Part 2: runtime (replaces shmem_init updown.c:160, shmem_my_pe/n_pes).   */
+
+/* Bootstrap from the environment: PE = $SHMEM_PE or $RANK, npes =
+ * $SHMEM_NPES or $WORLD_SIZE (default 1), device = $LOCAL_RANK or PE mod the
+ * visible device count.  With npes > 1 the RCCL unique id is exchanged through
+ * the file $SHMEM_BOOTSTRAP_FILE (PE 0 writes it, the others wait for it);
+ * launchers that have their own channel should call shmemx_init_attr(). */
+void shmem_init(void);
+void shmem_finalize(void);
+int shmem_my_pe(void);
+int shmem_n_pes(void);
+void pshmem_init(void);
+void pshmem_finalize(void);
+int pshmem_my_pe(void);
+int pshmem_n_pes(void);
+
+/* ------------------------------------------------------------------------ */
+/* Part 3: extensions.                                                      */
+
+/* Type and op codes. */
+enum {
+    SHMEMX_TYPE_SHORT = 0, SHMEMX_TYPE_INT, SHMEMX_TYPE_LONG,
+    SHMEMX_TYPE_LONGLONG, SHMEMX_TYPE_FLOAT, SHMEMX_TYPE_DOUBLE,
+    SHMEMX_TYPE_LONGDOUBLE, SHMEMX_TYPE_COMPLEXD, SHMEMX_TYPE_COMPLEXF,
+    SHMEMX_NTYPES
+};
+enum {
+    SHMEMX_OP_SUM = 0, SHMEMX_OP_PROD, SHMEMX_OP_AND, SHMEMX_OP_OR,
+    SHMEMX_OP_XOR, SHMEMX_OP_MIN, SHMEMX_OP_MAX, SHMEMX_NOPS
+};
+
+/* Exchange algorithms (DESIGN.md "Multi-GPU").
+ *   AUTO    RCCL for what RCCL reduces exactly as specified, A2A otherwise
+ *   RCCL    ncclReduceScatter + ncclAllGather (+ ncclAllReduce on the
+ *           <P*16-byte tail); full active set, RCCL-native type/op only
+ *   A2A     shard exchange (grouped ncclSend/ncclRecv) -> HIP fold of the P
+ *           shards in active-set order -> shard all-gather; any set, any op;
+ *           every PE gets the reference's PE_start result bit for bit
+ *   GATHER  every PE receives every source and folds in its own reference
+ *           order: bit-exact with the reference on EVERY PE, (P-1)x traffic */
+enum {
+    SHMEMX_ALGO_AUTO = 0, SHMEMX_ALGO_RCCL, SHMEMX_ALGO_A2A,
+    SHMEMX_ALGO_GATHER, SHMEMX_NALGOS
+};
+
+/* Error codes returned by shmemx_* and stored for shmemx_reduce_last_error. */
+enum {
+    SHMEMX_OK = 0,
+    SHMEMX_EINVAL = 1,     /* bad argument (nreduce < 0, bad set, ...)     */
+    SHMEMX_ENOTMEMBER = 2, /* calling PE is not in the active set          */
+    SHMEMX_ENOTSUP = 3,    /* type/op/algorithm combination not supported  */
+    SHMEMX_ENOINIT = 4,    /* runtime not initialised and npes > 1         */
+    SHMEMX_ENOMEM = 5,     /* device workspace allocation failed           */
+    SHMEMX_EDEVICE = 6     /* HIP or RCCL reported an error                */
+};
+
+/* Bootstrap with a caller-distributed RCCL unique id (128 bytes): PE `pe` of
+ * `npes` on HIP device `device` (-1: pe mod device count).  PE 0 creates the
+ * id with shmemx_get_uniqueid() and the launcher broadcasts it. */
+int shmemx_uniqueid_size(void);
+int shmemx_get_uniqueid(void *uid_out);
+int shmemx_init_attr(int pe, int npes, int device, const void *uid);
+int shmemx_initialized(void);
+
+/* The HIP stream (hipStream_t) the blocking entry points run on. */
+void *shmemx_get_stream(void);
+
+/* Algorithm used by the entry points (default AUTO, or $SHMEM_REDUCE_ALGO =
+ * auto|rccl|a2a|gather).  Returns the previous value. */
+int shmemx_set_algo(int algo);
+
+/* Stream-ordered reduction: enqueue on `stream` (hipStream_t; NULL = the
+ * runtime's stream) and return without waiting.  Buffers must be device
+ * memory.  Capturable into a hipGraph once a call of the same shape has run
+ * (workspaces are allocated on first use). */
+int shmemx_reduce_on_stream(int type, int op, void *target, const void *source,
+                            int nreduce, int PE_start, int logPE_stride,
+                            int PE_size, int algo, void *stream);
+
+/* The local element-wise fold, reduce-op.c:231-235 as one HIP kernel:
+ *   acc[i] = op(acc[i], in[i])                              (fold2)
+ *   out[i] = op(...op(op(ins[0][i], ins[1][i]), ins[2][i])..., ins[nins-1][i])
+ * out may alias ins[0].  Device pointers, stream-ordered. */
+int shmemx_fold_on_stream(int type, int op, void *acc, const void *in,
+                          size_t nelems, void *stream);
+int shmemx_fold_n_on_stream(int type, int op, void *out,
+                            const void *const *ins, int nins, size_t nelems,
+                            void *stream);
+
+/* How a call would be executed (pure host logic, no device needed). */
+typedef struct {
+    int algo;          /* resolved SHMEMX_ALGO_* (never AUTO)               */
+    int member;        /* index of `pe` in the active set, -1 if none       */
+    int nmembers;      /* PE_size                                           */
+    int elem_size;     /* bytes per element                                 */
+    long long chunk;   /* elements per shard (A2A) / per RCCL shard (RCCL)  */
+    long long main;    /* RCCL: elements done by reduce-scatter+all-gather  */
+    long long tail;    /* RCCL: elements done by the all-reduce tail        */
+    long long ws_bytes;/* device workspace this call needs                  */
+} shmemx_plan_t;
+int shmemx_reduce_plan(int type, int op, int nreduce, int PE_start,
+                       int logPE_stride, int PE_size, int pe, int npes,
+                       int algo, shmemx_plan_t *plan);
+
+/* Element size in bytes of a SHMEMX_TYPE_* (0 if unknown); 1 if the
+ * reference defines shmem_<type>_<op>_to_all (reduce-op.c:388-431);
+ * 1 if this build runs that pair on the GPU. */
+size_t shmemx_type_size(int type);
+int shmemx_op_valid(int type, int op);
+int shmemx_op_on_device(int type, int op);
+
+/* Last error of this thread and its text. */
+int shmemx_reduce_last_error(void);
+const char *shmemx_reduce_error_string(int err);
+
+/* Typed stream-ordered forms of the 44 entry points. */
+#define SHMEMX_DECL_REDUCE_STREAM(Name, Op, T)                                 \
+    void shmemx_##Name##_##Op##_to_all_on_stream(                            \
+        T *target, const T *source, int nreduce, int PE_start,               \
+        int logPE_stride, int PE_size, void *stream);
+SHMEMX_DECL_REDUCE_STREAM(double, sum, double)
+SHMEMX_DECL_REDUCE_STREAM(float, sum, float)
+SHMEMX_DECL_REDUCE_STREAM(int, sum, int)
+SHMEMX_DECL_REDUCE_STREAM(long, sum, long)
+SHMEMX_DECL_REDUCE_STREAM(long, and, long)
+SHMEMX_DECL_REDUCE_STREAM(long, or, long)
+SHMEMX_DECL_REDUCE_STREAM(long, xor, long)
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SHMEM_REDUCE_MI355X_H */

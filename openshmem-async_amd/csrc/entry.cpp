@@ -1,0 +1,91 @@
+// The 44 drop-in entry points.  Each replaces one
+// SHMEM_REDUCE_TYPE_OP(op, name, type) instantiation of the reference
+// (/root/reference/src/reduce/reduce-op.c:372-431): same name, same
+// signature (src/shmem.h:1412-1648), pshmem_* strong with a weak shmem_*
+// alias as with --enable-pshmem (reduce-op.c:275-364).  pWrk and pSync are
+// accepted for ABI compatibility and not used: the exchange runs over RCCL,
+// not through pWrk, and completion is stream order + a host wait, not the
+// pSync barrier, so pSync keeps its SHMEM_SYNC_VALUE contents.
+#include <complex>
+
+#include "internal.h"
+#include "shmem_reduce_mi355x.h"
+
+namespace shmx {
+void reduce_blocking(int type, int op, void *target, const void *source,
+                     int nreduce, int start, int logstride, int size);
+int reduce_on_stream(int type, int op, void *target, const void *source,
+                     int nreduce, int start, int logstride, int size, int algo,
+                     void *stream);
+}  // namespace shmx
+
+#define SHMX_ENTRY(Name, Op, T, TYPE, OPC)                                     \
+    void pshmem_##Name##_##Op##_to_all(T *target, T *source, int nreduce,    \
+                                       int PE_start, int logPE_stride,       \
+                                       int PE_size, T *pWrk, long *pSync)    \
+    {                                                                        \
+        (void)pWrk;                                                          \
+        (void)pSync;                                                         \
+        shmx::reduce_blocking(TYPE, OPC, target, source, nreduce, PE_start,  \
+                              logPE_stride, PE_size);                        \
+    }                                                                        \
+    void shmem_##Name##_##Op##_to_all(T *, T *, int, int, int, int, T *,     \
+                                      long *)                                \
+        __attribute__((weak, alias("pshmem_" #Name "_" #Op "_to_all")));
+
+#define SHMX_ARITH(Name, T, TYPE)                                              \
+    SHMX_ENTRY(Name, sum, T, TYPE, SHMEMX_OP_SUM)                            \
+    SHMX_ENTRY(Name, prod, T, TYPE, SHMEMX_OP_PROD)
+#define SHMX_LOGIC(Name, T, TYPE)                                              \
+    SHMX_ENTRY(Name, and, T, TYPE, SHMEMX_OP_AND)                            \
+    SHMX_ENTRY(Name, or, T, TYPE, SHMEMX_OP_OR)                              \
+    SHMX_ENTRY(Name, xor, T, TYPE, SHMEMX_OP_XOR)
+#define SHMX_MINMAX(Name, T, TYPE)                                             \
+    SHMX_ENTRY(Name, min, T, TYPE, SHMEMX_OP_MIN)                            \
+    SHMX_ENTRY(Name, max, T, TYPE, SHMEMX_OP_MAX)
+
+extern "C" {
+
+// sum / prod (reduce-op.c:388-405)
+SHMX_ARITH(short, short, SHMEMX_TYPE_SHORT)
+SHMX_ARITH(int, int, SHMEMX_TYPE_INT)
+SHMX_ARITH(long, long, SHMEMX_TYPE_LONG)
+SHMX_ARITH(longlong, long long, SHMEMX_TYPE_LONGLONG)
+SHMX_ARITH(double, double, SHMEMX_TYPE_DOUBLE)
+SHMX_ARITH(float, float, SHMEMX_TYPE_FLOAT)
+SHMX_ARITH(longdouble, long double, SHMEMX_TYPE_LONGDOUBLE)
+SHMX_ARITH(complexd, std::complex<double>, SHMEMX_TYPE_COMPLEXD)
+SHMX_ARITH(complexf, std::complex<float>, SHMEMX_TYPE_COMPLEXF)
+// and / or / xor (reduce-op.c:406-417)
+SHMX_LOGIC(short, short, SHMEMX_TYPE_SHORT)
+SHMX_LOGIC(int, int, SHMEMX_TYPE_INT)
+SHMX_LOGIC(long, long, SHMEMX_TYPE_LONG)
+SHMX_LOGIC(longlong, long long, SHMEMX_TYPE_LONGLONG)
+// max / min (reduce-op.c:418-431)
+SHMX_MINMAX(short, short, SHMEMX_TYPE_SHORT)
+SHMX_MINMAX(int, int, SHMEMX_TYPE_INT)
+SHMX_MINMAX(long, long, SHMEMX_TYPE_LONG)
+SHMX_MINMAX(longlong, long long, SHMEMX_TYPE_LONGLONG)
+SHMX_MINMAX(double, double, SHMEMX_TYPE_DOUBLE)
+SHMX_MINMAX(float, float, SHMEMX_TYPE_FLOAT)
+SHMX_MINMAX(longdouble, long double, SHMEMX_TYPE_LONGDOUBLE)
+
+// Stream-ordered typed forms (header Part 3).
+#define SHMX_STREAM(Name, Op, T, TYPE, OPC)                                    \
+    void shmemx_##Name##_##Op##_to_all_on_stream(                            \
+        T *target, const T *source, int nreduce, int PE_start,               \
+        int logPE_stride, int PE_size, void *stream)                         \
+    {                                                                        \
+        shmx::reduce_on_stream(TYPE, OPC, target, source, nreduce, PE_start, \
+                               logPE_stride, PE_size, SHMEMX_ALGO_AUTO,      \
+                               stream);                                      \
+    }
+SHMX_STREAM(double, sum, double, SHMEMX_TYPE_DOUBLE, SHMEMX_OP_SUM)
+SHMX_STREAM(float, sum, float, SHMEMX_TYPE_FLOAT, SHMEMX_OP_SUM)
+SHMX_STREAM(int, sum, int, SHMEMX_TYPE_INT, SHMEMX_OP_SUM)
+SHMX_STREAM(long, sum, long, SHMEMX_TYPE_LONG, SHMEMX_OP_SUM)
+SHMX_STREAM(long, and, long, SHMEMX_TYPE_LONG, SHMEMX_OP_AND)
+SHMX_STREAM(long, or, long, SHMEMX_TYPE_LONG, SHMEMX_OP_OR)
+SHMX_STREAM(long, xor, long, SHMEMX_TYPE_LONG, SHMEMX_OP_XOR)
+
+}  // extern "C"

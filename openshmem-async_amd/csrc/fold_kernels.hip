@@ -1,0 +1,421 @@
+// gfx950 (MI355X, CDNA4) kernels for the OpenSHMEM reduction collectives.
+//
+// One kernel family does all the arithmetic of the path: the element-wise
+// left fold of reduce-op.c:213-248,
+//     write_to = source_me;  for each other PE p: write_to = op(write_to, src_p)
+// here as ONE pass over all inputs instead of one pass per peer:
+//     out[i] = op(...op(op(in0[i], in1[i]), in2[i])..., in_{k-1}[i])
+// with the element ops of reduce-op.c:71-150 (sum a+b, prod a*b, and/or/xor,
+// min a<b?a:b, max a>b?a:b).  nins == 2 with out == in0 is the reference's
+// inner fold write_to[ti] = op(write_to[ti], pWrk[j]) (reduce-op.c:231-235);
+// nins == 1 is the copy of reduce-op.c:213-216.
+//
+// Design for gfx950 (DESIGN.md "Kernels"):
+//   * HBM-bound streaming: 16-byte loads/stores per lane (global_load_dwordx4),
+//     a wave-instruction covers 1 KiB contiguous; UNROLL independent vectors
+//     per input per lane are issued before any op, so a 256-lane workgroup
+//     keeps UNROLL*nins*4 KiB in flight;
+//   * whole-chunk fast path with no per-vector guards (a guarded unrolled load
+//     makes hipcc wait vmcnt(0) per element), guarded path only for the last
+//     partial chunk;
+//   * scalar head/tail peeling so 8-byte-aligned (dlmalloc, dlmalloc.c:557)
+//     or odd-length arrays still take the vector body;
+//   * no LDS, no DPP: an element-wise fold has no intra-wave reduction and no
+//     reuse, so an LDS round trip would be pure overhead;
+//   * bit-exact with the reference's C: integers wrap in unsigned arithmetic,
+//     short is computed in int and truncated, no FP contraction
+//     (-ffp-contract=off), min/max are selects (not v_min_f64, whose NaN / -0
+//     behaviour differs), complex products follow C99 Annex G / libgcc
+//     __muldc3 including its NaN-recovery branch.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdlib>
+#include <type_traits>
+
+#include "internal.h"
+#include "shmem_reduce_mi355x.h"
+
+namespace shmx {
+
+namespace {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+struct cplxd { double re, im; };
+struct cplxf { float re, im; };
+
+// ------------------------------------------------------------- element ops
+template <typename T> struct Wide { using U = std::make_unsigned_t<T>; };
+template <> struct Wide<short> { using U = unsigned int; };  // int promotion
+
+template <typename T>
+__device__ __forceinline__ T add_wrap(T a, T b) {
+    using U = typename Wide<T>::U;
+    return (T)((U)a + (U)b);
+}
+template <typename T>
+__device__ __forceinline__ T mul_wrap(T a, T b) {
+    using U = typename Wide<T>::U;
+    return (T)((U)a * (U)b);
+}
+
+// C99 Annex G complex multiply as libgcc's __muldc3 / __mulsc3 compute it.
+template <typename S>
+__device__ __forceinline__ void cmul(S a, S b, S c, S d, S &xr, S &yr) {
+    S ac = a * c, bd = b * d, ad = a * d, bc = b * c;
+    S x = ac - bd, y = ad + bc;
+    if (__builtin_isnan(x) && __builtin_isnan(y)) {
+        bool recalc = false;
+        const S inf = __builtin_inf();
+        if (__builtin_isinf(a) || __builtin_isinf(b)) {
+            a = __builtin_copysign(__builtin_isinf(a) ? S(1) : S(0), a);
+            b = __builtin_copysign(__builtin_isinf(b) ? S(1) : S(0), b);
+            if (__builtin_isnan(c)) c = __builtin_copysign(S(0), c);
+            if (__builtin_isnan(d)) d = __builtin_copysign(S(0), d);
+            recalc = true;
+        }
+        if (__builtin_isinf(c) || __builtin_isinf(d)) {
+            c = __builtin_copysign(__builtin_isinf(c) ? S(1) : S(0), c);
+            d = __builtin_copysign(__builtin_isinf(d) ? S(1) : S(0), d);
+            if (__builtin_isnan(a)) a = __builtin_copysign(S(0), a);
+            if (__builtin_isnan(b)) b = __builtin_copysign(S(0), b);
+            recalc = true;
+        }
+        if (!recalc && (__builtin_isinf(ac) || __builtin_isinf(bd) ||
+                        __builtin_isinf(ad) || __builtin_isinf(bc))) {
+            if (__builtin_isnan(a)) a = __builtin_copysign(S(0), a);
+            if (__builtin_isnan(b)) b = __builtin_copysign(S(0), b);
+            if (__builtin_isnan(c)) c = __builtin_copysign(S(0), c);
+            if (__builtin_isnan(d)) d = __builtin_copysign(S(0), d);
+            recalc = true;
+        }
+        if (recalc) {
+            x = inf * (a * c - b * d);
+            y = inf * (a * d + b * c);
+        }
+    }
+    xr = x;
+    yr = y;
+}
+
+template <typename T, int OP> struct Op;
+
+// Integer types: all seven ops (reduce-op.c:85-90,120-123,144-147).
+#define SHMX_INT_OPS(T)                                                        \
+    template <> struct Op<T, SHMEMX_OP_SUM> {                                \
+        __device__ static T ap(T a, T b) { return add_wrap(a, b); } };       \
+    template <> struct Op<T, SHMEMX_OP_PROD> {                               \
+        __device__ static T ap(T a, T b) { return mul_wrap(a, b); } };       \
+    template <> struct Op<T, SHMEMX_OP_AND> {                                \
+        __device__ static T ap(T a, T b) { return (T)(a & b); } };           \
+    template <> struct Op<T, SHMEMX_OP_OR> {                                 \
+        __device__ static T ap(T a, T b) { return (T)(a | b); } };           \
+    template <> struct Op<T, SHMEMX_OP_XOR> {                                \
+        __device__ static T ap(T a, T b) { return (T)(a ^ b); } };           \
+    template <> struct Op<T, SHMEMX_OP_MIN> {                                \
+        __device__ static T ap(T a, T b) { return a < b ? a : b; } };        \
+    template <> struct Op<T, SHMEMX_OP_MAX> {                                \
+        __device__ static T ap(T a, T b) { return a > b ? a : b; } };
+SHMX_INT_OPS(short)
+SHMX_INT_OPS(int)
+SHMX_INT_OPS(long)
+#undef SHMX_INT_OPS
+
+// Real floating types: sum, prod, min, max (reduce-op.c:88-89,148-149).
+#define SHMX_FP_OPS(T)                                                         \
+    template <> struct Op<T, SHMEMX_OP_SUM> {                                \
+        __device__ static T ap(T a, T b) { return a + b; } };                \
+    template <> struct Op<T, SHMEMX_OP_PROD> {                               \
+        __device__ static T ap(T a, T b) { return a * b; } };               \
+    template <> struct Op<T, SHMEMX_OP_MIN> {                                \
+        __device__ static T ap(T a, T b) { return a < b ? a : b; } };        \
+    template <> struct Op<T, SHMEMX_OP_MAX> {                                \
+        __device__ static T ap(T a, T b) { return a > b ? a : b; } };
+SHMX_FP_OPS(float)
+SHMX_FP_OPS(double)
+#undef SHMX_FP_OPS
+
+// Complex: sum and prod (reduce-op.c:92-93).
+#define SHMX_CPLX_OPS(C, S)                                                    \
+    template <> struct Op<C, SHMEMX_OP_SUM> {                                \
+        __device__ static C ap(C a, C b) {                                   \
+            return C{a.re + b.re, a.im + b.im}; } };                         \
+    template <> struct Op<C, SHMEMX_OP_PROD> {                               \
+        __device__ static C ap(C a, C b) {                                   \
+            C r; cmul<S>(a.re, a.im, b.re, b.im, r.re, r.im); return r; } };
+SHMX_CPLX_OPS(cplxd, double)
+SHMX_CPLX_OPS(cplxf, float)
+#undef SHMX_CPLX_OPS
+
+// ------------------------------------------------------- vector plumbing
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const u32x4 *p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st16(u32x4 *p, u32x4 v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+template <typename T, int OP>
+__device__ __forceinline__ u32x4 apply16(u32x4 a, u32x4 b) {
+    constexpr int E = 16 / sizeof(T);
+    union U { u32x4 v; T e[E]; };
+    U x, y;
+    x.v = a;
+    y.v = b;
+#pragma unroll
+    for (int e = 0; e < E; ++e) x.e[e] = Op<T, OP>::ap(x.e[e], y.e[e]);
+    return x.v;
+}
+
+struct FoldArgs {
+    void *out;
+    const void *ins[kMaxFoldInputs];
+    int nins;
+    size_t head;   // scalar elements before the first 16-B aligned vector
+    size_t nvec;   // 16-B vectors in the aligned body
+    size_t tail;   // scalar elements after it
+};
+
+constexpr int kBlock = 256;  // 4 waves of 64
+
+// NIN > 0: number of inputs fixed at compile time (all loads hoisted);
+// NIN == 0: runtime args.nins.
+template <typename T, int OP, int NIN, int UNROLL, bool NT>
+__global__ __launch_bounds__(kBlock) void fold_kernel(FoldArgs args) {
+    constexpr int E = 16 / sizeof(T);
+    const int nins = NIN > 0 ? NIN : args.nins;
+    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t nthr = (size_t)gridDim.x * kBlock;
+
+    // Scalar head and tail (grid-stride: the whole array when the inputs
+    // do not share one alignment).
+    {
+        T *out = static_cast<T *>(args.out);
+        const size_t body_end = args.head + args.nvec * E;
+        const size_t nscalar = args.head + args.tail;
+        for (size_t s = tid; s < nscalar; s += nthr) {
+            const size_t i = s < args.head ? s : body_end + (s - args.head);
+            T acc = static_cast<const T *>(args.ins[0])[i];
+            for (int k = 1; k < nins; ++k)
+                acc = Op<T, OP>::ap(acc, static_cast<const T *>(args.ins[k])[i]);
+            out[i] = acc;
+        }
+    }
+    if (args.nvec == 0) return;
+
+    u32x4 *out = reinterpret_cast<u32x4 *>(static_cast<T *>(args.out) + args.head);
+    const size_t nvec = args.nvec;
+    const size_t step = (size_t)gridDim.x * kBlock * UNROLL;
+    for (size_t base = (size_t)blockIdx.x * kBlock * UNROLL; base < nvec;
+         base += step) {
+        const size_t v0 = base + threadIdx.x;
+        if (base + (size_t)kBlock * UNROLL <= nvec) {
+            // whole chunk in range: unguarded, every load issued up front
+            u32x4 acc[UNROLL];
+            const u32x4 *in0 = reinterpret_cast<const u32x4 *>(
+                static_cast<const T *>(args.ins[0]) + args.head);
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) acc[u] = ld16<NT>(in0 + v0 + u * kBlock);
+            if constexpr (NIN > 0) {
+                u32x4 x[NIN > 1 ? NIN - 1 : 1][UNROLL];
+#pragma unroll
+                for (int k = 1; k < NIN; ++k) {
+                    const u32x4 *ink = reinterpret_cast<const u32x4 *>(
+                        static_cast<const T *>(args.ins[k]) + args.head);
+#pragma unroll
+                    for (int u = 0; u < UNROLL; ++u)
+                        x[k - 1][u] = ld16<NT>(ink + v0 + u * kBlock);
+                }
+#pragma unroll
+                for (int k = 1; k < NIN; ++k)
+#pragma unroll
+                    for (int u = 0; u < UNROLL; ++u)
+                        acc[u] = apply16<T, OP>(acc[u], x[k - 1][u]);
+            } else {
+                for (int k = 1; k < nins; ++k) {
+                    const u32x4 *ink = reinterpret_cast<const u32x4 *>(
+                        static_cast<const T *>(args.ins[k]) + args.head);
+                    u32x4 x[UNROLL];
+#pragma unroll
+                    for (int u = 0; u < UNROLL; ++u) x[u] = ld16<NT>(ink + v0 + u * kBlock);
+#pragma unroll
+                    for (int u = 0; u < UNROLL; ++u) acc[u] = apply16<T, OP>(acc[u], x[u]);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) st16<NT>(out + v0 + u * kBlock, acc[u]);
+        } else {
+            // last partial chunk: one vector at a time, guarded
+            for (int u = 0; u < UNROLL; ++u) {
+                const size_t v = v0 + (size_t)u * kBlock;
+                if (v >= nvec) break;
+                u32x4 acc = ld16<NT>(reinterpret_cast<const u32x4 *>(
+                                         static_cast<const T *>(args.ins[0]) + args.head) + v);
+                for (int k = 1; k < nins; ++k)
+                    acc = apply16<T, OP>(acc, ld16<NT>(reinterpret_cast<const u32x4 *>(
+                                                 static_cast<const T *>(args.ins[k]) + args.head) + v));
+                st16<NT>(out + v, acc);
+            }
+        }
+    }
+}
+
+// Vectors per lane per input, by element size: keeps ~64 B per lane per input
+// in flight for every type.
+constexpr int kUnroll = 4;
+
+template <typename T, int OP, bool NT>
+hipError_t launch_typed(const FoldArgs &a, hipStream_t stream) {
+    const FoldTuning &tune = fold_tuning();
+    size_t work_blocks;
+    if (a.nvec > 0)
+        work_blocks = (a.nvec + (size_t)kBlock * kUnroll - 1) / ((size_t)kBlock * kUnroll);
+    else
+        work_blocks = (a.head + a.tail + kBlock - 1) / kBlock;
+    // The scalar-only case (inputs of different alignment) is capped hard; the
+    // vector body runs one chunk per block unless a cap is set.
+    size_t cap = tune.max_blocks > 0 ? (size_t)tune.max_blocks : (size_t)1 << 30;
+    if (a.nvec == 0 && cap > 2048) cap = 2048;
+    size_t blocks = work_blocks < cap ? work_blocks : cap;
+    if (blocks < 1) blocks = 1;
+    if (blocks > (size_t)INT_MAX) blocks = INT_MAX;
+    if (a.nins == 2)
+        hipLaunchKernelGGL((fold_kernel<T, OP, 2, kUnroll, NT>), dim3((unsigned)blocks),
+                           dim3(kBlock), 0, stream, a);
+    else
+        hipLaunchKernelGGL((fold_kernel<T, OP, 0, kUnroll, NT>), dim3((unsigned)blocks),
+                           dim3(kBlock), 0, stream, a);
+    return hipGetLastError();
+}
+
+template <typename T, int OP>
+hipError_t launch_nt(const FoldArgs &a, hipStream_t stream) {
+    return fold_tuning().nontemporal ? launch_typed<T, OP, true>(a, stream)
+                                     : launch_typed<T, OP, false>(a, stream);
+}
+
+template <typename T>
+hipError_t launch_int_ops(int op, const FoldArgs &a, hipStream_t s) {
+    switch (op) {
+    case SHMEMX_OP_SUM: return launch_nt<T, SHMEMX_OP_SUM>(a, s);
+    case SHMEMX_OP_PROD: return launch_nt<T, SHMEMX_OP_PROD>(a, s);
+    case SHMEMX_OP_AND: return launch_nt<T, SHMEMX_OP_AND>(a, s);
+    case SHMEMX_OP_OR: return launch_nt<T, SHMEMX_OP_OR>(a, s);
+    case SHMEMX_OP_XOR: return launch_nt<T, SHMEMX_OP_XOR>(a, s);
+    case SHMEMX_OP_MIN: return launch_nt<T, SHMEMX_OP_MIN>(a, s);
+    case SHMEMX_OP_MAX: return launch_nt<T, SHMEMX_OP_MAX>(a, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+template <typename T>
+hipError_t launch_fp_ops(int op, const FoldArgs &a, hipStream_t s) {
+    switch (op) {
+    case SHMEMX_OP_SUM: return launch_nt<T, SHMEMX_OP_SUM>(a, s);
+    case SHMEMX_OP_PROD: return launch_nt<T, SHMEMX_OP_PROD>(a, s);
+    case SHMEMX_OP_MIN: return launch_nt<T, SHMEMX_OP_MIN>(a, s);
+    case SHMEMX_OP_MAX: return launch_nt<T, SHMEMX_OP_MAX>(a, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+template <typename T>
+hipError_t launch_cplx_ops(int op, const FoldArgs &a, hipStream_t s) {
+    switch (op) {
+    case SHMEMX_OP_SUM: return launch_nt<T, SHMEMX_OP_SUM>(a, s);
+    case SHMEMX_OP_PROD: return launch_nt<T, SHMEMX_OP_PROD>(a, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace
+
+FoldTuning &fold_tuning() {
+    static FoldTuning t = [] {
+        FoldTuning r{0, 0};
+        if (const char *e = std::getenv("SHMEMX_FOLD_MAX_BLOCKS")) r.max_blocks = std::atoi(e);
+        if (const char *e = std::getenv("SHMEMX_FOLD_NT")) r.nontemporal = std::atoi(e);
+        return r;
+    }();
+    return t;
+}
+
+size_t type_size(int type) {
+    switch (type) {
+    case SHMEMX_TYPE_SHORT: return sizeof(short);
+    case SHMEMX_TYPE_INT: return sizeof(int);
+    case SHMEMX_TYPE_LONG: return sizeof(long);
+    case SHMEMX_TYPE_LONGLONG: return sizeof(long long);
+    case SHMEMX_TYPE_FLOAT: return sizeof(float);
+    case SHMEMX_TYPE_DOUBLE: return sizeof(double);
+    case SHMEMX_TYPE_LONGDOUBLE: return sizeof(long double);
+    case SHMEMX_TYPE_COMPLEXD: return 2 * sizeof(double);
+    case SHMEMX_TYPE_COMPLEXF: return 2 * sizeof(float);
+    default: return 0;
+    }
+}
+
+bool op_valid(int type, int op) {
+    if (type < 0 || type >= SHMEMX_NTYPES || op < 0 || op >= SHMEMX_NOPS) return false;
+    switch (op) {
+    case SHMEMX_OP_SUM:
+    case SHMEMX_OP_PROD: return true;
+    case SHMEMX_OP_AND:
+    case SHMEMX_OP_OR:
+    case SHMEMX_OP_XOR: return type <= SHMEMX_TYPE_LONGLONG;
+    default: return type != SHMEMX_TYPE_COMPLEXD && type != SHMEMX_TYPE_COMPLEXF;
+    }
+}
+
+bool op_on_device(int type, int op) {
+    return op_valid(type, op) && type != SHMEMX_TYPE_LONGDOUBLE;
+}
+
+hipError_t launch_fold(int type, int op, void *out, const void *const *ins,
+                       int nins, size_t n, hipStream_t stream) {
+    if (!op_on_device(type, op) || nins < 1 || nins > kMaxFoldInputs || !out)
+        return hipErrorInvalidValue;
+    if (n == 0) return hipSuccess;
+    const size_t sz = type_size(type);
+    FoldArgs a{};
+    a.out = out;
+    a.nins = nins;
+    for (int k = 0; k < nins; ++k) {
+        if (!ins[k]) return hipErrorInvalidValue;
+        a.ins[k] = ins[k];
+    }
+    // Vector body only if every array sits at the same offset mod 16 and that
+    // offset is a whole number of elements.
+    const uintptr_t off = reinterpret_cast<uintptr_t>(out) & 15u;
+    bool same = (off % sz) == 0;
+    for (int k = 0; k < nins && same; ++k)
+        same = (reinterpret_cast<uintptr_t>(ins[k]) & 15u) == off;
+    if (same) {
+        size_t head = ((16 - off) & 15u) / sz;
+        if (head > n) head = n;
+        const size_t E = 16 / sz;
+        a.head = head;
+        a.nvec = (n - head) / E;
+        a.tail = n - head - a.nvec * E;
+    } else {
+        a.head = n;
+        a.nvec = 0;
+        a.tail = 0;
+    }
+    switch (type) {
+    case SHMEMX_TYPE_SHORT: return launch_int_ops<short>(op, a, stream);
+    case SHMEMX_TYPE_INT: return launch_int_ops<int>(op, a, stream);
+    case SHMEMX_TYPE_LONG:
+    case SHMEMX_TYPE_LONGLONG: return launch_int_ops<long>(op, a, stream);
+    case SHMEMX_TYPE_FLOAT: return launch_fp_ops<float>(op, a, stream);
+    case SHMEMX_TYPE_DOUBLE: return launch_fp_ops<double>(op, a, stream);
+    case SHMEMX_TYPE_COMPLEXD: return launch_cplx_ops<cplxd>(op, a, stream);
+    case SHMEMX_TYPE_COMPLEXF: return launch_cplx_ops<cplxf>(op, a, stream);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace shmx

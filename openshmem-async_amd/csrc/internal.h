@@ -1,0 +1,38 @@
+// Internal interfaces between the C-ABI/runtime (runtime.cpp, entry.cpp) and
+// the gfx950 kernels (fold_kernels.hip).  Not installed; not part of the ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+
+namespace shmx {
+
+// Upper bound on inputs one fold launch reads; longer folds are chained
+// (out = fold(ins[0..15]); out = fold(out, ins[16..30]); ...) which keeps the
+// reference's left-to-right order.
+constexpr int kMaxFoldInputs = 16;
+
+// Element sizes per SHMEMX_TYPE_* (long double is the host's 16-byte x87
+// slot; long and long long are both 8 bytes on LP64).
+size_t type_size(int type);
+bool op_valid(int type, int op);       // reference defines the pair
+bool op_on_device(int type, int op);   // this build has a HIP kernel for it
+
+// out[i] = op(...op(ins[0][i], ins[1][i])..., ins[nins-1][i]) for i < n.
+// nins in [1, kMaxFoldInputs]; nins == 1 is a copy.  out may be the very
+// same array as any input (each element is read by the lane that writes it,
+// before it writes it) but must not partially overlap one.  Returns
+// hipSuccess or the launch error.
+hipError_t launch_fold(int type, int op, void *out, const void *const *ins,
+                       int nins, size_t n, hipStream_t stream);
+
+// Tuning knobs for the fold kernels (read once from the environment:
+// SHMEMX_FOLD_MAX_BLOCKS, SHMEMX_FOLD_NT).
+struct FoldTuning {
+    int max_blocks;   // grid cap; 0 = one 16-B vector per lane per unroll slot
+    int nontemporal;  // 1: nt loads/stores on the streamed arrays
+};
+FoldTuning &fold_tuning();
+
+}  // namespace shmx

@@ -1,0 +1,666 @@
+// Host runtime of libshmem_reduce_mi355x.so: PE identity, HIP stream, RCCL
+// communicator, device workspaces, and the reduction engine that every
+// shmem_<T>_<op>_to_all entry point (entry.cpp) lands in.
+//
+// Reference mapping (all paths under /root/reference/src):
+//   shmemi_udr_<T>_to_all  reduce/reduce-op.c:169-260  -> reduce_device()
+//     copy write_to=source (:213-216)     -> fold kernel, 1 input (P == 1)
+//     barrier (:217,:250)                  -> stream order of RCCL + kernels
+//     per-peer shmem_getmem into pWrk      -> RCCL shard exchange over xGMI
+//       (:219-248, ptp/putget.c:234-240)
+//     (*the_op)(write_to, pWrk) (:231-235) -> one fold kernel over P shards
+//     overlap temp (:166-167,187-203)      -> stage source to a workspace
+//   GET_STATE(mype) utils/state.h:100-101  -> g_state.pe
+//   shmem_init      updown/updown.c:160    -> shmem_init / shmemx_init_attr
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "internal.h"
+#include "shmem_reduce_mi355x.h"
+
+namespace shmx {
+
+struct State {
+    bool inited = false;
+    int pe = 0;
+    int npes = 1;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    ncclComm_t comm = nullptr;
+    int algo = SHMEMX_ALGO_AUTO;
+    // grow-only device workspaces
+    void *ws = nullptr;        // A2A shard receive area / GATHER sources
+    size_t ws_bytes = 0;
+    void *tmp = nullptr;       // overlap temporary (reduce-op.c:187-203)
+    size_t tmp_bytes = 0;
+    void *stage_src = nullptr; // host-resident endpoints
+    void *stage_tgt = nullptr;
+    size_t stage_bytes = 0;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+};
+
+static State g_state;
+static std::recursive_mutex g_mu;
+static thread_local int t_last_error = SHMEMX_OK;
+
+static int set_error(int e) {
+    t_last_error = e;
+    return e;
+}
+
+// "%-8.8f PE %d: LEVEL: msg", the reference's trace line (utils/trace.c:400-431)
+static void trace(const char *level, const char *fmt, ...) {
+    const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() -
+                                                   g_state.t0).count();
+    char msg[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(msg, sizeof msg, fmt, ap);
+    va_end(ap);
+    fprintf(stderr, "%-8.8f PE %d: %s: %s\n", t, g_state.pe, level, msg);
+    fflush(stderr);
+}
+
+[[noreturn]] static void fatal(const char *what, const char *detail) {
+    trace("FATAL", "%s: %s", what, detail);
+    std::abort();
+}
+
+#define SHMX_HIP(call)                                                         \
+    do {                                                                     \
+        hipError_t e_ = (call);                                              \
+        if (e_ != hipSuccess) fatal(#call, hipGetErrorString(e_));           \
+    } while (0)
+#define SHMX_NCCL(call)                                                        \
+    do {                                                                     \
+        ncclResult_t r_ = (call);                                            \
+        if (r_ != ncclSuccess) fatal(#call, ncclGetErrorString(r_));         \
+    } while (0)
+
+static int env_int(const char *a, const char *b, int dflt) {
+    for (const char *k : {a, b}) {
+        if (!k) continue;
+        if (const char *v = std::getenv(k)) {
+            if (*v) return std::atoi(v);
+        }
+    }
+    return dflt;
+}
+
+static int parse_algo(const char *s) {
+    if (!s) return SHMEMX_ALGO_AUTO;
+    std::string v(s);
+    if (v == "rccl") return SHMEMX_ALGO_RCCL;
+    if (v == "a2a") return SHMEMX_ALGO_A2A;
+    if (v == "gather") return SHMEMX_ALGO_GATHER;
+    return SHMEMX_ALGO_AUTO;
+}
+
+static int init_locked(int pe, int npes, int device, const void *uid) {
+    if (g_state.inited) return SHMEMX_OK;
+    if (npes < 1 || pe < 0 || pe >= npes) return set_error(SHMEMX_EINVAL);
+    int ndev = 0;
+    SHMX_HIP(hipGetDeviceCount(&ndev));
+    if (ndev < 1) fatal("shmem_init", "no HIP device visible");
+    if (device < 0 && !(npes == 1 && hipGetDevice(&device) == hipSuccess)) device = pe % ndev;
+    if (device < 0 || device >= ndev) return set_error(SHMEMX_EINVAL);
+    SHMX_HIP(hipSetDevice(device));
+    SHMX_HIP(hipStreamCreateWithFlags(&g_state.stream, hipStreamNonBlocking));
+    if (npes > 1) {
+        if (!uid) return set_error(SHMEMX_EINVAL);
+        ncclUniqueId id;
+        std::memcpy(&id, uid, sizeof id);
+        SHMX_NCCL(ncclCommInitRank(&g_state.comm, npes, id, pe));
+    }
+    g_state.pe = pe;
+    g_state.npes = npes;
+    g_state.device = device;
+    g_state.algo = parse_algo(std::getenv("SHMEM_REDUCE_ALGO"));
+    g_state.inited = true;
+    return SHMEMX_OK;
+}
+
+// Exchange the RCCL id through a file: PE 0 writes it (atomically, via
+// rename), the others wait for a file no older than this process (minus a
+// margin), so a stale id from an earlier job is never used.
+static int file_bootstrap(int pe, int npes, int device) {
+    std::string path;
+    if (const char *p = std::getenv("SHMEM_BOOTSTRAP_FILE")) path = p;
+    else {
+        const char *port = std::getenv("MASTER_PORT");
+        path = std::string("/tmp/shmem_mi355x_uid.") + (port ? port : "0");
+    }
+    ncclUniqueId id;
+    const time_t started = time(nullptr);
+    if (pe == 0) {
+        SHMX_NCCL(ncclGetUniqueId(&id));
+        const std::string tmp = path + ".tmp." + std::to_string(getpid());
+        FILE *f = fopen(tmp.c_str(), "wb");
+        if (!f || fwrite(&id, sizeof id, 1, f) != 1) fatal("shmem_init", "cannot write bootstrap file");
+        fclose(f);
+        if (rename(tmp.c_str(), path.c_str()) != 0) fatal("shmem_init", "cannot publish bootstrap file");
+    } else {
+        for (int waited_ms = 0;; waited_ms += 20) {
+            struct stat st;
+            if (stat(path.c_str(), &st) == 0 && st.st_size == (off_t)sizeof id &&
+                st.st_mtime + 30 >= started) {
+                FILE *f = fopen(path.c_str(), "rb");
+                if (f) {
+                    const bool ok = fread(&id, sizeof id, 1, f) == 1;
+                    fclose(f);
+                    if (ok) break;
+                }
+            }
+            if (waited_ms > 300000) fatal("shmem_init", "timed out waiting for the bootstrap file");
+            std::this_thread::sleep_for(std::chrono::milliseconds(20));
+        }
+    }
+    const int rc = init_locked(pe, npes, device, &id);
+    if (pe == 0) unlink(path.c_str());  // every PE has read it: the init is collective
+    return rc;
+}
+
+static int ensure_init() {
+    if (g_state.inited) return SHMEMX_OK;
+    const int npes = env_int("SHMEM_NPES", "WORLD_SIZE", 1);
+    if (npes != 1) return set_error(SHMEMX_ENOINIT);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    return init_locked(0, 1, dev, nullptr);
+}
+
+// ----------------------------------------------------------------- plans
+
+static bool is_member(int pe, int start, int logstride, int size, int *index) {
+    const int step = 1 << logstride;
+    if (pe < start || (pe - start) % step) return false;
+    const int i = (pe - start) / step;
+    if (i >= size) return false;
+    if (index) *index = i;
+    return true;
+}
+
+static bool rccl_dtype(int type, ncclDataType_t *dt) {
+    switch (type) {
+    case SHMEMX_TYPE_INT: *dt = ncclInt32; return true;
+    case SHMEMX_TYPE_LONG:
+    case SHMEMX_TYPE_LONGLONG: *dt = ncclInt64; return true;
+    case SHMEMX_TYPE_FLOAT: *dt = ncclFloat32; return true;
+    case SHMEMX_TYPE_DOUBLE: *dt = ncclFloat64; return true;
+    default: return false;
+    }
+}
+
+// Pairs RCCL reduces exactly as reduce-op.c specifies: every integer op it
+// has (wrapping sum/prod, min, max), and float/double sum/prod (rounding
+// order differs from the reference's linear fold: ULP tolerance).
+// Float min/max are excluded: a<b?a:b is not RCCL's NaN/-0 behaviour.
+static bool rccl_native(int type, int op) {
+    ncclDataType_t dt;
+    if (!rccl_dtype(type, &dt)) return false;
+    const bool fp = type == SHMEMX_TYPE_FLOAT || type == SHMEMX_TYPE_DOUBLE;
+    switch (op) {
+    case SHMEMX_OP_SUM:
+    case SHMEMX_OP_PROD: return true;
+    case SHMEMX_OP_MIN:
+    case SHMEMX_OP_MAX: return !fp;
+    default: return false;
+    }
+}
+
+static ncclRedOp_t rccl_op(int op) {
+    switch (op) {
+    case SHMEMX_OP_SUM: return ncclSum;
+    case SHMEMX_OP_PROD: return ncclProd;
+    case SHMEMX_OP_MIN: return ncclMin;
+    default: return ncclMax;
+    }
+}
+
+static int make_plan(int type, int op, int nreduce, int start, int logstride,
+                     int size, int pe, int npes, int algo, shmemx_plan_t *p) {
+    std::memset(p, 0, sizeof *p);
+    p->member = -1;
+    if (!op_valid(type, op)) return SHMEMX_EINVAL;
+    if (nreduce < 0 || start < 0 || logstride < 0 || logstride > 30 || size < 1 ||
+        npes < 1 || algo < 0 || algo >= SHMEMX_NALGOS)
+        return SHMEMX_EINVAL;
+    if ((long long)start + (long long)(size - 1) * (1LL << logstride) >= npes)
+        return SHMEMX_EINVAL;
+    int m = -1;
+    if (!is_member(pe, start, logstride, size, &m)) return SHMEMX_ENOTMEMBER;
+    if (!op_on_device(type, op)) return SHMEMX_ENOTSUP;
+    const long long n = nreduce;
+    const int P = size;
+    const int sz = (int)type_size(type);
+    const long long g = sz >= 16 ? 1 : 16 / sz;  // elements per 16-byte granule
+    const bool world = start == 0 && (logstride == 0 || size == 1) && size == npes;
+    if (algo == SHMEMX_ALGO_AUTO)
+        algo = (world && rccl_native(type, op)) ? SHMEMX_ALGO_RCCL : SHMEMX_ALGO_A2A;
+    if (algo == SHMEMX_ALGO_RCCL && !(world && rccl_native(type, op))) return SHMEMX_ENOTSUP;
+    p->algo = algo;
+    p->member = m;
+    p->nmembers = P;
+    p->elem_size = sz;
+    if (P == 1) {
+        p->chunk = n;
+        return SHMEMX_OK;
+    }
+    switch (algo) {
+    case SHMEMX_ALGO_RCCL:
+        p->chunk = (n / (P * g)) * g;
+        p->main = p->chunk * P;
+        p->tail = n - p->main;
+        break;
+    case SHMEMX_ALGO_A2A: {
+        long long c = (n + P - 1) / P;
+        c = (c + g - 1) / g * g;
+        p->chunk = c;
+        p->ws_bytes = c * P * sz;
+        break;
+    }
+    default:  // GATHER
+        p->chunk = n;
+        p->ws_bytes = n * P * sz;
+        break;
+    }
+    return SHMEMX_OK;
+}
+
+// ------------------------------------------------------------- workspaces
+
+static void *grow(void *&buf, size_t &have, size_t need) {
+    if (need <= have) return buf;
+    if (buf) {
+        SHMX_HIP(hipStreamSynchronize(g_state.stream));
+        SHMX_HIP(hipFree(buf));
+        buf = nullptr;
+        have = 0;
+    }
+    if (hipMalloc(&buf, need) != hipSuccess) {
+        (void)hipGetLastError();
+        buf = nullptr;
+        return nullptr;
+    }
+    have = need;
+    return buf;
+}
+
+static bool overlap(const void *a, const void *b, size_t bytes) {
+    const char *x = static_cast<const char *>(a), *y = static_cast<const char *>(b);
+    return x != y && x < y + bytes && y < x + bytes;
+}
+
+static long long count_of(long long n, long long chunk, int i) {
+    const long long lo = chunk * i;
+    return std::max(0LL, std::min(chunk, n - lo));
+}
+
+static void fold_chain(int type, int op, void *out, const void **ins, int nins,
+                       size_t n, hipStream_t s) {
+    // Left fold in groups of kMaxFoldInputs: out = fold(ins[0..15]);
+    // out = fold(out, ins[16..30]); ... (same order as one long fold).
+    int done = std::min(nins, kMaxFoldInputs);
+    SHMX_HIP(launch_fold(type, op, out, ins, done, n, s));
+    while (done < nins) {
+        const void *grp[kMaxFoldInputs];
+        grp[0] = out;
+        int k = 1;
+        while (k < kMaxFoldInputs && done < nins) grp[k++] = ins[done++];
+        SHMX_HIP(launch_fold(type, op, out, grp, k, n, s));
+    }
+}
+
+// The engine: device-resident target/source, stream-ordered.
+static int reduce_device(int type, int op, void *target, const void *source,
+                         int nreduce, int start, int logstride, int size,
+                         int algo, hipStream_t s) {
+    shmemx_plan_t p;
+    int rc = make_plan(type, op, nreduce, start, logstride, size, g_state.pe,
+                       g_state.npes, algo, &p);
+    if (rc) return set_error(rc);
+    if (nreduce == 0) return SHMEMX_OK;
+    if (size > 1 && !g_state.comm) return set_error(SHMEMX_ENOINIT);
+    const size_t sz = (size_t)p.elem_size;
+    const size_t bytes = sz * (size_t)nreduce;
+    char *tgt = static_cast<char *>(target);
+    const char *src = static_cast<const char *>(source);
+
+    // Partially overlapping target/source: reduce from a private copy of the
+    // source (the reference's temporary target, reduce-op.c:187-203).
+    if (overlap(tgt, src, bytes)) {
+        void *t = grow(g_state.tmp, g_state.tmp_bytes, bytes);
+        if (!t) return set_error(SHMEMX_ENOMEM);
+        const void *in[1] = {src};
+        fold_chain(type, op, t, in, 1, (size_t)nreduce, s);
+        src = static_cast<const char *>(t);
+    }
+
+    const int P = size, m = p.member, step = 1 << logstride;
+    if (P == 1) {  // reduce-op.c:213-216 with no peers: a copy
+        if (tgt != src) {
+            const void *in[1] = {src};
+            fold_chain(type, op, tgt, in, 1, (size_t)nreduce, s);
+        }
+        return SHMEMX_OK;
+    }
+    auto peer = [&](int i) { return start + i * step; };
+
+    if (p.algo == SHMEMX_ALGO_RCCL) {
+        ncclDataType_t dt;
+        rccl_dtype(type, &dt);
+        const ncclRedOp_t rop = rccl_op(op);
+        if (p.chunk > 0) {
+            char *mine = tgt + (size_t)m * (size_t)p.chunk * sz;
+            SHMX_NCCL(ncclReduceScatter(src, mine, (size_t)p.chunk, dt, rop, g_state.comm, s));
+            SHMX_NCCL(ncclAllGather(mine, tgt, (size_t)p.chunk, dt, g_state.comm, s));
+        }
+        if (p.tail > 0) {
+            const size_t off = (size_t)p.main * sz;
+            SHMX_NCCL(ncclAllReduce(src + off, tgt + off, (size_t)p.tail, dt, rop, g_state.comm, s));
+        }
+        return SHMEMX_OK;
+    }
+
+    char *ws = static_cast<char *>(grow(g_state.ws, g_state.ws_bytes, (size_t)p.ws_bytes));
+    if (!ws) return set_error(SHMEMX_ENOMEM);
+    const long long n = nreduce;
+
+    if (p.algo == SHMEMX_ALGO_A2A) {
+        const size_t cb = (size_t)p.chunk * sz;
+        const long long my_cnt = count_of(n, p.chunk, m);
+        // 1. shard exchange: member i gets chunk i of every source
+        SHMX_NCCL(ncclGroupStart());
+        for (int i = 0; i < P; ++i) {
+            if (i == m) continue;
+            const long long ci = count_of(n, p.chunk, i);
+            if (ci > 0) SHMX_NCCL(ncclSend(src + i * cb, (size_t)ci * sz, ncclUint8, peer(i), g_state.comm, s));
+            if (my_cnt > 0) SHMX_NCCL(ncclRecv(ws + i * cb, (size_t)my_cnt * sz, ncclUint8, peer(i), g_state.comm, s));
+        }
+        SHMX_NCCL(ncclGroupEnd());
+        // 2. fold the P copies of my chunk in active-set order (PE_start first)
+        if (my_cnt > 0) {
+            std::vector<const void *> ins(P);
+            for (int i = 0; i < P; ++i) ins[i] = (i == m) ? src + m * cb : ws + i * cb;
+            fold_chain(type, op, tgt + m * cb, ins.data(), P, (size_t)my_cnt, s);
+        }
+        // 3. shard all-gather
+        SHMX_NCCL(ncclGroupStart());
+        for (int i = 0; i < P; ++i) {
+            if (i == m) continue;
+            const long long ci = count_of(n, p.chunk, i);
+            if (my_cnt > 0) SHMX_NCCL(ncclSend(tgt + m * cb, (size_t)my_cnt * sz, ncclUint8, peer(i), g_state.comm, s));
+            if (ci > 0) SHMX_NCCL(ncclRecv(tgt + i * cb, (size_t)ci * sz, ncclUint8, peer(i), g_state.comm, s));
+        }
+        SHMX_NCCL(ncclGroupEnd());
+        return SHMEMX_OK;
+    }
+
+    // GATHER: every source to every member, then the reference's own order on
+    // each PE: r = src_me; r = op(r, src_p) for p ascending, p != me.
+    SHMX_NCCL(ncclGroupStart());
+    for (int i = 0; i < P; ++i) {
+        if (i == m) continue;
+        SHMX_NCCL(ncclSend(src, bytes, ncclUint8, peer(i), g_state.comm, s));
+        SHMX_NCCL(ncclRecv(ws + (size_t)i * bytes, bytes, ncclUint8, peer(i), g_state.comm, s));
+    }
+    SHMX_NCCL(ncclGroupEnd());
+    {
+        std::vector<const void *> ins;
+        ins.reserve(P);
+        ins.push_back(src);
+        for (int i = 0; i < P; ++i)
+            if (i != m) ins.push_back(ws + (size_t)i * bytes);
+        fold_chain(type, op, tgt, ins.data(), P, (size_t)nreduce, s);
+    }
+    return SHMEMX_OK;
+}
+
+static bool device_accessible(const void *ptr) {
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, ptr) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
+}
+
+}  // namespace shmx
+
+// ------------------------------------------------------------- internal API
+// (used by entry.cpp; C++ linkage, not exported in the header)
+namespace shmx {
+
+// The blocking entry point body: host- or device-resident arrays.
+void reduce_blocking(int type, int op, void *target, const void *source,
+                     int nreduce, int start, int logstride, int size) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    t_last_error = SHMEMX_OK;
+    if (ensure_init()) {
+        trace("FATAL", "reduction called before shmem_init with npes > 1");
+        return;
+    }
+    if (!op_on_device(type, op)) {
+        if (op_valid(type, op))
+            trace("FATAL", "type %d op %d (long double) is not implemented on the device in this build", type, op);
+        set_error(op_valid(type, op) ? SHMEMX_ENOTSUP : SHMEMX_EINVAL);
+        return;
+    }
+    if (nreduce <= 0 || !target || !source) {
+        if (nreduce < 0 || ((!target || !source) && nreduce > 0)) set_error(SHMEMX_EINVAL);
+        else {  // n == 0: nothing moves, but validate membership like a call would
+            shmemx_plan_t p;
+            int rc = make_plan(type, op, 0, start, logstride, size, g_state.pe, g_state.npes,
+                               g_state.algo, &p);
+            if (rc) set_error(rc);
+        }
+        return;
+    }
+    const size_t bytes = type_size(type) * (size_t)nreduce;
+    const bool tdev = device_accessible(target), sdev = device_accessible(source);
+    hipStream_t s = g_state.stream;
+    if (tdev && sdev) {
+        reduce_device(type, op, target, source, nreduce, start, logstride, size, g_state.algo, s);
+        SHMX_HIP(hipStreamSynchronize(s));
+        return;
+    }
+    // Host-resident symmetric arrays (the reference's heap): stage over PCIe.
+    if (bytes > g_state.stage_bytes) {
+        SHMX_HIP(hipStreamSynchronize(s));
+        if (g_state.stage_src) SHMX_HIP(hipFree(g_state.stage_src));
+        if (g_state.stage_tgt) SHMX_HIP(hipFree(g_state.stage_tgt));
+        g_state.stage_src = g_state.stage_tgt = nullptr;
+        g_state.stage_bytes = 0;
+        if (hipMalloc(&g_state.stage_src, bytes) != hipSuccess ||
+            hipMalloc(&g_state.stage_tgt, bytes) != hipSuccess) {
+            (void)hipGetLastError();
+            set_error(SHMEMX_ENOMEM);
+            return;
+        }
+        g_state.stage_bytes = bytes;
+    }
+    const void *dsrc = source;
+    if (!sdev) {
+        SHMX_HIP(hipMemcpyAsync(g_state.stage_src, source, bytes, hipMemcpyHostToDevice, s));
+        dsrc = g_state.stage_src;
+    }
+    void *dtgt = tdev ? target : g_state.stage_tgt;
+    const int rc = reduce_device(type, op, dtgt, dsrc, nreduce, start, logstride, size,
+                                 g_state.algo, s);
+    if (!rc && !tdev)
+        SHMX_HIP(hipMemcpyAsync(target, dtgt, bytes, hipMemcpyDeviceToHost, s));
+    SHMX_HIP(hipStreamSynchronize(s));
+}
+
+int reduce_on_stream(int type, int op, void *target, const void *source,
+                     int nreduce, int start, int logstride, int size, int algo,
+                     void *stream) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    t_last_error = SHMEMX_OK;
+    if (int rc = ensure_init()) return rc;
+    if (nreduce > 0 && (!target || !source)) return set_error(SHMEMX_EINVAL);
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : g_state.stream;
+    return reduce_device(type, op, target, source, nreduce, start, logstride, size,
+                         algo == SHMEMX_ALGO_AUTO ? g_state.algo : algo, s);
+}
+
+}  // namespace shmx
+
+// ------------------------------------------------------------------ C ABI
+
+using namespace shmx;
+
+extern "C" {
+
+void pshmem_init(void) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    if (g_state.inited) return;
+    const int npes = env_int("SHMEM_NPES", "WORLD_SIZE", 1);
+    const int pe = npes > 1 ? env_int("SHMEM_PE", "RANK", 0) : 0;
+    const int dev = npes > 1 ? env_int("LOCAL_RANK", nullptr, -1) : -1;
+    if (npes < 1 || pe < 0 || pe >= npes) {
+        char why[128];
+        snprintf(why, sizeof why, "bad PE identity from the environment: pe %d of %d", pe, npes);
+        fatal("shmem_init", why);
+    }
+    const int rc = npes > 1 ? file_bootstrap(pe, npes, dev) : init_locked(0, 1, dev, nullptr);
+    if (rc) fatal("shmem_init", shmemx_reduce_error_string(rc));
+}
+
+void pshmem_finalize(void) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    if (!g_state.inited) return;
+    (void)hipStreamSynchronize(g_state.stream);
+    if (g_state.comm) {
+        ncclCommDestroy(g_state.comm);
+        g_state.comm = nullptr;
+    }
+    for (void **b : {&g_state.ws, &g_state.tmp, &g_state.stage_src, &g_state.stage_tgt}) {
+        if (*b) (void)hipFree(*b);
+        *b = nullptr;
+    }
+    g_state.ws_bytes = g_state.tmp_bytes = g_state.stage_bytes = 0;
+    (void)hipStreamDestroy(g_state.stream);
+    g_state.stream = nullptr;
+    g_state.inited = false;
+}
+
+int pshmem_my_pe(void) { return g_state.pe; }
+int pshmem_n_pes(void) { return g_state.npes; }
+
+void shmem_init(void) __attribute__((weak, alias("pshmem_init")));
+void shmem_finalize(void) __attribute__((weak, alias("pshmem_finalize")));
+int shmem_my_pe(void) __attribute__((weak, alias("pshmem_my_pe")));
+int shmem_n_pes(void) __attribute__((weak, alias("pshmem_n_pes")));
+
+int shmemx_uniqueid_size(void) { return (int)sizeof(ncclUniqueId); }
+
+int shmemx_get_uniqueid(void *uid_out) {
+    if (!uid_out) return set_error(SHMEMX_EINVAL);
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return set_error(SHMEMX_EDEVICE);
+    std::memcpy(uid_out, &id, sizeof id);
+    return SHMEMX_OK;
+}
+
+int shmemx_init_attr(int pe, int npes, int device, const void *uid) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    return init_locked(pe, npes, device, uid);
+}
+
+int shmemx_initialized(void) { return g_state.inited ? 1 : 0; }
+
+void *shmemx_get_stream(void) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    if (ensure_init()) return nullptr;
+    return g_state.stream;
+}
+
+int shmemx_set_algo(int algo) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    const int prev = g_state.algo;
+    if (algo >= 0 && algo < SHMEMX_NALGOS) g_state.algo = algo;
+    return prev;
+}
+
+int shmemx_reduce_on_stream(int type, int op, void *target, const void *source,
+                            int nreduce, int PE_start, int logPE_stride,
+                            int PE_size, int algo, void *stream) {
+    return reduce_on_stream(type, op, target, source, nreduce, PE_start,
+                            logPE_stride, PE_size, algo, stream);
+}
+
+int shmemx_fold_on_stream(int type, int op, void *acc, const void *in,
+                          size_t nelems, void *stream) {
+    t_last_error = SHMEMX_OK;
+    if (!op_on_device(type, op)) return set_error(op_valid(type, op) ? SHMEMX_ENOTSUP : SHMEMX_EINVAL);
+    if (nelems == 0) return SHMEMX_OK;
+    if (!acc || !in) return set_error(SHMEMX_EINVAL);
+    const void *ins[2] = {acc, in};
+    if (launch_fold(type, op, acc, ins, 2, nelems, static_cast<hipStream_t>(stream)) != hipSuccess)
+        return set_error(SHMEMX_EDEVICE);
+    return SHMEMX_OK;
+}
+
+int shmemx_fold_n_on_stream(int type, int op, void *out, const void *const *ins,
+                            int nins, size_t nelems, void *stream) {
+    t_last_error = SHMEMX_OK;
+    if (!op_on_device(type, op)) return set_error(op_valid(type, op) ? SHMEMX_ENOTSUP : SHMEMX_EINVAL);
+    if (nins < 1 || !ins) return set_error(SHMEMX_EINVAL);
+    if (nelems == 0) return SHMEMX_OK;
+    if (!out) return set_error(SHMEMX_EINVAL);
+    for (int k = 0; k < nins; ++k)
+        if (!ins[k]) return set_error(SHMEMX_EINVAL);
+    int done = std::min(nins, kMaxFoldInputs);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (launch_fold(type, op, out, ins, done, nelems, s) != hipSuccess) return set_error(SHMEMX_EDEVICE);
+    while (done < nins) {
+        const void *grp[kMaxFoldInputs];
+        grp[0] = out;
+        int k = 1;
+        while (k < kMaxFoldInputs && done < nins) grp[k++] = ins[done++];
+        if (launch_fold(type, op, out, grp, k, nelems, s) != hipSuccess) return set_error(SHMEMX_EDEVICE);
+    }
+    return SHMEMX_OK;
+}
+
+int shmemx_reduce_plan(int type, int op, int nreduce, int PE_start,
+                       int logPE_stride, int PE_size, int pe, int npes,
+                       int algo, shmemx_plan_t *plan) {
+    if (!plan) return SHMEMX_EINVAL;
+    return make_plan(type, op, nreduce, PE_start, logPE_stride, PE_size, pe, npes, algo, plan);
+}
+
+size_t shmemx_type_size(int type) { return type_size(type); }
+int shmemx_op_valid(int type, int op) { return op_valid(type, op) ? 1 : 0; }
+int shmemx_op_on_device(int type, int op) { return op_on_device(type, op) ? 1 : 0; }
+int shmemx_reduce_last_error(void) { return t_last_error; }
+
+const char *shmemx_reduce_error_string(int err) {
+    switch (err) {
+    case SHMEMX_OK: return "success";
+    case SHMEMX_EINVAL: return "invalid argument";
+    case SHMEMX_ENOTMEMBER: return "calling PE is not in the active set";
+    case SHMEMX_ENOTSUP: return "type/op/algorithm not supported";
+    case SHMEMX_ENOINIT: return "runtime not initialised (npes > 1 needs shmem_init)";
+    case SHMEMX_ENOMEM: return "device workspace allocation failed";
+    case SHMEMX_EDEVICE: return "HIP or RCCL error";
+    default: return "unknown error";
+    }
+}
+
+}  // extern "C"

@@ -1,0 +1,247 @@
+"""Python view of libshmem_reduce_mi355x.so (ctypes, no torch types in the ABI).
+
+The product is the C ABI in ``include/shmem_reduce_mi355x.h``; this module is
+the thin host-side mirror used by the tests and ``bench.py``.  It keeps the
+reference's names and argument meaning: ``to_all("double", "sum", target,
+source, nreduce, PE_start, logPE_stride, PE_size, pWrk, pSync)`` calls the C
+entry point ``shmem_double_sum_to_all`` (reference src/reduce/reduce-op.c:
+372-431, prototype src/shmem.h:1412-1648) with raw pointers.
+
+Array arguments may be torch tensors (device or host), numpy arrays, or plain
+integer addresses.  Loading fails loudly when the shared library has not been
+built: there is no Python or CPU fallback for any reduction.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "libshmem_reduce_mi355x.so")
+
+# SHMEMX_TYPE_* / SHMEMX_OP_* / SHMEMX_ALGO_* of the header.
+TYPES = {"short": 0, "int": 1, "long": 2, "longlong": 3, "float": 4,
+         "double": 5, "longdouble": 6, "complexd": 7, "complexf": 8}
+OPS = {"sum": 0, "prod": 1, "and": 2, "or": 3, "xor": 4, "min": 5, "max": 6}
+ALGOS = {"auto": 0, "rccl": 1, "a2a": 2, "gather": 3}
+ERRORS = {0: "OK", 1: "EINVAL", 2: "ENOTMEMBER", 3: "ENOTSUP", 4: "ENOINIT",
+          5: "ENOMEM", 6: "EDEVICE"}
+
+# Which (type, op) pairs the reference exports (reduce-op.c:388-431).
+REFERENCE_PAIRS = [(t, o) for t in TYPES for o in ("sum", "prod")] + \
+    [(t, o) for t in ("short", "int", "long", "longlong") for o in ("and", "or", "xor")] + \
+    [(t, o) for t in ("short", "int", "long", "longlong", "float", "double", "longdouble")
+     for o in ("max", "min")]
+
+
+class ShmemError(RuntimeError):
+    """A shmemx_* call returned an error code."""
+
+    def __init__(self, code: int, what: str):
+        super().__init__(f"{what}: {ERRORS.get(code, code)}")
+        self.code = code
+
+
+class Plan(ctypes.Structure):
+    _fields_ = [("algo", ctypes.c_int), ("member", ctypes.c_int),
+                ("nmembers", ctypes.c_int), ("elem_size", ctypes.c_int),
+                ("chunk", ctypes.c_longlong), ("main", ctypes.c_longlong),
+                ("tail", ctypes.c_longlong), ("ws_bytes", ctypes.c_longlong)]
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load the shared library (once).  Raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} is not built; run `make -C openshmem-async_amd` "
+            "(or __graft_entry__.build()) — there is no fallback path")
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so.7
+    # and loads it by path.  Import torch first (when present) so that the
+    # library's DT_NEEDED libamdhip64.so.7 / librccl.so.1 bind to the copies
+    # already loaded; loading ours first would put two HIP runtimes in the
+    # process and the second sees no device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i, sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+    L.shmemx_reduce_on_stream.argtypes = [i, i, vp, vp, i, i, i, i, i, vp]
+    L.shmemx_reduce_on_stream.restype = i
+    L.shmemx_fold_on_stream.argtypes = [i, i, vp, vp, sz, vp]
+    L.shmemx_fold_on_stream.restype = i
+    L.shmemx_fold_n_on_stream.argtypes = [i, i, vp, ctypes.POINTER(vp), i, sz, vp]
+    L.shmemx_fold_n_on_stream.restype = i
+    L.shmemx_reduce_plan.argtypes = [i, i, i, i, i, i, i, i, i, ctypes.POINTER(Plan)]
+    L.shmemx_reduce_plan.restype = i
+    L.shmemx_get_uniqueid.argtypes = [vp]
+    L.shmemx_get_uniqueid.restype = i
+    L.shmemx_uniqueid_size.restype = i
+    L.shmemx_init_attr.argtypes = [i, i, i, vp]
+    L.shmemx_init_attr.restype = i
+    L.shmemx_get_stream.restype = vp
+    L.shmemx_set_algo.argtypes = [i]
+    L.shmemx_set_algo.restype = i
+    L.shmemx_type_size.argtypes = [i]
+    L.shmemx_type_size.restype = sz
+    L.shmemx_op_valid.argtypes = [i, i]
+    L.shmemx_op_on_device.argtypes = [i, i]
+    L.shmemx_reduce_last_error.restype = i
+    L.shmemx_reduce_error_string.argtypes = [i]
+    L.shmemx_reduce_error_string.restype = ctypes.c_char_p
+    for t, o in REFERENCE_PAIRS:
+        for prefix in ("shmem", "pshmem"):
+            f = getattr(L, f"{prefix}_{t}_{o}_to_all")
+            f.argtypes = [vp, vp, i, i, i, i, vp, vp]
+            f.restype = None
+    _lib = L
+    return L
+
+
+def addr(x) -> int | None:
+    """Raw address of a torch tensor, numpy array, ctypes object or int."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if hasattr(x, "ctypes"):
+        return x.ctypes.data
+    return ctypes.addressof(x)
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise ShmemError(rc, what)
+
+
+# ------------------------------------------------------------------ runtime
+def init_attr(pe: int, npes: int, device: int = -1, uid: bytes | None = None) -> None:
+    buf = None
+    if uid is not None:
+        buf = ctypes.create_string_buffer(bytes(uid), len(uid))
+    _check(lib().shmemx_init_attr(pe, npes, device, buf), "shmemx_init_attr")
+
+
+def get_uniqueid() -> bytes:
+    n = lib().shmemx_uniqueid_size()
+    buf = ctypes.create_string_buffer(n)
+    _check(lib().shmemx_get_uniqueid(buf), "shmemx_get_uniqueid")
+    return buf.raw
+
+
+def init_from_torch_distributed(device: int = -1) -> None:
+    """Bootstrap every rank of an initialised torch.distributed group (gloo is
+    enough: it only carries the 128-byte RCCL id)."""
+    import torch
+    import torch.distributed as dist
+    rank, world = dist.get_rank(), dist.get_world_size()
+    if world == 1:
+        init_attr(0, 1, device, None)
+        return
+    n = lib().shmemx_uniqueid_size()
+    t = torch.zeros(n, dtype=torch.uint8)
+    if rank == 0:
+        t.copy_(torch.frombuffer(bytearray(get_uniqueid()), dtype=torch.uint8))
+    dist.broadcast(t, src=0)
+    init_attr(rank, world, device, bytes(t.numpy().tobytes()))
+
+
+def init() -> None:
+    lib().shmem_init()
+
+
+def finalize() -> None:
+    lib().shmem_finalize()
+
+
+def my_pe() -> int:
+    return lib().shmem_my_pe()
+
+
+def n_pes() -> int:
+    return lib().shmem_n_pes()
+
+
+def get_stream() -> int:
+    return lib().shmemx_get_stream() or 0
+
+
+def set_algo(name: str) -> str:
+    prev = lib().shmemx_set_algo(ALGOS[name])
+    return {v: k for k, v in ALGOS.items()}[prev]
+
+
+def last_error() -> int:
+    return lib().shmemx_reduce_last_error()
+
+
+# --------------------------------------------------------------- reductions
+def to_all(type_name: str, op: str, target, source, nreduce: int, PE_start: int,
+           logPE_stride: int, PE_size: int, pWrk=None, pSync=None) -> None:
+    """shmem_<type>_<op>_to_all, blocking (reference reduce-op.c:372-386)."""
+    f = getattr(lib(), f"shmem_{type_name}_{op}_to_all")
+    f(addr(target), addr(source), nreduce, PE_start, logPE_stride, PE_size,
+      addr(pWrk), addr(pSync))
+
+
+def reduce_on_stream(type_name: str, op: str, target, source, nreduce: int,
+                     PE_start: int = 0, logPE_stride: int = 0, PE_size: int = 1,
+                     algo: str = "auto", stream: int = 0) -> None:
+    rc = lib().shmemx_reduce_on_stream(TYPES[type_name], OPS[op], addr(target), addr(source),
+                                       nreduce, PE_start, logPE_stride, PE_size,
+                                       ALGOS[algo], stream or None)
+    _check(rc, f"shmemx_reduce_on_stream({type_name},{op})")
+
+
+def fold(type_name: str, op: str, acc, inp, nelems: int, stream: int = 0) -> None:
+    """acc[i] = op(acc[i], inp[i]) on the GPU (reduce-op.c:231-235)."""
+    rc = lib().shmemx_fold_on_stream(TYPES[type_name], OPS[op], addr(acc), addr(inp),
+                                     nelems, stream or None)
+    _check(rc, f"shmemx_fold_on_stream({type_name},{op})")
+
+
+def fold_n(type_name: str, op: str, out, ins, nelems: int, stream: int = 0) -> None:
+    arr = (ctypes.c_void_p * len(ins))(*[addr(x) for x in ins])
+    rc = lib().shmemx_fold_n_on_stream(TYPES[type_name], OPS[op], addr(out), arr, len(ins),
+                                       nelems, stream or None)
+    _check(rc, f"shmemx_fold_n_on_stream({type_name},{op})")
+
+
+@dataclass
+class PlanInfo:
+    algo: str
+    member: int
+    nmembers: int
+    elem_size: int
+    chunk: int
+    main: int
+    tail: int
+    ws_bytes: int
+
+
+def plan(type_name: str, op: str, nreduce: int, PE_start: int, logPE_stride: int,
+         PE_size: int, pe: int, npes: int, algo: str = "auto") -> PlanInfo:
+    p = Plan()
+    rc = lib().shmemx_reduce_plan(TYPES[type_name], OPS[op], nreduce, PE_start, logPE_stride,
+                                  PE_size, pe, npes, ALGOS[algo], ctypes.byref(p))
+    _check(rc, "shmemx_reduce_plan")
+    inv = {v: k for k, v in ALGOS.items()}
+    return PlanInfo(inv[p.algo], p.member, p.nmembers, p.elem_size, p.chunk, p.main,
+                    p.tail, p.ws_bytes)
+
+
+def type_size(type_name: str) -> int:
+    return lib().shmemx_type_size(TYPES[type_name])
+
+
+def op_on_device(type_name: str, op: str) -> bool:
+    return bool(lib().shmemx_op_on_device(TYPES[type_name], OPS[op]))

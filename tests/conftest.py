@@ -1,0 +1,51 @@
+"""Shared test setup.
+
+* registers the `gpu` marker (tests that need an MI355X; the CPU suite runs
+  with -m "not gpu");
+* puts the product's Python mirror (openshmem-async_amd/shmem_mi355x) and the
+  test-only oracle (oracle/oracle.py) on sys.path.
+"""
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "openshmem-async_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu)")
+
+
+def gpu_count() -> int:
+    try:
+        import torch
+        return torch.cuda.device_count() if torch.cuda.is_available() else 0
+    except Exception:
+        return 0
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import oracle as O
+    O.lib()
+    return O
+
+
+@pytest.fixture(scope="session")
+def shm():
+    """The product library (must be built; fails loudly otherwise)."""
+    import shmem_mi355x as S
+    S.lib()
+    return S
+
+
+@pytest.fixture(scope="session")
+def cuda(shm):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test run without a visible GPU")
+    torch.cuda.set_device(0)
+    return torch.device("cuda:0")

@@ -1,0 +1,104 @@
+"""GPU tests of the drop-in entry points (shmem_<T>_<op>_to_all) at one PE.
+
+On one PE the reference's call is `write_to = source` plus two barriers
+(reduce-op.c:213-217,250): target must equal source, for device- and
+host-resident arrays (the reference's symmetric heap is host memory,
+memory/symmem.c:168-227), in place or not, and pWrk/pSync are left alone.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_runtime_single_pe(cuda, shm):
+    shm.init()
+    assert shm.my_pe() == 0 and shm.n_pes() == 1
+    assert shm.get_stream() != 0
+
+
+@pytest.mark.parametrize("t", ["short", "int", "long", "longlong", "float", "double",
+                               "complexd", "complexf"])
+def test_api_pe1_device_copy(cuda, shm, oracle, t):
+    import torch
+    n = 4103
+    src = oracle.fill(t, 1, 77, n)
+    want = oracle.reduce_sim(t, "sum", src[None, :], 0, 0, 1)[0]
+    s = torch.from_numpy(src).cuda()
+    d = torch.zeros_like(s)
+    psync = np.full(128, -1, dtype=np.int64)
+    pwrk = np.zeros(64, dtype=src.dtype)
+    shm.to_all(t, "sum", d, s, n, 0, 0, 1, pwrk, psync)
+    assert shm.last_error() == 0
+    assert d.cpu().numpy().tobytes() == want.tobytes()
+    assert (psync == -1).all()
+
+
+@pytest.mark.parametrize("t,op", [("double", "sum"), ("int", "and"), ("float", "max"),
+                                  ("long", "xor")])
+def test_api_pe1_host_arrays(cuda, shm, oracle, t, op):
+    """Host-resident symmetric arrays go H2D -> device path -> D2H."""
+    n = 100003
+    src = oracle.fill(t, 1, 99, n)
+    tgt = np.zeros_like(src)
+    psync = np.full(128, -1, dtype=np.int64)
+    shm.to_all(t, op, tgt, src, n, 0, 0, 1, None, psync)
+    assert shm.last_error() == 0
+    assert tgt.tobytes() == src.tobytes()
+    # in place on host memory
+    src2 = src.copy()
+    shm.to_all(t, op, src2, src2, n, 0, 0, 1, None, psync)
+    assert src2.tobytes() == src.tobytes()
+    assert (psync == -1).all()
+
+
+def test_api_pe1_in_place_and_overlap_device(cuda, shm, oracle):
+    import torch
+    n = 70001
+    src = oracle.fill("double", 1, 5, n + 10)
+    buf = torch.from_numpy(src).cuda()
+    shm.to_all("double", "sum", buf, buf, n, 0, 0, 1)   # in place
+    assert buf.cpu().numpy().tobytes() == src.tobytes()
+    # partial overlap: target = source + 3 elements (reference's temp path)
+    shm.to_all("double", "sum", buf[3:], buf, n, 0, 0, 1)
+    got = buf.cpu().numpy()
+    assert got[3:3 + n].tobytes() == src[:n].tobytes()
+    assert got[:3].tobytes() == src[:3].tobytes()
+
+
+def test_api_zero_and_invalid(cuda, shm):
+    import torch
+    d = torch.full((16,), 7.0, dtype=torch.float64, device="cuda")
+    s = torch.ones(16, dtype=torch.float64, device="cuda")
+    shm.to_all("double", "sum", d, s, 0, 0, 0, 1)            # n == 0: no effect
+    assert shm.last_error() == 0 and (d == 7.0).all()
+    shm.to_all("double", "sum", d, s, -1, 0, 0, 1)           # n < 0 (reference: UB)
+    assert shm.last_error() == 1 and (d == 7.0).all()
+    shm.to_all("double", "sum", d, s, 16, 1, 0, 1)           # set {1} beyond npes
+    assert shm.last_error() == 1 and (d == 7.0).all()
+    shm.to_all("double", "sum", d, s, 16, 0, 0, 2)           # set beyond npes
+    assert shm.last_error() == 1 and (d == 7.0).all()
+
+
+def test_longdouble_is_loud(cuda, shm):
+    """long double has no device kernel in this build: the call must fail
+    visibly (error code + FATAL line), never silently fall back to the CPU."""
+    src = (ctypes.c_longdouble * 4)(1, 2, 3, 4)
+    tgt = (ctypes.c_longdouble * 4)()
+    shm.to_all("longdouble", "sum", ctypes.addressof(tgt), ctypes.addressof(src), 4, 0, 0, 1)
+    assert shm.last_error() == 3
+    assert list(tgt) == [0, 0, 0, 0]
+
+
+def test_reduce_on_stream_torch_stream(cuda, shm, oracle):
+    import torch
+    n = 1 << 20
+    src = oracle.fill("float", 1, 3, n)
+    s = torch.from_numpy(src).cuda()
+    d = torch.zeros_like(s)
+    st = torch.cuda.Stream()
+    shm.reduce_on_stream("float", "sum", d, s, n, 0, 0, 1, "auto", st.cuda_stream)
+    st.synchronize()
+    assert d.cpu().numpy().tobytes() == src.tobytes()

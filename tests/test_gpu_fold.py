@@ -1,0 +1,199 @@
+"""GPU parity of the fold kernels against the oracle (through the C ABI).
+
+The fold kernel is the arithmetic of the whole path: every PE's result in the
+reference is a left fold of the active set's sources (reduce-op.c:213-248).
+On the GPU the multi-PE exchange only moves bytes (RCCL), so a fold of P
+sources in a given order on one GPU must equal the oracle's output of the PE
+whose order that is:
+  * order 0..P-1            -> the reference's PE_start (A2A path, all PEs)
+  * order me, others asc.   -> the reference's PE `me`  (GATHER path)
+Bit-exact for every type/op (floats included: same op order, same IEEE ops).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+DEVICE_PAIRS = [
+    ("short", o) for o in ("sum", "prod", "and", "or", "xor", "min", "max")] + [
+    ("int", o) for o in ("sum", "prod", "and", "or", "xor", "min", "max")] + [
+    ("long", o) for o in ("sum", "prod", "and", "or", "xor", "min", "max")] + [
+    ("longlong", o) for o in ("sum", "prod", "and", "or", "xor", "min", "max")] + [
+    ("float", o) for o in ("sum", "prod", "min", "max")] + [
+    ("double", o) for o in ("sum", "prod", "min", "max")] + [
+    ("complexd", "sum"), ("complexd", "prod"), ("complexf", "sum"), ("complexf", "prod")]
+
+SIZES = [1, 2, 63, 64, 65, 127, 1000, 4103, 65536 + 13]
+
+
+def to_dev(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def same_bits(a: np.ndarray, b: np.ndarray) -> bool:
+    return a.dtype == b.dtype and a.shape == b.shape and a.tobytes() == b.tobytes()
+
+
+@pytest.mark.parametrize("t,op", DEVICE_PAIRS)
+def test_fold_pe_start_order_matches_oracle(cuda, shm, oracle, t, op):
+    import torch
+    for kind in (0, 1):
+        for P in (1, 2, 3, 5, 8):
+            for n in (SIZES if P in (2, 5) else SIZES[:7]):
+                srcs = oracle.sources(t, kind, P, n, base_seed=0x5EED0000 + 97 * P + n)
+                want = oracle.reduce_sim(t, op, srcs, 0, 0, P)[0]
+                ins = [to_dev(torch, srcs[p]) for p in range(P)]
+                out = torch.empty_like(ins[0])
+                shm.fold_n(t, op, out, ins, n)
+                torch.cuda.synchronize()
+                got = out.cpu().numpy()
+                assert same_bits(got, want), f"{t} {op} kind={kind} P={P} n={n}"
+
+
+@pytest.mark.parametrize("t,op", [("double", "sum"), ("double", "prod"), ("float", "sum"),
+                                  ("float", "prod"), ("double", "min"), ("complexd", "prod"),
+                                  ("complexf", "sum")])
+def test_fold_gather_order_every_pe(cuda, shm, oracle, t, op):
+    """GATHER algorithm order (me first, then ascending) == reference PE me."""
+    import torch
+    P, n = 5, 4103
+    srcs = oracle.sources(t, 1, P, n)
+    want = oracle.reduce_sim(t, op, srcs, 0, 0, P)
+    dev = [to_dev(torch, srcs[p]) for p in range(P)]
+    for me in range(P):
+        order = [me] + [p for p in range(P) if p != me]
+        out = torch.empty_like(dev[0])
+        shm.fold_n(t, op, out, [dev[p] for p in order], n)
+        torch.cuda.synchronize()
+        assert same_bits(out.cpu().numpy(), want[me]), f"PE {me}"
+
+
+@pytest.mark.parametrize("t,op", [("double", "sum"), ("int", "xor"), ("short", "max"),
+                                  ("float", "min"), ("complexf", "prod")])
+def test_fold_in_place_acc(cuda, shm, oracle, t, op):
+    """shmemx_fold: acc = op(acc, in), the inner loop reduce-op.c:231-235."""
+    import torch
+    n = 10007
+    srcs = oracle.sources(t, 1, 2, n)
+    want = oracle.reduce_sim(t, op, srcs, 0, 0, 2)[0]
+    acc, inp = to_dev(torch, srcs[0]), to_dev(torch, srcs[1])
+    shm.fold(t, op, acc, inp, n)
+    torch.cuda.synchronize()
+    assert same_bits(acc.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("t", ["double", "int", "short", "complexf"])
+def test_fold_misaligned_and_mixed_alignment(cuda, shm, oracle, t):
+    """Head/tail peeling (same offset mod 16) and the all-scalar path
+    (inputs at different offsets mod 16), as 8-byte dlmalloc pointers give."""
+    import torch
+    P, n = 3, 5003
+    srcs = oracle.sources(t, 1, P, n + 8)
+    isz = srcs.itemsize
+    for offs in ([1, 1, 1, 1], [0, 1, 2, 3], [3, 0, 1, 1], [1, 0, 0, 0]):
+        if 16 // isz <= 1 and any(offs):
+            continue
+        want = oracle.reduce_sim(t, "sum", np.stack([srcs[p][offs[p + 1]:offs[p + 1] + n]
+                                                     for p in range(P)]), 0, 0, P)[0]
+        dev = [to_dev(torch, srcs[p]) for p in range(P)]
+        outbuf = torch.zeros(n + 8, dtype=dev[0].dtype, device="cuda")
+        out = outbuf[offs[0]:offs[0] + n]
+        ins = [dev[p][offs[p + 1]:offs[p + 1] + n] for p in range(P)]
+        shm.fold_n(t, "sum", out, ins, n)
+        torch.cuda.synchronize()
+        got = outbuf.cpu().numpy()
+        assert same_bits(got[offs[0]:offs[0] + n], want), f"offs={offs}"
+        assert not got[:offs[0]].any() and not got[offs[0] + n:].any(), "wrote outside"
+
+
+def test_fold_long_chain_beyond_16_inputs(cuda, shm, oracle):
+    """More inputs than one launch takes: chained launches keep the order."""
+    import torch
+    P, n = 37, 999
+    srcs = oracle.sources("double", 1, P, n)
+    want = oracle.reduce_sim("double", "sum", srcs, 0, 0, P)[0]
+    dev = [to_dev(torch, srcs[p]) for p in range(P)]
+    out = torch.empty_like(dev[0])
+    shm.fold_n("double", "sum", out, dev, n)
+    torch.cuda.synchronize()
+    assert same_bits(out.cpu().numpy(), want)
+
+
+def _special(t):
+    if t in ("float", "double"):
+        ft = np.float32 if t == "float" else np.float64
+        tiny = np.finfo(ft).tiny
+        vals = [np.nan, -np.nan, 0.0, -0.0, np.inf, -np.inf, 1.0, -1.0,
+                tiny, -tiny, tiny / 4, np.finfo(ft).max, -np.finfo(ft).max, 2.5]
+        return np.array(vals, dtype=ft)
+    info = np.iinfo({"short": np.int16, "int": np.int32, "long": np.int64}[t])
+    return np.array([info.min, info.max, 0, -1, 1, info.min + 1, info.max - 1, 12345],
+                    dtype=info.dtype)
+
+
+@pytest.mark.parametrize("t", ["float", "double", "short", "int", "long"])
+def test_fold_special_values_all_pairs(cuda, shm, oracle, t):
+    """NaN / +-0 / inf / subnormals / integer wrap, every ordered pair, every op.
+    min/max are selects: bit-exact even for NaN payloads and signed zeros.
+    sum/prod: bit-exact except NaN results, which must be NaN on both sides
+    (the NaN payload an add produces is not specified by IEEE 754)."""
+    import torch
+    v = _special(t)
+    a = np.repeat(v, len(v))
+    b = np.tile(v, len(v))
+    srcs = np.stack([a, b])
+    ops = ["sum", "prod", "min", "max"] + ([] if t in ("float", "double") else ["and", "or", "xor"])
+    for op in ops:
+        for order in ((0, 1), (1, 0)):
+            want = oracle.reduce_sim(t, op, srcs[list(order)], 0, 0, 2)[0]
+            out = torch.empty(len(a), dtype=to_dev(torch, a).dtype, device="cuda")
+            shm.fold_n(t, op, out, [to_dev(torch, srcs[order[0]]), to_dev(torch, srcs[order[1]])],
+                       len(a))
+            torch.cuda.synchronize()
+            got = out.cpu().numpy()
+            if t in ("float", "double") and op in ("sum", "prod"):
+                nan_w, nan_g = np.isnan(want), np.isnan(got)
+                assert np.array_equal(nan_w, nan_g), op
+                assert same_bits(got[~nan_g], want[~nan_w]), op
+            else:
+                assert same_bits(got, want), (op, order)
+
+
+@pytest.mark.parametrize("t", ["complexd", "complexf"])
+def test_complex_prod_annex_g(cuda, shm, oracle, t):
+    """Complex multiply with inf/NaN parts: the __muldc3 recovery branch."""
+    import torch
+    ft = np.float64 if t == "complexd" else np.float32
+    parts = np.array([0.0, -0.0, 1.0, -2.0, np.inf, -np.inf, np.nan, 3.5], dtype=ft)
+    zs = np.array([complex(x, y) for x in parts for y in parts],
+                  dtype=np.complex128 if t == "complexd" else np.complex64)
+    a, b = np.repeat(zs, len(zs)), np.tile(zs, len(zs))
+    want = oracle.reduce_sim(t, "prod", np.stack([a, b]), 0, 0, 2)[0]
+    out = torch.empty(len(a), dtype=to_dev(torch, a).dtype, device="cuda")
+    shm.fold_n(t, "prod", out, [to_dev(torch, a), to_dev(torch, b)], len(a))
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    for comp in ("real", "imag"):
+        g, w = getattr(got, comp), getattr(want, comp)
+        assert np.array_equal(np.isnan(g), np.isnan(w)), comp
+        m = ~np.isnan(w)
+        assert g[m].tobytes() == w[m].tobytes(), comp
+
+
+def test_fold_full_size_double_sum(cuda, shm, oracle):
+    """BASELINE configs[1] size (32 Mi doubles): acc += in must equal the
+    oracle's 2-PE PE_start result; checked exactly against numpy's a+b (one
+    IEEE add per element, the identical operation) and on a sampled window
+    against the oracle itself."""
+    import torch
+    n = 32 * 1024 * 1024
+    a = oracle.fill("double", 0, 0x5EED0000, n)
+    b = oracle.fill("double", 0, 0x5EED0001, n)
+    acc, inp = to_dev(torch, a), to_dev(torch, b)
+    shm.fold("double", "sum", acc, inp, n)
+    torch.cuda.synchronize()
+    got = acc.cpu().numpy()
+    assert same_bits(got, a + b)
+    lo = n // 2 - 4099
+    win = oracle.reduce_sim("double", "sum", np.stack([a[lo:lo + 8192], b[lo:lo + 8192]]), 0, 0, 2)[0]
+    assert same_bits(got[lo:lo + 8192], win)
