@@ -184,6 +184,13 @@ int shmemx_fold_n_on_stream(int type, int op, void *out,
                             const void *const *ins, int nins, size_t nelems,
                             void *stream);
 
+/* Fold-kernel launch shape (defaults from $SHMEMX_FOLD_MAX_BLOCKS,
+ * $SHMEMX_FOLD_NT, $SHMEMX_FOLD_UNROLL): grid cap (0 = no cap), non-temporal
+ * mode (-1 = by size, the default: both non-temporal once the arrays exceed
+ * the 256 MiB Infinity Cache; else bit 0 loads, bit 1 stores), 16-byte
+ * vectors per lane per input of the 2-input fold (2, 4 or 8; default 4). */
+int shmemx_fold_set_tuning(int max_blocks, int nontemporal, int unroll);
+
 /* How a call would be executed (pure host logic, no device needed). */
 typedef struct {
     int algo;          /* resolved SHMEMX_ALGO_* (never AUTO)               */

@@ -149,14 +149,15 @@ SHMX_CPLX_OPS(cplxf, float)
 #undef SHMX_CPLX_OPS
 
 // ------------------------------------------------------- vector plumbing
-template <bool NT>
+// NT: bit 0 = non-temporal loads, bit 1 = non-temporal stores.
+template <int NT>
 __device__ __forceinline__ u32x4 ld16(const u32x4 *p) {
-    if constexpr (NT) return __builtin_nontemporal_load(p);
+    if constexpr ((NT & 1) != 0) return __builtin_nontemporal_load(p);
     else return *p;
 }
-template <bool NT>
+template <int NT>
 __device__ __forceinline__ void st16(u32x4 *p, u32x4 v) {
-    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    if constexpr ((NT & 2) != 0) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
 
@@ -185,7 +186,7 @@ constexpr int kBlock = 256;  // 4 waves of 64
 
 // NIN > 0: number of inputs fixed at compile time (all loads hoisted);
 // NIN == 0: runtime args.nins.
-template <typename T, int OP, int NIN, int UNROLL, bool NT>
+template <typename T, int OP, int NIN, int UNROLL, int NT>
 __global__ __launch_bounds__(kBlock) void fold_kernel(FoldArgs args) {
     constexpr int E = 16 / sizeof(T);
     const int nins = NIN > 0 ? NIN : args.nins;
@@ -265,16 +266,14 @@ __global__ __launch_bounds__(kBlock) void fold_kernel(FoldArgs args) {
     }
 }
 
-// Vectors per lane per input, by element size: keeps ~64 B per lane per input
-// in flight for every type.
-constexpr int kUnroll = 4;
+// 16-B vectors per lane per input for the runtime-nins kernel.
+constexpr int kUnrollN = 4;
 
-template <typename T, int OP, bool NT>
-hipError_t launch_typed(const FoldArgs &a, hipStream_t stream) {
+static size_t grid_for(const FoldArgs &a, int unroll) {
     const FoldTuning &tune = fold_tuning();
     size_t work_blocks;
     if (a.nvec > 0)
-        work_blocks = (a.nvec + (size_t)kBlock * kUnroll - 1) / ((size_t)kBlock * kUnroll);
+        work_blocks = (a.nvec + (size_t)kBlock * unroll - 1) / ((size_t)kBlock * unroll);
     else
         work_blocks = (a.head + a.tail + kBlock - 1) / kBlock;
     // The scalar-only case (inputs of different alignment) is capped hard; the
@@ -284,19 +283,47 @@ hipError_t launch_typed(const FoldArgs &a, hipStream_t stream) {
     size_t blocks = work_blocks < cap ? work_blocks : cap;
     if (blocks < 1) blocks = 1;
     if (blocks > (size_t)INT_MAX) blocks = INT_MAX;
-    if (a.nins == 2)
-        hipLaunchKernelGGL((fold_kernel<T, OP, 2, kUnroll, NT>), dim3((unsigned)blocks),
+    return blocks;
+}
+
+template <typename T, int OP, int NT>
+hipError_t launch_typed(const FoldArgs &a, hipStream_t stream) {
+    if (a.nins == 2) {
+        // the two-input fold (reduce-op.c:231-235): the hot kernel
+        const int u = fold_tuning().unroll;
+        const dim3 grid((unsigned)grid_for(a, u));
+        if (u == 2)
+            hipLaunchKernelGGL((fold_kernel<T, OP, 2, 2, NT>), grid, dim3(kBlock), 0, stream, a);
+        else if (u == 8)
+            hipLaunchKernelGGL((fold_kernel<T, OP, 2, 8, NT>), grid, dim3(kBlock), 0, stream, a);
+        else
+            hipLaunchKernelGGL((fold_kernel<T, OP, 2, 4, NT>), grid, dim3(kBlock), 0, stream, a);
+    } else {
+        hipLaunchKernelGGL((fold_kernel<T, OP, 0, kUnrollN, NT>), dim3((unsigned)grid_for(a, kUnrollN)),
                            dim3(kBlock), 0, stream, a);
-    else
-        hipLaunchKernelGGL((fold_kernel<T, OP, 0, kUnroll, NT>), dim3((unsigned)blocks),
-                           dim3(kBlock), 0, stream, a);
+    }
     return hipGetLastError();
 }
 
+// Cache policy: streams larger than the 256 MiB Infinity Cache go
+// non-temporal on both loads and stores (measured +15-20 % at 768 MiB,
+// profiles/ and DESIGN.md); smaller working sets keep the default policy so
+// back-to-back calls can hit in the MALL.
+constexpr size_t kNtThresholdBytes = size_t(256) << 20;
+
 template <typename T, int OP>
 hipError_t launch_nt(const FoldArgs &a, hipStream_t stream) {
-    return fold_tuning().nontemporal ? launch_typed<T, OP, true>(a, stream)
-                                     : launch_typed<T, OP, false>(a, stream);
+    int mode = fold_tuning().nontemporal;
+    if (mode < 0) {
+        const size_t n = a.head + a.nvec * (16 / sizeof(T)) + a.tail;
+        mode = (size_t)(a.nins + 1) * n * sizeof(T) >= kNtThresholdBytes ? 3 : 0;
+    }
+    switch (mode & 3) {
+    case 0: return launch_typed<T, OP, 0>(a, stream);
+    case 1: return launch_typed<T, OP, 1>(a, stream);
+    case 2: return launch_typed<T, OP, 2>(a, stream);
+    default: return launch_typed<T, OP, 3>(a, stream);
+    }
 }
 
 template <typename T>
@@ -335,9 +362,10 @@ hipError_t launch_cplx_ops(int op, const FoldArgs &a, hipStream_t s) {
 
 FoldTuning &fold_tuning() {
     static FoldTuning t = [] {
-        FoldTuning r{0, 0};
+        FoldTuning r{0, -1, 4};
         if (const char *e = std::getenv("SHMEMX_FOLD_MAX_BLOCKS")) r.max_blocks = std::atoi(e);
         if (const char *e = std::getenv("SHMEMX_FOLD_NT")) r.nontemporal = std::atoi(e);
+        if (const char *e = std::getenv("SHMEMX_FOLD_UNROLL")) r.unroll = std::atoi(e);
         return r;
     }();
     return t;

@@ -27,11 +27,13 @@ bool op_on_device(int type, int op);   // this build has a HIP kernel for it
 hipError_t launch_fold(int type, int op, void *out, const void *const *ins,
                        int nins, size_t n, hipStream_t stream);
 
-// Tuning knobs for the fold kernels (read once from the environment:
-// SHMEMX_FOLD_MAX_BLOCKS, SHMEMX_FOLD_NT).
+// Tuning knobs for the fold kernels (initialised from the environment:
+// SHMEMX_FOLD_MAX_BLOCKS, SHMEMX_FOLD_NT, SHMEMX_FOLD_UNROLL; changed at run
+// time by shmemx_fold_set_tuning).
 struct FoldTuning {
-    int max_blocks;   // grid cap; 0 = one 16-B vector per lane per unroll slot
-    int nontemporal;  // 1: nt loads/stores on the streamed arrays
+    int max_blocks;   // grid cap; 0 = one chunk of 256 x unroll vectors per block
+    int nontemporal;  // -1 auto by size; else bit 0: nt loads, bit 1: nt stores
+    int unroll;       // 2, 4 or 8 16-B vectors per lane per input (2-input fold)
 };
 FoldTuning &fold_tuning();
 

@@ -645,6 +645,15 @@ int shmemx_reduce_plan(int type, int op, int nreduce, int PE_start,
     return make_plan(type, op, nreduce, PE_start, logPE_stride, PE_size, pe, npes, algo, plan);
 }
 
+int shmemx_fold_set_tuning(int max_blocks, int nontemporal, int unroll) {
+    if (max_blocks < 0 || (unroll != 2 && unroll != 4 && unroll != 8)) return set_error(SHMEMX_EINVAL);
+    FoldTuning &t = fold_tuning();
+    t.max_blocks = max_blocks;
+    t.nontemporal = nontemporal < 0 ? -1 : (nontemporal & 3);
+    t.unroll = unroll;
+    return SHMEMX_OK;
+}
+
 size_t shmemx_type_size(int type) { return type_size(type); }
 int shmemx_op_valid(int type, int op) { return op_valid(type, op) ? 1 : 0; }
 int shmemx_op_on_device(int type, int op) { return op_on_device(type, op) ? 1 : 0; }

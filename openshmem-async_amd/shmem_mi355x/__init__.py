@@ -89,6 +89,8 @@ def lib() -> ctypes.CDLL:
     L.shmemx_get_stream.restype = vp
     L.shmemx_set_algo.argtypes = [i]
     L.shmemx_set_algo.restype = i
+    L.shmemx_fold_set_tuning.argtypes = [i, i, i]
+    L.shmemx_fold_set_tuning.restype = i
     L.shmemx_type_size.argtypes = [i]
     L.shmemx_type_size.restype = sz
     L.shmemx_op_valid.argtypes = [i, i]
@@ -237,6 +239,11 @@ def plan(type_name: str, op: str, nreduce: int, PE_start: int, logPE_stride: int
     inv = {v: k for k, v in ALGOS.items()}
     return PlanInfo(inv[p.algo], p.member, p.nmembers, p.elem_size, p.chunk, p.main,
                     p.tail, p.ws_bytes)
+
+
+def set_fold_tuning(max_blocks: int = 0, nontemporal: int = -1, unroll: int = 4) -> None:
+    """Launch shape of the fold kernels (grid cap, nt loads/stores, unroll)."""
+    _check(lib().shmemx_fold_set_tuning(max_blocks, nontemporal, unroll), "shmemx_fold_set_tuning")
 
 
 def type_size(type_name: str) -> int:

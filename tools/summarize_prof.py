@@ -1,0 +1,76 @@
+"""Summarise rocprofv3 output of bench.py into profiles/.
+
+usage: summarize_prof.py <trace_dir> <fetch_dir> <write_dir> <round_tag>
+
+* <trace_dir>: `rocprofv3 --kernel-trace --stats --output-format csv` run
+  -> copies *kernel_stats.csv to profiles/<tag>_kernel_stats.csv
+* <fetch_dir>/<write_dir>: `rocprofv3 --pmc FETCH_SIZE` / `--pmc WRITE_SIZE`
+  runs (separate passes: FETCH_SIZE and WRITE_SIZE do not fit one pass of the
+  4 TCC slots, MI355X_MICROARCH.md "rocprofv3 PMC slots").
+  HBM bytes per launch = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024: both
+  counters are in KiB, and on gfx950 FETCH_SIZE reports exactly half of the
+  bytes of a wide coalesced streaming read (MI355X_MICROARCH.md "HBM").
+  -> profiles/<tag>_pmc.json
+"""
+import csv, glob, json, os, shutil, statistics, sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEY = "fold_kernel"        # the dominant kernel of the 1-GPU bench
+
+
+def find(d, pat):
+    hits = sorted(glob.glob(os.path.join(d, "**", pat), recursive=True))
+    return hits
+
+
+def counter_values(d, counter):
+    vals = {}
+    for f in find(d, "*counter_collection.csv"):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                name = row.get("Kernel_Name", "")
+                if row.get("Counter_Name") != counter:
+                    continue
+                vals.setdefault(name, []).append(float(row["Counter_Value"]))
+    return vals
+
+
+def main():
+    trace, fetch, write, tag = sys.argv[1:5]
+    out = os.path.join(REPO, "profiles")
+    os.makedirs(out, exist_ok=True)
+    stats = find(trace, "*kernel_stats.csv")
+    summary = {}
+    if stats:
+        shutil.copy(stats[0], os.path.join(out, f"{tag}_kernel_stats.csv"))
+        with open(stats[0]) as fh:
+            for row in csv.DictReader(fh):
+                if KEY in row["Name"]:
+                    summary.setdefault("trace", []).append(
+                        {"name": row["Name"][:160], "calls": int(row["Calls"]),
+                         "avg_us": float(row["AverageNs"]) / 1e3})
+    fv, wv = counter_values(fetch, "FETCH_SIZE"), counter_values(write, "WRITE_SIZE")
+    for name in fv:
+        if KEY not in name:
+            continue
+        f = statistics.median(fv[name])
+        w = statistics.median(wv.get(name, [0.0]))
+        summary.setdefault("pmc", []).append(
+            {"name": name[:160], "launches": len(fv[name]), "FETCH_SIZE_KiB": f,
+             "WRITE_SIZE_KiB": w, "hbm_bytes_per_launch": 2 * f * 1024 + w * 1024})
+    # the 2-input double-sum fold over 32 Mi elements = the bench's timed kernel
+    best = None
+    for p in summary.get("pmc", []):
+        if "<double, 0, 2" in p["name"].replace("Li", "").replace("ELi", ", ") or best is None:
+            best = p
+    if best:
+        summary["fold_double_sum"] = {"hbm_bytes_per_launch": best["hbm_bytes_per_launch"],
+                                      "alg_bytes_per_launch": 3 * 8 * 32 * 1024 * 1024,
+                                      "kernel": best["name"]}
+    with open(os.path.join(out, f"{tag}_pmc.json"), "w") as fh:
+        json.dump(summary, fh, indent=1)
+    print(json.dumps(summary, indent=1))
+
+
+if __name__ == "__main__":
+    main()
