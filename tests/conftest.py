@@ -19,6 +19,20 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu)")
 
 
+def _ensure_built():
+    """Build the HIP library (hipcc, gfx950) and the oracle if a fresh
+    checkout lacks them (built .so files are not in git)."""
+    import subprocess
+    lib = os.path.join(REPO, "openshmem-async_amd", "libshmem_reduce_mi355x.so")
+    if not os.path.exists(lib):
+        subprocess.run(["make", "-j8", "-C", os.path.join(REPO, "openshmem-async_amd")], check=True)
+    if not os.path.exists(os.path.join(REPO, "oracle", "liboracle_reduce.so")):
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
+
+
+_ensure_built()
+
+
 def gpu_count() -> int:
     try:
         import torch

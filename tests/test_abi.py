@@ -1,0 +1,168 @@
+"""CPU tests of the C ABI library: it loads, exports every symbol the header
+declares (pshmem_* strong, shmem_* weak aliases, reduce-op.c:275-364), the
+header compiles and links from C, and the host-side planning logic (which
+algorithm, which shards) is right.  No GPU calls here."""
+import os
+import re
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "shmem_reduce_mi355x.h")
+LIBDIR = os.path.join(REPO, "openshmem-async_amd")
+LIB = os.path.join(LIBDIR, "libshmem_reduce_mi355x.so")
+
+
+def declared_functions():
+    pre = subprocess.run(["gcc", "-E", "-P", "-x", "c", HEADER], check=True,
+                         capture_output=True, text=True).stdout
+    return sorted(set(re.findall(r"\b(p?shmemx?_[A-Za-z0-9_]+)\s*\(", pre)))
+
+
+def exported():
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], check=True,
+                         capture_output=True, text=True).stdout
+    syms = {}
+    for line in out.splitlines():
+        parts = line.split()
+        if len(parts) == 3:
+            syms[parts[2]] = (parts[0], parts[1])
+    return syms
+
+
+def test_library_loads(shm):
+    assert shm.lib() is not None
+
+
+def test_every_declared_symbol_is_exported():
+    decl = declared_functions()
+    assert len(decl) >= 88 + 8
+    syms = exported()
+    missing = [d for d in decl if d not in syms]
+    assert not missing, missing
+
+
+def test_pshmem_strong_shmem_weak_same_address(shm):
+    syms = exported()
+    pairs = [f"{t}_{o}_to_all" for t, o in shm.REFERENCE_PAIRS] + ["init", "finalize", "my_pe", "n_pes"]
+    assert len(shm.REFERENCE_PAIRS) == 44
+    for p in pairs:
+        addr_s, kind_s = syms["shmem_" + p]
+        addr_p, kind_p = syms["pshmem_" + p]
+        assert kind_p == "T" and kind_s == "W", p
+        assert addr_s == addr_p, p
+
+
+def test_reference_pair_set_matches_reduce_op_c(shm, oracle):
+    """The 44 (type, op) pairs are exactly those reduce-op.c:388-431 defines."""
+    for t in shm.TYPES:
+        for o in shm.OPS:
+            assert ((t, o) in shm.REFERENCE_PAIRS) == oracle.op_valid(t, o), (t, o)
+            assert bool(shm.lib().shmemx_op_valid(shm.TYPES[t], shm.OPS[o])) == oracle.op_valid(t, o)
+
+
+def test_enum_numbering_matches_oracle(shm, oracle):
+    assert shm.TYPES == oracle.TYPES and shm.OPS == oracle.OPS
+    for t in shm.TYPES:
+        assert shm.type_size(t) == oracle.lib().oracle_type_size(oracle.TYPES[t])
+
+
+def test_header_compiles_and_links_from_c(tmp_path):
+    """A C99 caller written like the reference's users (ISx, isx.c:617)."""
+    src = tmp_path / "caller.c"
+    src.write_text(r'''
+#include <complex.h>
+#include "shmem_reduce_mi355x.h"
+static long pSync[SHMEM_REDUCE_SYNC_SIZE];
+static long long llWrk[SHMEM_REDUCE_MIN_WRKDATA_SIZE];
+int main(void) {
+    static long long total, mine = 3;
+    double complex z = 1.0, w;
+    for (int i = 0; i < SHMEM_REDUCE_SYNC_SIZE; i++) pSync[i] = SHMEM_SYNC_VALUE;
+    shmem_init();
+    shmem_longlong_sum_to_all(&total, &mine, 1, 0, 0, shmem_n_pes(), llWrk, pSync);
+    shmem_complexd_prod_to_all(&w, &z, 1, 0, 0, 1, NULL, pSync);
+    pshmem_double_max_to_all(NULL, NULL, 0, 0, 0, 1, NULL, pSync);
+    shmem_finalize();
+    return (int)(total != 3 * shmem_n_pes());
+}
+''')
+    exe = tmp_path / "caller"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.dirname(HEADER), str(src),
+                    "-L", LIBDIR, "-lshmem_reduce_mi355x", f"-Wl,-rpath,{LIBDIR}", "-o", str(exe)],
+                   check=True)
+    assert exe.exists()
+
+
+def test_header_compiles_as_cpp(tmp_path):
+    src = tmp_path / "caller.cpp"
+    src.write_text('#include "shmem_reduce_mi355x.h"\n'
+                   'int main(){ std::complex<double> a, b; '
+                   'shmem_complexd_sum_to_all(&a, &b, 1, 0, 0, 1, nullptr, nullptr); return 0; }\n')
+    subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-I", os.path.dirname(HEADER), str(src)],
+                   check=True)
+
+
+# ------------------------------------------------------------------- plans
+def test_plan_algorithm_selection(shm):
+    P = shm.plan
+    # full set, RCCL-native pairs -> RCCL
+    assert P("double", "sum", 1 << 25, 0, 0, 8, 3, 8).algo == "rccl"
+    assert P("long", "max", 1000, 0, 0, 4, 0, 4).algo == "rccl"
+    assert P("int", "prod", 1000, 0, 0, 2, 1, 2).algo == "rccl"
+    # bitwise (no RCCL op), float min/max (NaN semantics), short (no RCCL type),
+    # complex -> A2A
+    for t, o in [("long", "xor"), ("int", "and"), ("double", "min"), ("float", "max"),
+                 ("short", "sum"), ("complexd", "prod")]:
+        assert P(t, o, 1000, 0, 0, 4, 2, 4).algo == "a2a", (t, o)
+    # strided or partial sets -> A2A, even for RCCL-native pairs
+    assert P("double", "sum", 1000, 0, 1, 4, 2, 8).algo == "a2a"
+    assert P("double", "sum", 1000, 1, 0, 3, 2, 8).algo == "a2a"
+    # explicit choices
+    assert P("double", "sum", 1000, 0, 0, 4, 2, 4, "gather").algo == "gather"
+    assert P("double", "sum", 1000, 0, 0, 4, 2, 4, "a2a").algo == "a2a"
+    with pytest.raises(shm.ShmemError) as e:
+        P("long", "xor", 1000, 0, 0, 4, 2, 4, "rccl")
+    assert e.value.code == 3
+
+
+def test_plan_errors(shm):
+    P = shm.plan
+    cases = [((100, 0, 0, 4, 5, 8), 2),      # PE 5 not in {0..3}
+             ((100, 1, 1, 3, 2, 8), 2),      # PE 2 not in {1,3,5}
+             ((100, 0, 0, 9, 0, 8), 1),      # set beyond npes
+             ((-1, 0, 0, 2, 0, 2), 1),       # nreduce < 0
+             ((100, 0, -1, 2, 0, 2), 1),     # negative stride
+             ((100, 0, 0, 0, 0, 2), 1)]      # empty set
+    for args, code in cases:
+        with pytest.raises(shm.ShmemError) as e:
+            P("double", "sum", *args)
+        assert e.value.code == code, args
+    with pytest.raises(shm.ShmemError) as e:
+        P("longdouble", "sum", 10, 0, 0, 1, 0, 1)
+    assert e.value.code == 3
+    with pytest.raises(shm.ShmemError) as e:
+        P("double", "xor", 10, 0, 0, 1, 0, 1)
+    assert e.value.code == 1
+
+
+@pytest.mark.parametrize("t", ["short", "int", "double", "complexd", "complexf"])
+@pytest.mark.parametrize("P_", [2, 3, 5, 8])
+@pytest.mark.parametrize("n", [0, 1, 7, 64, 1000, 4103, (1 << 25) + 3])
+def test_plan_shards_cover_and_align(shm, t, P_, n):
+    """A2A shards tile [0, n) exactly, every shard starts on a 16-byte
+    boundary of the array; RCCL main+tail == n with 16-byte shards."""
+    sz = shm.type_size(t)
+    g = max(1, 16 // sz)
+    p = shm.plan(t, "sum", n, 0, 0, P_, 0, P_, "a2a")
+    assert p.chunk % g == 0 and p.chunk * P_ >= n
+    counts = [max(0, min(p.chunk, n - i * p.chunk)) for i in range(P_)]
+    assert sum(counts) == n
+    assert p.ws_bytes == p.chunk * P_ * sz
+    if t in ("int", "double"):
+        r = shm.plan(t, "sum", n, 0, 0, P_, 0, P_, "rccl")
+        assert r.main == r.chunk * P_ and r.main + r.tail == n
+        assert r.chunk % g == 0 and r.tail < P_ * g
+    q = shm.plan(t, "sum", n, 0, 0, P_, 0, P_, "gather")
+    assert q.ws_bytes == n * P_ * sz

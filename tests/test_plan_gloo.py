@@ -1,0 +1,201 @@
+"""Multi-PE path on CPU: world_size 2 and 4 over torch.distributed gloo.
+
+Each rank asks the C library for its plan (shmemx_reduce_plan: algorithm,
+member index, shard size, RCCL main/tail split) and then runs exactly the
+exchange schedule runtime.cpp enqueues on RCCL, with gloo point-to-point
+messages standing in for ncclSend/ncclRecv and the oracle folding the
+received shards in the order the HIP kernel uses:
+
+  A2A    shard i of every source -> member i; fold in active-set order;
+         shard all-gather              -> must equal the reference PE_start
+                                          result on every member, bit for bit
+  GATHER every source -> every member; fold me first, then ascending
+                                       -> must equal the reference PE me
+                                          result, bit for bit
+  RCCL   main = P * chunk elements reduce-scattered + all-gathered, the tail
+         all-reduced              -> equals the reference up to summation order
+                                     (bit-exact for integers)
+
+This proves the decomposition (plan + schedule) on CPU; the GPU tests prove
+the fold kernel, and RCCL moves the bytes.
+"""
+import multiprocessing as mp
+import os
+import socket
+import sys
+import traceback
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CASES = [
+    # (type, op, kind, n, set, algo)
+    ("double", "sum", 0, 1000, None, "a2a"),
+    ("double", "sum", 0, 4103, None, "gather"),
+    ("double", "sum", 0, 4103, None, "rccl"),
+    ("int", "sum", 1, 4103, None, "rccl"),
+    ("long", "xor", 1, 777, None, "auto"),
+    ("long", "and", 1, 65, None, "a2a"),
+    ("short", "max", 1, 130, None, "auto"),
+    ("float", "min", 1, 1001, None, "auto"),
+    ("complexd", "prod", 0, 99, None, "a2a"),
+    ("complexf", "sum", 1, 5, None, "gather"),
+    ("double", "prod", 0, 3, None, "a2a"),     # fewer elements than PEs
+    ("double", "sum", 0, 0, None, "a2a"),      # nreduce = 0
+    ("int", "min", 1, 300, "strided", "auto"),
+    ("double", "sum", 0, 300, "offset", "auto"),
+]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _set_for(kind, world):
+    if kind is None:
+        return (0, 0, world)
+    if kind == "strided":
+        return (0, 1, world // 2) if world >= 4 else (1, 0, 1)
+    return (1, 0, world - 1)  # offset
+
+
+def _send(dist, arr, dst):
+    import torch
+    dist.send(torch.from_numpy(np.ascontiguousarray(arr).view(np.uint8).copy()), dst)
+
+
+def _recv(dist, nbytes, src):
+    import torch
+    t = torch.empty(nbytes, dtype=torch.uint8)
+    dist.recv(t, src)
+    return t.numpy()
+
+
+def _exchange(dist, me, sends, recvs):
+    """sends: {peer: array}, recvs: {peer: nbytes}; lower rank sends first."""
+    got = {}
+    for peer in sorted(set(sends) | set(recvs)):
+        if me < peer:
+            if peer in sends:
+                _send(dist, sends[peer], peer)
+            if peer in recvs:
+                got[peer] = _recv(dist, recvs[peer], peer)
+        else:
+            if peer in recvs:
+                got[peer] = _recv(dist, recvs[peer], peer)
+            if peer in sends:
+                _send(dist, sends[peer], peer)
+    return got
+
+
+def _run_case(dist, shm, oracle, rank, world, case):
+    t, op, kind, n, setkind, algo = case
+    s = _set_for(setkind, world)
+    members = [s[0] + i * (1 << s[1]) for i in range(s[2])]
+    srcs = oracle.sources(t, kind, world, n, base_seed=0x5EED0000 + n)
+    want = oracle.reduce_sim(t, op, srcs, *s)
+    if rank not in members:
+        with pytest.raises(shm.ShmemError):
+            shm.plan(t, op, n, *s, rank, world, algo)
+        return
+    p = shm.plan(t, op, n, *s, rank, world, algo)
+    P, m, dt = p.nmembers, p.member, srcs.dtype
+    src = srcs[rank]
+    out = np.zeros(n, dtype=dt)
+    if P == 1:
+        out[:] = src
+    elif p.algo == "a2a":
+        c = p.chunk
+        cnt = [max(0, min(c, n - i * c)) for i in range(P)]
+        lo = m * c
+        sends = {members[i]: src[i * c:i * c + cnt[i]] for i in range(P) if i != m and cnt[i]}
+        recvs = {members[i]: cnt[m] * dt.itemsize for i in range(P) if i != m and cnt[m]}
+        got = _exchange(dist, rank, sends, recvs)
+        if cnt[m]:
+            shards = np.stack([src[lo:lo + cnt[m]] if i == m else
+                               got[members[i]].view(dt) for i in range(P)])
+            out[lo:lo + cnt[m]] = oracle.reduce_sim(t, op, shards, 0, 0, P)[0]
+        sends = {members[i]: out[lo:lo + cnt[m]] for i in range(P) if i != m and cnt[m]}
+        recvs = {members[i]: cnt[i] * dt.itemsize for i in range(P) if i != m and cnt[i]}
+        got = _exchange(dist, rank, sends, recvs)
+        for i in range(P):
+            if i != m and cnt[i]:
+                out[i * c:i * c + cnt[i]] = got[members[i]].view(dt)
+        assert out.tobytes() == want[members[0]].tobytes(), case
+    elif p.algo == "gather":
+        sends = {members[i]: src for i in range(P) if i != m}
+        recvs = {members[i]: n * dt.itemsize for i in range(P) if i != m}
+        got = _exchange(dist, rank, sends, recvs) if n else {}
+        full = np.stack([src if i == m else got[members[i]].view(dt) for i in range(P)]) \
+            if n else np.zeros((P, 0), dt)
+        out = oracle.reduce_sim(t, op, full, 0, 0, P)[m]
+        assert out.tobytes() == want[rank].tobytes(), case
+    else:  # rccl: reduce-scatter main part, all-gather, all-reduce tail
+        c, main = p.chunk, p.main
+        assert main + p.tail == n
+        if c:
+            sends = {members[i]: src[i * c:(i + 1) * c] for i in range(P) if i != m}
+            recvs = {members[i]: c * dt.itemsize for i in range(P) if i != m}
+            got = _exchange(dist, rank, sends, recvs)
+            shards = np.stack([src[m * c:(m + 1) * c] if i == m else got[members[i]].view(dt)
+                               for i in range(P)])
+            out[m * c:(m + 1) * c] = oracle.reduce_sim(t, op, shards, 0, 0, P)[0]
+            sends = {members[i]: out[m * c:(m + 1) * c] for i in range(P) if i != m}
+            got = _exchange(dist, rank, sends, recvs)
+            for i in range(P):
+                if i != m:
+                    out[i * c:(i + 1) * c] = got[members[i]].view(dt)
+        if p.tail:
+            sends = {members[i]: src[main:] for i in range(P) if i != m}
+            recvs = {members[i]: p.tail * dt.itemsize for i in range(P) if i != m}
+            got = _exchange(dist, rank, sends, recvs)
+            tails = np.stack([src[main:] if i == m else got[members[i]].view(dt)
+                              for i in range(P)])
+            out[main:] = oracle.reduce_sim(t, op, tails, 0, 0, P)[0]
+        if dt.kind in "iu":
+            assert out.tobytes() == want[rank].tobytes(), case
+        else:
+            # any summation order: |d| <= 2 (P-1) u sum|x| (BASELINE/SURVEY §8d)
+            u = np.finfo(dt).eps / 2
+            bound = 2 * (P - 1) * u * np.abs(srcs[members]).sum(axis=0)
+            assert (np.abs(out - want[rank]) <= bound).all(), case
+
+
+def _worker(rank, world, port, q):
+    try:
+        sys.path.insert(0, os.path.join(REPO, "openshmem-async_amd"))
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import torch.distributed as dist
+        import oracle
+        import shmem_mi355x as shm
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}",
+                                rank=rank, world_size=world)
+        for case in CASES:
+            _run_case(dist, shm, oracle, rank, world, case)
+            dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, "ok"))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_multi_pe_schedule_over_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    results = {}
+    for _ in range(world):
+        r, msg = q.get(timeout=600)
+        results[r] = msg
+    for p in procs:
+        p.join(timeout=60)
+    bad = {r: m for r, m in results.items() if m != "ok"}
+    assert not bad, "\n".join(f"rank {r}:\n{m}" for r, m in bad.items())
