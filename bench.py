@@ -92,6 +92,33 @@ def cpu_baseline(n: int, reps: int):
                       f"({med * 1e3:.1f} ms/call, {wall:.1f} s wall)"}
 
 
+def host_e2e(n: int):
+    """The north-star end-to-end rate: source/target in HOST memory (the
+    reference's symmetric heap), blocking shmem_double_sum_to_all at
+    PE_size = 1 = H2D + device path + D2H.  Pageable (numpy) and pinned."""
+    import numpy as np
+    res = {}
+    psync = np.full(128, -1, dtype=np.int64)
+    for kind in ("pageable", "pinned"):
+        if kind == "pageable":
+            src = np.random.default_rng(1).random(n) + 1.0
+            tgt = np.zeros(n)
+        else:
+            src = torch.rand(n, dtype=torch.float64).pin_memory()
+            tgt = torch.zeros(n, dtype=torch.float64).pin_memory()
+        shm.to_all("double", "sum", tgt, src, n, 0, 0, 1, None, psync)   # warm-up
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            shm.to_all("double", "sum", tgt, src, n, 0, 0, 1, None, psync)
+            ts.append(time.perf_counter() - t0)
+        t = statistics.median(ts)
+        ok = bool((np.asarray(tgt) == np.asarray(src)).all())
+        res[kind] = {"GiBps": round(n * 8 / t / GiB, 2), "ms_per_call": round(t * 1e3, 2),
+                     "correct": ok}
+    return res
+
+
 def time_region(fn, steps, stream, barrier):
     """Run fn() `steps` times on `stream`; returns (wall_s, event_s)."""
     barrier()
@@ -218,6 +245,7 @@ def main():
                 "GiBps": round(nbytes * k2 / w2 / GiB, 1),
                 "hbm_GBps": round(2 * nbytes / (e2 / k2) / 1e9, 1),
                 "us_per_call": round(e2 / k2 * 1e6, 2)}
+            extras["host_resident_e2e"] = host_e2e(n)
     else:
         t_call = ev / a.steps
         xgmi_bytes = 2 * (world - 1) / world * nbytes        # per GPU, RS + AG

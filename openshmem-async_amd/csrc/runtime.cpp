@@ -119,7 +119,11 @@ static int init_locked(int pe, int npes, int device, const void *uid) {
     if (device < 0 && !(npes == 1 && hipGetDevice(&device) == hipSuccess)) device = pe % ndev;
     if (device < 0 || device >= ndev) return set_error(SHMEMX_EINVAL);
     SHMX_HIP(hipSetDevice(device));
-    SHMX_HIP(hipStreamCreateWithFlags(&g_state.stream, hipStreamNonBlocking));
+    // A BLOCKING stream: ordered after the legacy default stream, where a
+    // plain HIP program (and PyTorch's default stream) writes the buffers it
+    // then hands to the blocking entry points.  Work on other non-blocking
+    // streams must be synchronised by the caller, as for any HIP library.
+    SHMX_HIP(hipStreamCreate(&g_state.stream));
     if (npes > 1) {
         if (!uid) return set_error(SHMEMX_EINVAL);
         ncclUniqueId id;

@@ -102,3 +102,34 @@ def test_reduce_on_stream_torch_stream(cuda, shm, oracle):
     shm.reduce_on_stream("float", "sum", d, s, n, 0, 0, 1, "auto", st.cuda_stream)
     st.synchronize()
     assert d.cpu().numpy().tobytes() == src.tobytes()
+
+
+def test_hip_graph_capture_and_replay(cuda, shm):
+    """The stream-ordered entry points are capturable (no allocation or host
+    sync inside once a call of the same shape has run): capture a 3-input fold
+    and a PE_size=1 reduction into one graph, change the inputs, replay."""
+    import torch
+    n = (1 << 20) + 5
+    a = torch.rand(n, dtype=torch.float64, device="cuda")
+    b = torch.rand(n, dtype=torch.float64, device="cuda")
+    c = torch.rand(n, dtype=torch.float64, device="cuda")
+    out = torch.empty_like(a)
+    out2 = torch.empty_like(a)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        shm.fold_n("double", "sum", out, [a, b, c], n, s.cuda_stream)
+        shm.reduce_on_stream("double", "sum", out2, out, n, 0, 0, 1, "auto", s.cuda_stream)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        st = torch.cuda.current_stream().cuda_stream
+        shm.fold_n("double", "sum", out, [a, b, c], n, st)
+        shm.reduce_on_stream("double", "sum", out2, out, n, 0, 0, 1, "auto", st)
+    for _ in range(2):
+        a.uniform_(); b.uniform_(); c.uniform_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, (a + b) + c)
+        assert torch.equal(out2, out)
