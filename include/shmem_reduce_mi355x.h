@@ -94,6 +94,36 @@ SHMEMX_DECL_MINMAX(float, float)
 SHMEMX_DECL_MINMAX(double, double)
 SHMEMX_DECL_MINMAX(longdouble, long double)
 
+/* Fortran bindings (reference src/fortran/fortran.c:1003-1054, gfortran
+ * name mangling FORTRANIFY(sym) = sym##_): arguments by reference, pSync an
+ * INTEGER array; each forwards to the C routine above. */
+#define SHMEMX_DECL_FORTRAN(Fname, Op, T)                                      \
+    void shmem_##Fname##_##Op##_to_all_(T *target, T *source, int *nreduce,  \
+                                        int *PE_start, int *logPE_stride,    \
+                                        int *PE_size, T *pWrk, int *pSync);  \
+    void pshmem_##Fname##_##Op##_to_all_(T *target, T *source, int *nreduce, \
+                                         int *PE_start, int *logPE_stride,   \
+                                         int *PE_size, T *pWrk, int *pSync);
+#define SHMEMX_DECL_FORTRAN_REAL(Op)                                           \
+    SHMEMX_DECL_FORTRAN(int2, Op, short) SHMEMX_DECL_FORTRAN(int4, Op, int)  \
+    SHMEMX_DECL_FORTRAN(int8, Op, long) SHMEMX_DECL_FORTRAN(real4, Op, float)\
+    SHMEMX_DECL_FORTRAN(real8, Op, double)                                   \
+    SHMEMX_DECL_FORTRAN(real16, Op, long double)
+#define SHMEMX_DECL_FORTRAN_INT(Op)                                            \
+    SHMEMX_DECL_FORTRAN(int2, Op, short) SHMEMX_DECL_FORTRAN(int4, Op, int)  \
+    SHMEMX_DECL_FORTRAN(int8, Op, long)
+SHMEMX_DECL_FORTRAN_REAL(sum)
+SHMEMX_DECL_FORTRAN_REAL(prod)
+SHMEMX_DECL_FORTRAN_REAL(max)
+SHMEMX_DECL_FORTRAN_REAL(min)
+SHMEMX_DECL_FORTRAN_INT(and)
+SHMEMX_DECL_FORTRAN_INT(or)
+SHMEMX_DECL_FORTRAN_INT(xor)
+SHMEMX_DECL_FORTRAN(comp4, sum, SHMEMX_COMPLEX(float))
+SHMEMX_DECL_FORTRAN(comp8, sum, SHMEMX_COMPLEX(double))
+SHMEMX_DECL_FORTRAN(comp4, prod, SHMEMX_COMPLEX(float))
+SHMEMX_DECL_FORTRAN(comp8, prod, SHMEMX_COMPLEX(double))
+
 /* ------------------------------------------------------------------------ */
 /* Part 2: runtime (replaces shmem_init updown.c:160, shmem_my_pe/n_pes).   */
 

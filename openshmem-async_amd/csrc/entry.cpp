@@ -70,6 +70,45 @@ SHMX_MINMAX(double, double, SHMEMX_TYPE_DOUBLE)
 SHMX_MINMAX(float, float, SHMEMX_TYPE_FLOAT)
 SHMX_MINMAX(longdouble, long double, SHMEMX_TYPE_LONGDOUBLE)
 
+// Fortran forwarders (reference src/fortran/fortran.c:1003-1054): every
+// argument by reference, pSync an INTEGER array, the C routine does the work.
+#define SHMX_FORTRAN(Op, Fname, Cname, T)                                      \
+    void pshmem_##Fname##_##Op##_to_all_(T *target, T *source, int *nreduce, \
+                                         int *PE_start, int *logPE_stride,   \
+                                         int *PE_size, T *pWrk, int *pSync)  \
+    {                                                                        \
+        pshmem_##Cname##_##Op##_to_all(target, source, *nreduce, *PE_start,  \
+                                       *logPE_stride, *PE_size, pWrk,        \
+                                       reinterpret_cast<long *>(pSync));     \
+    }                                                                        \
+    void shmem_##Fname##_##Op##_to_all_(T *, T *, int *, int *, int *, int *,\
+                                        T *, int *)                          \
+        __attribute__((weak, alias("pshmem_" #Fname "_" #Op "_to_all_")));
+
+#define SHMX_FORTRAN_REAL(Op)                                                  \
+    SHMX_FORTRAN(Op, int2, short, short)                                     \
+    SHMX_FORTRAN(Op, int4, int, int)                                         \
+    SHMX_FORTRAN(Op, int8, long, long)                                       \
+    SHMX_FORTRAN(Op, real4, float, float)                                    \
+    SHMX_FORTRAN(Op, real8, double, double)                                  \
+    SHMX_FORTRAN(Op, real16, longdouble, long double)
+#define SHMX_FORTRAN_INT(Op)                                                   \
+    SHMX_FORTRAN(Op, int2, short, short)                                     \
+    SHMX_FORTRAN(Op, int4, int, int)                                         \
+    SHMX_FORTRAN(Op, int8, long, long)
+
+SHMX_FORTRAN_REAL(sum)
+SHMX_FORTRAN_REAL(prod)
+SHMX_FORTRAN_REAL(max)
+SHMX_FORTRAN_REAL(min)
+SHMX_FORTRAN_INT(and)
+SHMX_FORTRAN_INT(or)
+SHMX_FORTRAN_INT(xor)
+SHMX_FORTRAN(sum, comp4, complexf, std::complex<float>)
+SHMX_FORTRAN(sum, comp8, complexd, std::complex<double>)
+SHMX_FORTRAN(prod, comp4, complexf, std::complex<float>)
+SHMX_FORTRAN(prod, comp8, complexd, std::complex<double>)
+
 // Stream-ordered typed forms (header Part 3).
 #define SHMX_STREAM(Name, Op, T, TYPE, OPC)                                    \
     void shmemx_##Name##_##Op##_to_all_on_stream(                            \

@@ -133,3 +133,22 @@ def test_hip_graph_capture_and_replay(cuda, shm):
         torch.cuda.synchronize()
         assert torch.equal(out, (a + b) + c)
         assert torch.equal(out2, out)
+
+
+def test_fortran_forwarder(cuda, shm, oracle):
+    """shmem_real8_sum_to_all_ (fortran.c:1003-1016): args by reference."""
+    import torch
+    n = 1001
+    src = oracle.fill("double", 1, 11, n)
+    s = torch.from_numpy(src).cuda()
+    d = torch.zeros_like(s)
+    c_int = ctypes.c_int
+    psync = np.full(128, -1, dtype=np.int32)
+    f = shm.lib().shmem_real8_sum_to_all_
+    f.restype = None
+    f(ctypes.c_void_p(d.data_ptr()), ctypes.c_void_p(s.data_ptr()), ctypes.byref(c_int(n)),
+      ctypes.byref(c_int(0)), ctypes.byref(c_int(0)), ctypes.byref(c_int(1)), None,
+      ctypes.c_void_p(psync.ctypes.data))
+    assert shm.last_error() == 0
+    assert d.cpu().numpy().tobytes() == src.tobytes()
+    assert (psync == -1).all()
