@@ -34,6 +34,7 @@
 #include <type_traits>
 
 #include "internal.h"
+#include "ld80.h"
 #include "shmem_reduce_mi355x.h"
 
 namespace shmx {
@@ -147,6 +148,18 @@ SHMX_FP_OPS(double)
 SHMX_CPLX_OPS(cplxd, double)
 SHMX_CPLX_OPS(cplxf, float)
 #undef SHMX_CPLX_OPS
+
+// long double: x87 80-bit in software (ld80.h), sum/prod/min/max
+// (reduce-op.c:91,150).
+using x87::ld80;
+template <> struct Op<ld80, SHMEMX_OP_SUM> {
+    __device__ static ld80 ap(ld80 a, ld80 b) { return x87::add(a, b); } };
+template <> struct Op<ld80, SHMEMX_OP_PROD> {
+    __device__ static ld80 ap(ld80 a, ld80 b) { return x87::mul(a, b); } };
+template <> struct Op<ld80, SHMEMX_OP_MIN> {
+    __device__ static ld80 ap(ld80 a, ld80 b) { return x87::less(a, b) ? a : b; } };
+template <> struct Op<ld80, SHMEMX_OP_MAX> {
+    __device__ static ld80 ap(ld80 a, ld80 b) { return x87::greater(a, b) ? a : b; } };
 
 // ------------------------------------------------------- vector plumbing
 // NT: bit 0 = non-temporal loads, bit 1 = non-temporal stores.
@@ -289,15 +302,21 @@ static size_t grid_for(const FoldArgs &a, int unroll) {
 template <typename T, int OP, int NT>
 hipError_t launch_typed(const FoldArgs &a, hipStream_t stream) {
     if (a.nins == 2) {
-        // the two-input fold (reduce-op.c:231-235): the hot kernel
-        const int u = fold_tuning().unroll;
-        const dim3 grid((unsigned)grid_for(a, u));
-        if (u == 2)
-            hipLaunchKernelGGL((fold_kernel<T, OP, 2, 2, NT>), grid, dim3(kBlock), 0, stream, a);
-        else if (u == 8)
-            hipLaunchKernelGGL((fold_kernel<T, OP, 2, 8, NT>), grid, dim3(kBlock), 0, stream, a);
-        else
-            hipLaunchKernelGGL((fold_kernel<T, OP, 2, 4, NT>), grid, dim3(kBlock), 0, stream, a);
+        // the two-input fold (reduce-op.c:231-235): the hot kernel.  The
+        // soft-float long double kernels exist at unroll 4 only.
+        if constexpr (std::is_same<T, ld80>::value) {
+            hipLaunchKernelGGL((fold_kernel<T, OP, 2, 4, NT>), dim3((unsigned)grid_for(a, 4)),
+                               dim3(kBlock), 0, stream, a);
+        } else {
+            const int u = fold_tuning().unroll;
+            const dim3 grid((unsigned)grid_for(a, u));
+            if (u == 2)
+                hipLaunchKernelGGL((fold_kernel<T, OP, 2, 2, NT>), grid, dim3(kBlock), 0, stream, a);
+            else if (u == 8)
+                hipLaunchKernelGGL((fold_kernel<T, OP, 2, 8, NT>), grid, dim3(kBlock), 0, stream, a);
+            else
+                hipLaunchKernelGGL((fold_kernel<T, OP, 2, 4, NT>), grid, dim3(kBlock), 0, stream, a);
+        }
     } else {
         hipLaunchKernelGGL((fold_kernel<T, OP, 0, kUnrollN, NT>), dim3((unsigned)grid_for(a, kUnrollN)),
                            dim3(kBlock), 0, stream, a);
@@ -318,11 +337,15 @@ hipError_t launch_nt(const FoldArgs &a, hipStream_t stream) {
         const size_t n = a.head + a.nvec * (16 / sizeof(T)) + a.tail;
         mode = (size_t)(a.nins + 1) * n * sizeof(T) >= kNtThresholdBytes ? 3 : 0;
     }
-    switch (mode & 3) {
-    case 0: return launch_typed<T, OP, 0>(a, stream);
-    case 1: return launch_typed<T, OP, 1>(a, stream);
-    case 2: return launch_typed<T, OP, 2>(a, stream);
-    default: return launch_typed<T, OP, 3>(a, stream);
+    if constexpr (std::is_same<T, ld80>::value) {  // fewer soft-float variants
+        return mode ? launch_typed<T, OP, 3>(a, stream) : launch_typed<T, OP, 0>(a, stream);
+    } else {
+        switch (mode & 3) {
+        case 0: return launch_typed<T, OP, 0>(a, stream);
+        case 1: return launch_typed<T, OP, 1>(a, stream);
+        case 2: return launch_typed<T, OP, 2>(a, stream);
+        default: return launch_typed<T, OP, 3>(a, stream);
+        }
     }
 }
 
@@ -398,9 +421,7 @@ bool op_valid(int type, int op) {
     }
 }
 
-bool op_on_device(int type, int op) {
-    return op_valid(type, op) && type != SHMEMX_TYPE_LONGDOUBLE;
-}
+bool op_on_device(int type, int op) { return op_valid(type, op); }
 
 hipError_t launch_fold(int type, int op, void *out, const void *const *ins,
                        int nins, size_t n, hipStream_t stream) {
@@ -440,6 +461,7 @@ hipError_t launch_fold(int type, int op, void *out, const void *const *ins,
     case SHMEMX_TYPE_LONGLONG: return launch_int_ops<long>(op, a, stream);
     case SHMEMX_TYPE_FLOAT: return launch_fp_ops<float>(op, a, stream);
     case SHMEMX_TYPE_DOUBLE: return launch_fp_ops<double>(op, a, stream);
+    case SHMEMX_TYPE_LONGDOUBLE: return launch_fp_ops<ld80>(op, a, stream);
     case SHMEMX_TYPE_COMPLEXD: return launch_cplx_ops<cplxd>(op, a, stream);
     case SHMEMX_TYPE_COMPLEXF: return launch_cplx_ops<cplxf>(op, a, stream);
     default: return hipErrorInvalidValue;

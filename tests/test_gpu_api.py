@@ -82,14 +82,16 @@ def test_api_zero_and_invalid(cuda, shm):
     assert shm.last_error() == 1 and (d == 7.0).all()
 
 
-def test_longdouble_is_loud(cuda, shm):
-    """long double has no device kernel in this build: the call must fail
-    visibly (error code + FATAL line), never silently fall back to the CPU."""
-    src = (ctypes.c_longdouble * 4)(1, 2, 3, 4)
-    tgt = (ctypes.c_longdouble * 4)()
-    shm.to_all("longdouble", "sum", ctypes.addressof(tgt), ctypes.addressof(src), 4, 0, 0, 1)
-    assert shm.last_error() == 3
-    assert list(tgt) == [0, 0, 0, 0]
+def test_longdouble_entry_point(cuda, shm, oracle):
+    """shmem_longdouble_*_to_all run on the GPU (soft x87, ld80.h): host
+    arrays at PE_size = 1 copy the value bytes."""
+    src = oracle.fill("longdouble", 1, 5, 1000)
+    tgt = np.zeros_like(src)
+    for op in ("sum", "prod", "min", "max"):
+        tgt[:] = 0
+        shm.to_all("longdouble", op, tgt, src, len(src), 0, 0, 1)
+        assert shm.last_error() == 0
+        assert np.array_equal(tgt, src)
 
 
 def test_reduce_on_stream_torch_stream(cuda, shm, oracle):

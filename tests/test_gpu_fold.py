@@ -11,6 +11,7 @@ Bit-exact for every type/op (floats included: same op order, same IEEE ops).
 """
 import numpy as np
 import pytest
+from gpu_util import from_dev, same_bits, to_dev
 
 pytestmark = pytest.mark.gpu
 
@@ -21,17 +22,10 @@ DEVICE_PAIRS = [
     ("longlong", o) for o in ("sum", "prod", "and", "or", "xor", "min", "max")] + [
     ("float", o) for o in ("sum", "prod", "min", "max")] + [
     ("double", o) for o in ("sum", "prod", "min", "max")] + [
+    ("longdouble", o) for o in ("sum", "prod", "min", "max")] + [
     ("complexd", "sum"), ("complexd", "prod"), ("complexf", "sum"), ("complexf", "prod")]
 
 SIZES = [1, 2, 63, 64, 65, 127, 1000, 4103, 65536 + 13]
-
-
-def to_dev(torch, a):
-    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
-
-
-def same_bits(a: np.ndarray, b: np.ndarray) -> bool:
-    return a.dtype == b.dtype and a.shape == b.shape and a.tobytes() == b.tobytes()
 
 
 @pytest.mark.parametrize("t,op", DEVICE_PAIRS)
@@ -46,7 +40,7 @@ def test_fold_pe_start_order_matches_oracle(cuda, shm, oracle, t, op):
                 out = torch.empty_like(ins[0])
                 shm.fold_n(t, op, out, ins, n)
                 torch.cuda.synchronize()
-                got = out.cpu().numpy()
+                got = from_dev(out, srcs.dtype)
                 assert same_bits(got, want), f"{t} {op} kind={kind} P={P} n={n}"
 
 
@@ -65,7 +59,7 @@ def test_fold_gather_order_every_pe(cuda, shm, oracle, t, op):
         out = torch.empty_like(dev[0])
         shm.fold_n(t, op, out, [dev[p] for p in order], n)
         torch.cuda.synchronize()
-        assert same_bits(out.cpu().numpy(), want[me]), f"PE {me}"
+        assert same_bits(from_dev(out, srcs.dtype), want[me]), f"PE {me}"
 
 
 @pytest.mark.parametrize("t,op", [("double", "sum"), ("int", "xor"), ("short", "max"),
@@ -197,3 +191,50 @@ def test_fold_full_size_double_sum(cuda, shm, oracle):
     lo = n // 2 - 4099
     win = oracle.reduce_sim("double", "sum", np.stack([a[lo:lo + 8192], b[lo:lo + 8192]]), 0, 0, 2)[0]
     assert same_bits(got[lo:lo + 8192], win)
+
+
+def _random_x87(rng, n):
+    """n random 80-bit encodings in 16-byte slots: normals over the whole
+    exponent range and near 1, denormals, pseudo-denormals, zeros, infs,
+    quiet/signalling NaNs, pseudo-NaNs and unnormals, and raw patterns."""
+    sig = rng.integers(0, 2**64, size=n, dtype=np.uint64)
+    exp = rng.integers(0, 0x8000, size=n, dtype=np.uint64)
+    cls = rng.integers(0, 8, size=n)
+    top = np.uint64(1 << 63)
+    sig = np.where(cls == 0, sig | top, sig)                                   # normal
+    exp = np.where(cls == 0, 1 + exp % 0x7FFE, exp)
+    sig = np.where(cls == 1, sig | top, sig)                                   # near 1.0
+    exp = np.where(cls == 1, 16380 + exp % 7, exp)
+    exp = np.where(cls == 2, 0, exp)                                           # denormal / pseudo
+    sig = np.where(cls == 3, top, sig)                                         # inf
+    exp = np.where(cls == 3, 0x7FFF, exp)
+    sig = np.where(cls == 4, sig | top, sig)                                   # NaN
+    exp = np.where(cls == 4, 0x7FFF, exp)
+    sig = np.where(cls == 5, 0, sig)                                           # zero
+    exp = np.where(cls == 5, 0, exp)
+    sign = rng.integers(0, 2, size=n, dtype=np.uint64) << np.uint64(15)
+    slots = np.zeros((n, 2), dtype=np.uint64)
+    slots[:, 0] = sig
+    slots[:, 1] = exp | sign
+    return slots.view(np.longdouble).reshape(n)
+
+
+def test_longdouble_x87_encodings(cuda, shm, oracle):
+    """The soft x87 on the GPU against the host x87 (through the oracle) over
+    random 80-bit encodings, every op, both PE orders, value bytes exact."""
+    import torch
+    rng = np.random.default_rng(87)
+    n = 1 << 16
+    a, b = _random_x87(rng, n), _random_x87(rng, n)
+    b[: n // 4] = a[: n // 4]                       # equal operands
+    b[n // 4: n // 2] = -a[n // 4: n // 2]          # exact cancellation
+    srcs = np.stack([a, b])
+    for op in ("sum", "prod", "min", "max"):
+        for order in ((0, 1), (1, 0)):
+            want = oracle.reduce_sim("longdouble", op, srcs[list(order)], 0, 0, 2)[0]
+            out = torch.zeros(n * 16, dtype=torch.uint8, device="cuda")
+            shm.fold_n("longdouble", op, out, [to_dev(torch, srcs[order[0]]),
+                                               to_dev(torch, srcs[order[1]])], n)
+            torch.cuda.synchronize()
+            got = from_dev(out, np.longdouble)
+            assert same_bits(got, want), (op, order)

@@ -12,6 +12,7 @@ import os
 
 import numpy as np
 import pytest
+from gpu_util import from_dev, to_dev
 
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
@@ -32,7 +33,7 @@ def test_gpu_reproduces_golden_hashes(cuda, shm, oracle):
             continue
         seed = 0x5EED0000 + 1009 * list(oracle.TYPES).index(t) + n
         srcs = oracle.sources(t, kind, npes, n, base_seed=seed)
-        dev = [torch.from_numpy(srcs[p]).cuda() for p in range(npes)]
+        dev = [to_dev(torch, srcs[p]) for p in range(npes)]
         out = torch.empty_like(dev[0])
         for op, sset, want in cases:
             if not shm.op_on_device(t, op):
@@ -42,11 +43,11 @@ def test_gpu_reproduces_golden_hashes(cuda, shm, oracle):
             for me in mem:
                 order = [me] + [p for p in mem if p != me]
                 shm.fold_n(t, op, out, [dev[p] for p in order], n)
-                got = out.cpu().numpy()
+                got = from_dev(out, srcs.dtype)
                 assert f"{oracle.value_hash(t, got):016x}" == want[me], (t, op, kind, n, s, me)
                 checked += 1
             shm.fold_n(t, op, out, [dev[p] for p in mem], n)
-            got = out.cpu().numpy()
+            got = from_dev(out, srcs.dtype)
             assert f"{oracle.value_hash(t, got):016x}" == want[mem[0]], (t, op, kind, n, s, "a2a")
     assert checked > 10000
 
