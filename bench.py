@@ -258,7 +258,7 @@ def main():
                     "busbw_GBps": round(achieved, 1),
                     "algbw_GiBps": round(nbytes / t_call / GiB, 2)}
         if a.extras:
-            for alt in ("rccl", "a2a", "gather"):
+            for alt in ("rccl", "allreduce", "a2a", "gather"):
                 if alt == algo_used:
                     continue
                 def alt_step(alt=alt):

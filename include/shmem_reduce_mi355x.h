@@ -164,10 +164,11 @@ enum {
  *           shards in active-set order -> shard all-gather; any set, any op;
  *           every PE gets the reference's PE_start result bit for bit
  *   GATHER  every PE receives every source and folds in its own reference
- *           order: bit-exact with the reference on EVERY PE, (P-1)x traffic */
+ *           order: bit-exact with the reference on EVERY PE, (P-1)x traffic
+ *   ALLREDUCE  one ncclAllReduce (full set, RCCL-native pairs, as RCCL) */
 enum {
     SHMEMX_ALGO_AUTO = 0, SHMEMX_ALGO_RCCL, SHMEMX_ALGO_A2A,
-    SHMEMX_ALGO_GATHER, SHMEMX_NALGOS
+    SHMEMX_ALGO_GATHER, SHMEMX_ALGO_ALLREDUCE, SHMEMX_NALGOS
 };
 
 /* Error codes returned by shmemx_* and stored for shmemx_reduce_last_error. */
@@ -193,7 +194,7 @@ int shmemx_initialized(void);
 void *shmemx_get_stream(void);
 
 /* Algorithm used by the entry points (default AUTO, or $SHMEM_REDUCE_ALGO =
- * auto|rccl|a2a|gather).  Returns the previous value. */
+ * auto|rccl|a2a|gather|allreduce).  Returns the previous value. */
 int shmemx_set_algo(int algo);
 
 /* Stream-ordered reduction: enqueue on `stream` (hipStream_t; NULL = the

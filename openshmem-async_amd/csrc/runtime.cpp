@@ -42,6 +42,10 @@ struct State {
     hipStream_t stream = nullptr;
     ncclComm_t comm = nullptr;
     int algo = SHMEMX_ALGO_AUTO;
+    // test hook ($SHMEMX_FORCE_COLLECTIVE=1): a 1-PE job still builds an RCCL
+    // communicator and runs the collective schedules, so a one-GPU box can
+    // execute every RCCL call of the path
+    bool force_collective = false;
     // grow-only device workspaces
     void *ws = nullptr;        // A2A shard receive area / GATHER sources
     size_t ws_bytes = 0;
@@ -107,6 +111,7 @@ static int parse_algo(const char *s) {
     if (v == "rccl") return SHMEMX_ALGO_RCCL;
     if (v == "a2a") return SHMEMX_ALGO_A2A;
     if (v == "gather") return SHMEMX_ALGO_GATHER;
+    if (v == "allreduce") return SHMEMX_ALGO_ALLREDUCE;
     return SHMEMX_ALGO_AUTO;
 }
 
@@ -124,11 +129,16 @@ static int init_locked(int pe, int npes, int device, const void *uid) {
     // then hands to the blocking entry points.  Work on other non-blocking
     // streams must be synchronised by the caller, as for any HIP library.
     SHMX_HIP(hipStreamCreate(&g_state.stream));
+    g_state.force_collective = env_int("SHMEMX_FORCE_COLLECTIVE", nullptr, 0) != 0;
     if (npes > 1) {
         if (!uid) return set_error(SHMEMX_EINVAL);
         ncclUniqueId id;
         std::memcpy(&id, uid, sizeof id);
         SHMX_NCCL(ncclCommInitRank(&g_state.comm, npes, id, pe));
+    } else if (g_state.force_collective) {
+        ncclUniqueId id;
+        SHMX_NCCL(ncclGetUniqueId(&id));
+        SHMX_NCCL(ncclCommInitRank(&g_state.comm, 1, id, 0));
     }
     g_state.pe = pe;
     g_state.npes = npes;
@@ -255,12 +265,14 @@ static int make_plan(int type, int op, int nreduce, int start, int logstride,
     const bool world = start == 0 && (logstride == 0 || size == 1) && size == npes;
     if (algo == SHMEMX_ALGO_AUTO)
         algo = (world && rccl_native(type, op)) ? SHMEMX_ALGO_RCCL : SHMEMX_ALGO_A2A;
-    if (algo == SHMEMX_ALGO_RCCL && !(world && rccl_native(type, op))) return SHMEMX_ENOTSUP;
+    if ((algo == SHMEMX_ALGO_RCCL || algo == SHMEMX_ALGO_ALLREDUCE) &&
+        !(world && rccl_native(type, op)))
+        return SHMEMX_ENOTSUP;
     p->algo = algo;
     p->member = m;
     p->nmembers = P;
     p->elem_size = sz;
-    if (P == 1) {
+    if (P == 1 && !g_state.force_collective) {
         p->chunk = n;
         return SHMEMX_OK;
     }
@@ -269,6 +281,10 @@ static int make_plan(int type, int op, int nreduce, int start, int logstride,
         p->chunk = (n / (P * g)) * g;
         p->main = p->chunk * P;
         p->tail = n - p->main;
+        break;
+    case SHMEMX_ALGO_ALLREDUCE:
+        p->chunk = n;
+        p->main = n;
         break;
     case SHMEMX_ALGO_A2A: {
         long long c = (n + P - 1) / P;
@@ -290,7 +306,8 @@ static int make_plan(int type, int op, int nreduce, int start, int logstride,
 static void *grow(void *&buf, size_t &have, size_t need) {
     if (need <= have) return buf;
     if (buf) {
-        SHMX_HIP(hipStreamSynchronize(g_state.stream));
+        // the old buffer may still be in use on any caller stream
+        SHMX_HIP(hipDeviceSynchronize());
         SHMX_HIP(hipFree(buf));
         buf = nullptr;
         have = 0;
@@ -355,7 +372,7 @@ static int reduce_device(int type, int op, void *target, const void *source,
     }
 
     const int P = size, m = p.member, step = 1 << logstride;
-    if (P == 1) {  // reduce-op.c:213-216 with no peers: a copy
+    if (P == 1 && !g_state.force_collective) {  // reduce-op.c:213-216, no peers: a copy
         if (tgt != src) {
             const void *in[1] = {src};
             fold_chain(type, op, tgt, in, 1, (size_t)nreduce, s);
@@ -364,6 +381,12 @@ static int reduce_device(int type, int op, void *target, const void *source,
     }
     auto peer = [&](int i) { return start + i * step; };
 
+    if (p.algo == SHMEMX_ALGO_ALLREDUCE) {  // one RCCL all-reduce, in place allowed
+        ncclDataType_t dt;
+        rccl_dtype(type, &dt);
+        SHMX_NCCL(ncclAllReduce(src, tgt, (size_t)nreduce, dt, rccl_op(op), g_state.comm, s));
+        return SHMEMX_OK;
+    }
     if (p.algo == SHMEMX_ALGO_RCCL) {
         ncclDataType_t dt;
         rccl_dtype(type, &dt);
@@ -484,7 +507,7 @@ void reduce_blocking(int type, int op, void *target, const void *source,
     }
     // Host-resident symmetric arrays (the reference's heap): stage over PCIe.
     if (bytes > g_state.stage_bytes) {
-        SHMX_HIP(hipStreamSynchronize(s));
+        SHMX_HIP(hipDeviceSynchronize());
         if (g_state.stage_src) SHMX_HIP(hipFree(g_state.stage_src));
         if (g_state.stage_tgt) SHMX_HIP(hipFree(g_state.stage_tgt));
         g_state.stage_src = g_state.stage_tgt = nullptr;

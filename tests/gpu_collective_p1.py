@@ -1,0 +1,37 @@
+"""Child process for test_gpu_api.py::test_rccl_schedules_one_rank: with
+SHMEMX_FORCE_COLLECTIVE=1 a one-PE job runs the full RCCL / ALLREDUCE / A2A /
+GATHER schedules (RCCL communicator of one rank), so every RCCL call of the
+path executes on a one-GPU box.  Prints "ok" or raises."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "openshmem-async_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import oracle  # noqa: E402
+import shmem_mi355x as shm  # noqa: E402
+
+assert os.environ.get("SHMEMX_FORCE_COLLECTIVE") == "1"
+torch.cuda.set_device(0)
+shm.init_attr(0, 1, 0, None)
+for t, op, algos in [("double", "sum", ("rccl", "allreduce", "a2a", "gather")),
+                     ("int", "max", ("rccl", "allreduce", "a2a", "gather")),
+                     ("long", "xor", ("a2a", "gather")),
+                     ("complexf", "prod", ("a2a", "gather")),
+                     ("longdouble", "min", ("a2a", "gather"))]:
+    for n in (1, 7, 4103, 1 << 20):
+        src = oracle.fill(t, 1, 3, n)
+        for algo in algos:
+            raw = src.view(np.uint8) if t == "longdouble" else src
+            s = torch.from_numpy(raw.copy()).cuda()
+            d = torch.zeros_like(s)
+            shm.reduce_on_stream(t, op, d, s, n, 0, 0, 1, algo)
+            torch.cuda.synchronize()
+            assert d.cpu().numpy().tobytes() == raw.tobytes(), (t, op, n, algo)
+            shm.reduce_on_stream(t, op, s, s, n, 0, 0, 1, algo)       # in place
+            torch.cuda.synchronize()
+            assert s.cpu().numpy().tobytes() == raw.tobytes(), (t, op, n, algo, "in place")
+print("ok")

@@ -6,6 +6,7 @@ host-resident arrays (the reference's symmetric heap is host memory,
 memory/symmem.c:168-227), in place or not, and pWrk/pSync are left alone.
 """
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -154,3 +155,15 @@ def test_fortran_forwarder(cuda, shm, oracle):
     assert shm.last_error() == 0
     assert d.cpu().numpy().tobytes() == src.tobytes()
     assert (psync == -1).all()
+
+
+def test_rccl_schedules_one_rank(cuda):
+    """Every RCCL call of the multi-PE path (reduce-scatter, all-gather,
+    all-reduce, grouped send/recv schedules) on a one-rank communicator."""
+    import subprocess
+    import sys
+    env = dict(os.environ, SHMEMX_FORCE_COLLECTIVE="1")
+    here = os.path.dirname(os.path.abspath(__file__))
+    out = subprocess.run([sys.executable, os.path.join(here, "gpu_collective_p1.py")],
+                         env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and out.stdout.strip().endswith("ok"), out.stdout + out.stderr
