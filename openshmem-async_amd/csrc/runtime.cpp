@@ -54,10 +54,16 @@ struct State {
     void *stage_src = nullptr; // host-resident endpoints
     void *stage_tgt = nullptr;
     size_t stage_bytes = 0;
+    hipStream_t h2d = nullptr;  // staging copy streams and their chunk events
+    hipStream_t d2h = nullptr;
+    std::vector<hipEvent_t> events;
     std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
 };
 
 static State g_state;
+
+// Host-resident arrays move over PCIe in chunks of this size (pipelined).
+constexpr size_t kStageChunkBytes = size_t(16) << 20;
 static std::recursive_mutex g_mu;
 static thread_local int t_last_error = SHMEMX_OK;
 
@@ -466,6 +472,18 @@ static bool device_accessible(const void *ptr) {
     return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
 }
 
+// Page-locked host memory (hipHostMalloc / hipHostRegister): DMA-able, so
+// chunked copies overlap; pageable memory is copied through HIP's own
+// staging, where chunking only adds overhead (measured).
+static bool host_pinned(const void *ptr) {
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, ptr) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return attr.type == hipMemoryTypeHost;
+}
+
 }  // namespace shmx
 
 // ------------------------------------------------------------- internal API
@@ -505,7 +523,20 @@ void reduce_blocking(int type, int op, void *target, const void *source,
         SHMX_HIP(hipStreamSynchronize(s));
         return;
     }
-    // Host-resident symmetric arrays (the reference's heap): stage over PCIe.
+    // Host-resident symmetric arrays (the reference's heap): stage over PCIe
+    // in chunks, H2D on one copy stream, the reduction on the library stream,
+    // D2H on a second copy stream, so the two PCIe directions and the device
+    // work overlap.  Every PE cuts the same chunks, so the collective
+    // sequence matches across PEs.
+    {
+        shmemx_plan_t p;
+        const int rc = make_plan(type, op, nreduce, start, logstride, size, g_state.pe,
+                                 g_state.npes, g_state.algo, &p);
+        if (rc) {
+            set_error(rc);
+            return;
+        }
+    }
     if (bytes > g_state.stage_bytes) {
         SHMX_HIP(hipDeviceSynchronize());
         if (g_state.stage_src) SHMX_HIP(hipFree(g_state.stage_src));
@@ -520,17 +551,52 @@ void reduce_blocking(int type, int op, void *target, const void *source,
         }
         g_state.stage_bytes = bytes;
     }
-    const void *dsrc = source;
-    if (!sdev) {
-        SHMX_HIP(hipMemcpyAsync(g_state.stage_src, source, bytes, hipMemcpyHostToDevice, s));
-        dsrc = g_state.stage_src;
+    if (!g_state.h2d) {
+        SHMX_HIP(hipStreamCreateWithFlags(&g_state.h2d, hipStreamNonBlocking));
+        SHMX_HIP(hipStreamCreateWithFlags(&g_state.d2h, hipStreamNonBlocking));
     }
-    void *dtgt = tdev ? target : g_state.stage_tgt;
-    const int rc = reduce_device(type, op, dtgt, dsrc, nreduce, start, logstride, size,
-                                 g_state.algo, s);
-    if (!rc && !tdev)
-        SHMX_HIP(hipMemcpyAsync(target, dtgt, bytes, hipMemcpyDeviceToHost, s));
+    const size_t sz = type_size(type);
+    const size_t g = sz >= 16 ? 1 : 16 / sz;
+    size_t chunk = ((kStageChunkBytes / sz) / g) * g;
+    if (chunk == 0) chunk = g;
+    // a host target that partially overlaps the host source would be
+    // overwritten under a later chunk's H2D: no pipelining then
+    if (!tdev && !sdev && overlap(target, source, bytes)) chunk = (size_t)nreduce;
+    if ((!tdev && !host_pinned(target)) || (!sdev && !host_pinned(source)))
+        chunk = (size_t)nreduce;
+    const size_t nchunks = ((size_t)nreduce + chunk - 1) / chunk;
+    while (g_state.events.size() < 2 * nchunks) {
+        hipEvent_t e;
+        SHMX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        g_state.events.push_back(e);
+    }
+    char *hsrc = static_cast<char *>(const_cast<void *>(source));
+    char *htgt = static_cast<char *>(target);
+    char *ssrc = static_cast<char *>(g_state.stage_src);
+    char *stgt = static_cast<char *>(g_state.stage_tgt);
+    int rc = SHMEMX_OK;
+    for (size_t k = 0; k < nchunks && !rc; ++k) {
+        const size_t off = k * chunk * sz;
+        const size_t cnt = std::min(chunk, (size_t)nreduce - k * chunk);
+        const size_t b = cnt * sz;
+        const void *dsrc = hsrc + off;
+        if (!sdev) {
+            SHMX_HIP(hipMemcpyAsync(ssrc + off, hsrc + off, b, hipMemcpyHostToDevice, g_state.h2d));
+            SHMX_HIP(hipEventRecord(g_state.events[2 * k], g_state.h2d));
+            SHMX_HIP(hipStreamWaitEvent(s, g_state.events[2 * k], 0));
+            dsrc = ssrc + off;
+        }
+        void *dtgt = tdev ? static_cast<void *>(htgt + off) : static_cast<void *>(stgt + off);
+        rc = reduce_device(type, op, dtgt, dsrc, (int)cnt, start, logstride, size, g_state.algo, s);
+        if (!rc && !tdev) {
+            SHMX_HIP(hipEventRecord(g_state.events[2 * k + 1], s));
+            SHMX_HIP(hipStreamWaitEvent(g_state.d2h, g_state.events[2 * k + 1], 0));
+            SHMX_HIP(hipMemcpyAsync(htgt + off, dtgt, b, hipMemcpyDeviceToHost, g_state.d2h));
+        }
+    }
+    SHMX_HIP(hipStreamSynchronize(g_state.h2d));
     SHMX_HIP(hipStreamSynchronize(s));
+    SHMX_HIP(hipStreamSynchronize(g_state.d2h));
 }
 
 int reduce_on_stream(int type, int op, void *target, const void *source,
@@ -581,6 +647,12 @@ void pshmem_finalize(void) {
         *b = nullptr;
     }
     g_state.ws_bytes = g_state.tmp_bytes = g_state.stage_bytes = 0;
+    for (hipEvent_t e : g_state.events) (void)hipEventDestroy(e);
+    g_state.events.clear();
+    for (hipStream_t *st : {&g_state.h2d, &g_state.d2h}) {
+        if (*st) (void)hipStreamDestroy(*st);
+        *st = nullptr;
+    }
     (void)hipStreamDestroy(g_state.stream);
     g_state.stream = nullptr;
     g_state.inited = false;

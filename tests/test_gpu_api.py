@@ -167,3 +167,30 @@ def test_rccl_schedules_one_rank(cuda):
     out = subprocess.run([sys.executable, os.path.join(here, "gpu_collective_p1.py")],
                          env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0 and out.stdout.strip().endswith("ok"), out.stdout + out.stderr
+
+
+@pytest.mark.parametrize("t", ["double", "short", "complexd", "longdouble"])
+def test_host_staging_pipeline_many_chunks(cuda, shm, oracle, t):
+    """Host-resident arrays larger than one 16 MiB staging chunk, every
+    combination of host/device endpoints, in place, and a partial overlap."""
+    import torch
+    from gpu_util import from_dev, to_dev
+    isz = np.dtype(oracle.NP_DTYPE[t]).itemsize
+    n = (48 << 20) // isz + 5
+    src = oracle.fill(t, 1, 21, n)
+    for tgt_host, src_host in ((True, True), (True, False), (False, True)):
+        s = src if src_host else to_dev(torch, src)
+        if tgt_host:
+            d = np.zeros_like(src)
+        else:
+            d = to_dev(torch, np.zeros_like(src))
+        shm.to_all(t, "sum", d, s, n, 0, 0, 1)
+        assert shm.last_error() == 0
+        got = d if tgt_host else from_dev(d, src.dtype)
+        assert got.tobytes() == src.tobytes(), (tgt_host, src_host)
+    buf = src.copy()
+    shm.to_all(t, "prod", buf, buf, n, 0, 0, 1)                     # in place, host
+    assert buf.tobytes() == src.tobytes()
+    big = np.concatenate([src, src[:7]])
+    shm.to_all(t, "sum", big[3:].ctypes.data, big.ctypes.data, n, 0, 0, 1)   # overlap
+    assert big[3:3 + n].tobytes() == src.tobytes()
