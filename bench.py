@@ -119,6 +119,43 @@ def host_e2e(n: int):
     return res
 
 
+def config_extras(world, stream, barrier, max_over_ranks):
+    """BASELINE.json configs[3] and [4] as extra lines (not `value`):
+    long and/or/xor over 64 Mi elements, and the float sum GiB/s-vs-size curve
+    for nreduce 4 Ki .. 256 Mi.  At N = 1 the step is the local fold (2
+    inputs), at N > 1 the full collective."""
+    sp = stream.cuda_stream
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0xC0F + int(os.environ.get("RANK", "0")))
+    out = {}
+
+    def rate(type_name, op, n, elem, steps):
+        x = (torch.randint(-2**62, 2**62, (n,), dtype=torch.int64, device="cuda", generator=g)
+             if elem == 8 and type_name == "long" else
+             torch.rand(n, dtype=torch.float32, device="cuda", generator=g))
+        y = torch.empty_like(x)
+        torch.cuda.synchronize()
+        if world == 1:
+            fn = lambda: shm.fold(type_name, op, y, x, n, sp)          # noqa: E731
+        else:
+            fn = lambda: shm.reduce_on_stream(type_name, op, y, x, n, 0, 0, world, "auto", sp)  # noqa: E731
+        for _ in range(2):
+            fn()
+        w, _ = time_region(fn, steps, stream, barrier)
+        w = max_over_ranks(w)
+        return round(world * n * elem * steps / w / GiB, 2)
+
+    for op in ("and", "or", "xor"):
+        out[f"long_{op}_64Mi_GiBps"] = rate("long", op, 64 * 1024 * 1024, 8, 10)
+    curve = {}
+    n = 4 * 1024
+    while n <= 256 * 1024 * 1024:
+        curve[str(n)] = rate("float", "sum", n, 4, 20 if n >= 1 << 24 else 50)
+        n *= 4
+    out["float_sum_GiBps_vs_nreduce"] = curve
+    return out
+
+
 def time_region(fn, steps, stream, barrier):
     """Run fn() `steps` times on `stream`; returns (wall_s, event_s)."""
     barrier()
@@ -246,6 +283,7 @@ def main():
                 "hbm_GBps": round(2 * nbytes / (e2 / k2) / 1e9, 1),
                 "us_per_call": round(e2 / k2 * 1e6, 2)}
             extras["host_resident_e2e"] = host_e2e(n)
+            extras["configs"] = config_extras(world, stream, barrier, max_over_ranks)
     else:
         t_call = ev / a.steps
         xgmi_bytes = 2 * (world - 1) / world * nbytes        # per GPU, RS + AG
@@ -272,6 +310,7 @@ def main():
                     extras[f"algo_{alt}_GiBps"] = round(world * nbytes * k3 / w3 / GiB, 2)
                 except shm.ShmemError as e:
                     extras[f"algo_{alt}_GiBps"] = str(e)
+            extras["configs"] = config_extras(world, stream, barrier, max_over_ranks)
 
     cpu = None
     if world == 1 and rank == 0 and not a.no_cpu_baseline:
