@@ -142,6 +142,42 @@ int pshmem_my_pe(void);
 int pshmem_n_pes(void);
 
 /* ------------------------------------------------------------------------ */
+/* Part 2b: the collectives next to the reductions and the symmetric heap   */
+/* (SURVEY.md §8f).  Reference prototypes: shmem.h:595-651 (barrier),       */
+/* :1654-1684 (broadcast, [f]collect), :821-941 (symmetric heap).  The heap */
+/* is HBM: shmem_malloc returns device memory, collectively.                */
+
+#ifndef SHMEM_BCAST_SYNC_SIZE
+#define SHMEM_BCAST_SYNC_SIZE   64L
+#define SHMEM_BARRIER_SYNC_SIZE 64L
+#define SHMEM_COLLECT_SYNC_SIZE 64L
+#endif
+
+#define SHMEMX_DECL_BOTH(ret, name, args) ret name args; ret p##name args;
+SHMEMX_DECL_BOTH(void, shmem_barrier, (int PE_start, int logPE_stride, int PE_size, long *pSync))
+SHMEMX_DECL_BOTH(void, shmem_barrier_all, (void))
+SHMEMX_DECL_BOTH(void, shmem_broadcast32, (void *target, const void *source, size_t nelems,
+                 int PE_root, int PE_start, int logPE_stride, int PE_size, long *pSync))
+SHMEMX_DECL_BOTH(void, shmem_broadcast64, (void *target, const void *source, size_t nelems,
+                 int PE_root, int PE_start, int logPE_stride, int PE_size, long *pSync))
+SHMEMX_DECL_BOTH(void, shmem_fcollect32, (void *target, const void *source, size_t nelems,
+                 int PE_start, int logPE_stride, int PE_size, long *pSync))
+SHMEMX_DECL_BOTH(void, shmem_fcollect64, (void *target, const void *source, size_t nelems,
+                 int PE_start, int logPE_stride, int PE_size, long *pSync))
+SHMEMX_DECL_BOTH(void, shmem_collect32, (void *target, const void *source, size_t nelems,
+                 int PE_start, int logPE_stride, int PE_size, long *pSync))
+SHMEMX_DECL_BOTH(void, shmem_collect64, (void *target, const void *source, size_t nelems,
+                 int PE_start, int logPE_stride, int PE_size, long *pSync))
+SHMEMX_DECL_BOTH(void *, shmem_malloc, (size_t size))
+SHMEMX_DECL_BOTH(void *, shmem_align, (size_t alignment, size_t size))
+SHMEMX_DECL_BOTH(void, shmem_free, (void *ptr))
+SHMEMX_DECL_BOTH(void *, shmem_realloc, (void *ptr, size_t size))
+SHMEMX_DECL_BOTH(void *, shmalloc, (size_t size))
+SHMEMX_DECL_BOTH(void, shfree, (void *ptr))
+SHMEMX_DECL_BOTH(void *, shrealloc, (void *ptr, size_t size))
+SHMEMX_DECL_BOTH(void *, shmemalign, (size_t alignment, size_t size))
+
+/* ------------------------------------------------------------------------ */
 /* Part 3: extensions.                                                      */
 
 /* Type and op codes. */

@@ -1,0 +1,396 @@
+// The collectives next to the reduction path, built
+// on the same runtime (one PE per GPU, one RCCL communicator, the library's
+// blocking stream):
+//
+//   shmem_barrier / shmem_barrier_all   barrier/barrier.c:74-127,
+//                                       barrier-linear.c:51-77
+//   shmem_broadcast32/64                broadcast/broadcast-linear.c:54-74
+//   shmem_fcollect32/64                 fcollect/fcollect-linear.c:69-91
+//   shmem_collect32/64                  collect/collect-linear.c:57-130
+//   shmem_malloc/free/realloc/align     memory/symmem.c:168-227 (+ the
+//   (and shmalloc/shfree/shrealloc/     deprecated names, shmem.h:821-941)
+//   shmemalign)
+//
+// Full active set: RCCL collectives (ncclBroadcast, ncclAllGather,
+// ncclAllReduce for the barrier token).  Any other set: grouped
+// ncclSend/ncclRecv between its members only (the members alone call, as in
+// OpenSHMEM, so no sub-communicator is needed).  Host buffers are staged
+// through device workspaces; pSync is never written.
+//
+// The symmetric heap is HBM: shmem_malloc returns device memory (hipMalloc),
+// collectively (a barrier_all follows, symmem.c:209), so a program keeps its
+// symmetric arrays resident on the GPU and the reductions take the
+// device-resident path.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include "internal.h"
+#include "shmem_reduce_mi355x.h"
+#include "state.h"
+
+namespace shmx {
+
+namespace {
+
+struct SetInfo {
+    int P = 0, m = -1, step = 1, start = 0;
+    bool world = false;
+    int peer(int i) const { return start + i * step; }
+};
+
+// Validate (PE_start, logPE_stride, PE_size) and the caller's membership.
+int set_info(int start, int logstride, int size, SetInfo &si) {
+    if (int rc = ensure_init()) return rc;
+    if (start < 0 || logstride < 0 || logstride > 30 || size < 1) return set_error(SHMEMX_EINVAL);
+    if ((long long)start + (long long)(size - 1) * (1LL << logstride) >= g_state.npes)
+        return set_error(SHMEMX_EINVAL);
+    si.P = size;
+    si.start = start;
+    si.step = 1 << logstride;
+    si.world = start == 0 && (logstride == 0 || size == 1) && size == g_state.npes;
+    if (!is_member(g_state.pe, start, logstride, size, &si.m)) return set_error(SHMEMX_ENOTMEMBER);
+    if ((size > 1 || g_state.force_collective) && !g_state.comm) return set_error(SHMEMX_ENOINIT);
+    return SHMEMX_OK;
+}
+
+bool collective(const SetInfo &si) { return si.P > 1 || g_state.force_collective; }
+
+// A device view of a possibly host-resident buffer.
+struct DevBuf {
+    char *dev = nullptr;
+    char *host = nullptr;   // non-null: staged, copy back to here
+    size_t bytes = 0;
+};
+
+DevBuf device_in(const void *p, size_t bytes, void *&ws, size_t &ws_bytes, hipStream_t s) {
+    DevBuf b;
+    b.bytes = bytes;
+    if (!bytes || device_accessible(p)) {
+        b.dev = static_cast<char *>(const_cast<void *>(p));
+        return b;
+    }
+    b.dev = static_cast<char *>(grow(ws, ws_bytes, bytes));
+    if (!b.dev) return b;
+    SHMX_HIP(hipMemcpyAsync(b.dev, p, bytes, hipMemcpyHostToDevice, s));
+    return b;
+}
+
+DevBuf device_out(void *p, size_t bytes, void *&ws, size_t &ws_bytes) {
+    DevBuf b;
+    b.bytes = bytes;
+    if (!bytes || device_accessible(p)) {
+        b.dev = static_cast<char *>(p);
+        return b;
+    }
+    b.dev = static_cast<char *>(grow(ws, ws_bytes, bytes));
+    b.host = static_cast<char *>(p);
+    return b;
+}
+
+void finish(const DevBuf &out, hipStream_t s) {
+    if (out.host && out.dev)
+        SHMX_HIP(hipMemcpyAsync(out.host, out.dev, out.bytes, hipMemcpyDeviceToHost, s));
+    SHMX_HIP(hipStreamSynchronize(s));
+}
+
+// Device token area for barriers (one byte per member, grown as needed).
+char *token_area(int P) {
+    return static_cast<char *>(grow(g_state.token, g_state.token_bytes,
+                                    (size_t)(P < 64 ? 64 : P) + 64));
+}
+
+int barrier_impl(int start, int logstride, int size) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    clear_error();
+    SetInfo si;
+    if (int rc = set_info(start, logstride, size, si)) return rc;
+    hipStream_t s = g_state.stream;
+    // quiet: everything this PE enqueued before the barrier is complete
+    SHMX_HIP(hipStreamSynchronize(s));
+    if (!collective(si)) return SHMEMX_OK;
+    char *tok = token_area(si.P);
+    if (!tok) return set_error(SHMEMX_ENOMEM);
+    if (si.world) {
+        SHMX_NCCL(ncclAllReduce(tok, tok, 1, ncclUint8, ncclMax, g_state.comm, s));
+    } else {
+        // every member hears from every other member (one byte each way)
+        SHMX_NCCL(ncclGroupStart());
+        for (int i = 0; i < si.P; ++i) {
+            if (i == si.m) continue;
+            SHMX_NCCL(ncclSend(tok, 1, ncclUint8, si.peer(i), g_state.comm, s));
+            SHMX_NCCL(ncclRecv(tok + 64 + i, 1, ncclUint8, si.peer(i), g_state.comm, s));
+        }
+        SHMX_NCCL(ncclGroupEnd());
+    }
+    SHMX_HIP(hipStreamSynchronize(s));
+    return SHMEMX_OK;
+}
+
+int broadcast_impl(size_t esize, void *target, const void *source, size_t nelems, int root_idx,
+                   int start, int logstride, int size) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    clear_error();
+    SetInfo si;
+    if (int rc = set_info(start, logstride, size, si)) return rc;
+    if (root_idx < 0 || root_idx >= size) return set_error(SHMEMX_EINVAL);
+    const size_t bytes = nelems * esize;
+    if (!bytes || !collective(si)) return SHMEMX_OK;  // the root's target is never written
+    if ((si.m == root_idx && !source) || (si.m != root_idx && !target)) return set_error(SHMEMX_EINVAL);
+    hipStream_t s = g_state.stream;
+    const int root = si.peer(root_idx);
+    const bool is_root = si.m == root_idx;
+    DevBuf in, out;
+    if (is_root) {
+        in = device_in(source, bytes, g_state.cws_src, g_state.cws_src_bytes, s);
+        if (!in.dev) return set_error(SHMEMX_ENOMEM);
+    } else {
+        out = device_out(target, bytes, g_state.cws_tgt, g_state.cws_tgt_bytes);
+        if (!out.dev) return set_error(SHMEMX_ENOMEM);
+    }
+    if (si.world) {
+        // in place on the root (sendbuff == recvbuff): its target is untouched
+        char *buf = is_root ? in.dev : out.dev;
+        SHMX_NCCL(ncclBroadcast(buf, buf, bytes, ncclUint8, root, g_state.comm, s));
+    } else {
+        SHMX_NCCL(ncclGroupStart());
+        if (is_root) {
+            for (int i = 0; i < si.P; ++i)
+                if (i != si.m) SHMX_NCCL(ncclSend(in.dev, bytes, ncclUint8, si.peer(i), g_state.comm, s));
+        } else {
+            SHMX_NCCL(ncclRecv(out.dev, bytes, ncclUint8, root, g_state.comm, s));
+        }
+        SHMX_NCCL(ncclGroupEnd());
+    }
+    finish(out, s);
+    return SHMEMX_OK;
+}
+
+// fcollect (equal counts) and collect (per-PE counts): member i's source
+// lands at element offset off[i] of every member's target, in set order.
+int collect_impl(size_t esize, void *target, const void *source, size_t nelems, int start,
+                 int logstride, int size, bool fixed) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    clear_error();
+    SetInfo si;
+    if (int rc = set_info(start, logstride, size, si)) return rc;
+    hipStream_t s = g_state.stream;
+    std::vector<long long> counts(si.P, (long long)nelems);
+    if (!fixed && collective(si)) {
+        // every member's count (the reference passes it down a chain of
+        // shmem_long_p, collect-linear.c:83-110)
+        long long *cnt = static_cast<long long *>(grow(g_state.token, g_state.token_bytes,
+                                                       sizeof(long long) * (si.P + 8)));
+        if (!cnt) return set_error(SHMEMX_ENOMEM);
+        const long long mine = (long long)nelems;
+        SHMX_HIP(hipMemcpyAsync(cnt + si.m, &mine, sizeof mine, hipMemcpyHostToDevice, s));
+        if (si.world) {
+            SHMX_NCCL(ncclAllGather(cnt + si.m, cnt, 1, ncclInt64, g_state.comm, s));
+        } else {
+            SHMX_NCCL(ncclGroupStart());
+            for (int i = 0; i < si.P; ++i) {
+                if (i == si.m) continue;
+                SHMX_NCCL(ncclSend(cnt + si.m, 1, ncclInt64, si.peer(i), g_state.comm, s));
+                SHMX_NCCL(ncclRecv(cnt + i, 1, ncclInt64, si.peer(i), g_state.comm, s));
+            }
+            SHMX_NCCL(ncclGroupEnd());
+        }
+        SHMX_HIP(hipMemcpyAsync(counts.data(), cnt, sizeof(long long) * si.P,
+                                hipMemcpyDeviceToHost, s));
+        SHMX_HIP(hipStreamSynchronize(s));
+    }
+    std::vector<size_t> off(si.P + 1, 0);
+    for (int i = 0; i < si.P; ++i) off[i + 1] = off[i] + (size_t)counts[i] * esize;
+    const size_t mine = (size_t)counts[si.m] * esize, total = off[si.P];
+    if (!total) return SHMEMX_OK;
+    if (!target || (mine && !source)) return set_error(SHMEMX_EINVAL);
+    DevBuf in = device_in(source, mine, g_state.cws_src, g_state.cws_src_bytes, s);
+    DevBuf out = device_out(target, total, g_state.cws_tgt, g_state.cws_tgt_bytes);
+    if ((mine && !in.dev) || !out.dev) return set_error(SHMEMX_ENOMEM);
+    if (mine && in.dev != out.dev + off[si.m])
+        SHMX_HIP(hipMemcpyAsync(out.dev + off[si.m], in.dev, mine, hipMemcpyDeviceToDevice, s));
+    if (collective(si)) {
+        if (si.world && fixed && !g_state.force_collective) {
+            SHMX_NCCL(ncclAllGather(out.dev + off[si.m], out.dev, mine, ncclUint8, g_state.comm, s));
+        } else {
+            SHMX_NCCL(ncclGroupStart());
+            for (int i = 0; i < si.P; ++i) {
+                if (i == si.m) continue;
+                const size_t bi = off[i + 1] - off[i];
+                if (mine) SHMX_NCCL(ncclSend(out.dev + off[si.m], mine, ncclUint8, si.peer(i), g_state.comm, s));
+                if (bi) SHMX_NCCL(ncclRecv(out.dev + off[i], bi, ncclUint8, si.peer(i), g_state.comm, s));
+            }
+            SHMX_NCCL(ncclGroupEnd());
+        }
+    }
+    finish(out, s);
+    return SHMEMX_OK;
+}
+
+// ---------------------------------------------------------- symmetric heap
+struct Block {
+    void *base;
+    size_t bytes;
+};
+std::map<void *, Block> g_heap;   // user pointer -> allocation
+
+void *heap_alloc(size_t alignment, size_t bytes) {
+    if (ensure_init()) return nullptr;
+    if (!bytes) return nullptr;
+    const size_t pad = alignment > 256 ? alignment : 0;
+    void *base = nullptr;
+    if (hipMalloc(&base, bytes + pad) != hipSuccess) {
+        (void)hipGetLastError();
+        set_error(SHMEMX_ENOMEM);
+        return nullptr;
+    }
+    uintptr_t u = reinterpret_cast<uintptr_t>(base);
+    if (pad) u = (u + alignment - 1) & ~(uintptr_t)(alignment - 1);
+    void *p = reinterpret_cast<void *>(u);
+    g_heap[p] = Block{base, bytes};
+    return p;
+}
+
+void heap_free(void *p) {
+    auto it = g_heap.find(p);
+    if (it == g_heap.end()) {
+        set_error(SHMEMX_EINVAL);
+        return;
+    }
+    SHMX_HIP(hipDeviceSynchronize());
+    SHMX_HIP(hipFree(it->second.base));
+    g_heap.erase(it);
+}
+
+}  // namespace
+}  // namespace shmx
+
+using namespace shmx;
+
+extern "C" {
+
+void pshmem_barrier(int PE_start, int logPE_stride, int PE_size, long *pSync) {
+    (void)pSync;
+    barrier_impl(PE_start, logPE_stride, PE_size);
+}
+
+void pshmem_barrier_all(void) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    if (ensure_init()) return;
+    barrier_impl(0, 0, g_state.npes);
+}
+
+void pshmem_broadcast32(void *target, const void *source, size_t nelems, int PE_root, int PE_start,
+                        int logPE_stride, int PE_size, long *pSync) {
+    (void)pSync;
+    broadcast_impl(4, target, source, nelems, PE_root, PE_start, logPE_stride, PE_size);
+}
+
+void pshmem_broadcast64(void *target, const void *source, size_t nelems, int PE_root, int PE_start,
+                        int logPE_stride, int PE_size, long *pSync) {
+    (void)pSync;
+    broadcast_impl(8, target, source, nelems, PE_root, PE_start, logPE_stride, PE_size);
+}
+
+void pshmem_fcollect32(void *target, const void *source, size_t nelems, int PE_start,
+                       int logPE_stride, int PE_size, long *pSync) {
+    (void)pSync;
+    collect_impl(4, target, source, nelems, PE_start, logPE_stride, PE_size, true);
+}
+
+void pshmem_fcollect64(void *target, const void *source, size_t nelems, int PE_start,
+                       int logPE_stride, int PE_size, long *pSync) {
+    (void)pSync;
+    collect_impl(8, target, source, nelems, PE_start, logPE_stride, PE_size, true);
+}
+
+void pshmem_collect32(void *target, const void *source, size_t nelems, int PE_start,
+                      int logPE_stride, int PE_size, long *pSync) {
+    (void)pSync;
+    collect_impl(4, target, source, nelems, PE_start, logPE_stride, PE_size, false);
+}
+
+void pshmem_collect64(void *target, const void *source, size_t nelems, int PE_start,
+                      int logPE_stride, int PE_size, long *pSync) {
+    (void)pSync;
+    collect_impl(8, target, source, nelems, PE_start, logPE_stride, PE_size, false);
+}
+
+void *pshmem_malloc(size_t size) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    clear_error();
+    void *p = heap_alloc(0, size);
+    pshmem_barrier_all();   // symmetric allocation is collective (symmem.c:209)
+    return p;
+}
+
+void *pshmem_align(size_t alignment, size_t size) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    clear_error();
+    if (alignment == 0 || (alignment & (alignment - 1))) {
+        set_error(SHMEMX_EINVAL);
+        return nullptr;
+    }
+    void *p = heap_alloc(alignment, size);
+    pshmem_barrier_all();
+    return p;
+}
+
+void pshmem_free(void *ptr) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    clear_error();
+    pshmem_barrier_all();
+    if (ptr) heap_free(ptr);
+}
+
+void *pshmem_realloc(void *ptr, size_t size) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    clear_error();
+    if (!ptr) return pshmem_malloc(size);
+    if (!size) {
+        pshmem_free(ptr);
+        return nullptr;
+    }
+    auto it = g_heap.find(ptr);
+    if (it == g_heap.end()) {
+        set_error(SHMEMX_EINVAL);
+        return nullptr;
+    }
+    void *p = heap_alloc(0, size);
+    if (p) {
+        const size_t keep = it->second.bytes < size ? it->second.bytes : size;
+        SHMX_HIP(hipMemcpy(p, ptr, keep, hipMemcpyDeviceToDevice));
+        heap_free(ptr);
+    }
+    pshmem_barrier_all();
+    return p;
+}
+
+void *pshmalloc(size_t size) { return pshmem_malloc(size); }
+void pshfree(void *ptr) { pshmem_free(ptr); }
+void *pshrealloc(void *ptr, size_t size) { return pshmem_realloc(ptr, size); }
+void *pshmemalign(size_t alignment, size_t size) { return pshmem_align(alignment, size); }
+
+#define SHMX_WEAK(ret, name, args) ret name args __attribute__((weak, alias("p" #name)));
+SHMX_WEAK(void, shmem_barrier, (int, int, int, long *))
+SHMX_WEAK(void, shmem_barrier_all, (void))
+SHMX_WEAK(void, shmem_broadcast32, (void *, const void *, size_t, int, int, int, int, long *))
+SHMX_WEAK(void, shmem_broadcast64, (void *, const void *, size_t, int, int, int, int, long *))
+SHMX_WEAK(void, shmem_fcollect32, (void *, const void *, size_t, int, int, int, long *))
+SHMX_WEAK(void, shmem_fcollect64, (void *, const void *, size_t, int, int, int, long *))
+SHMX_WEAK(void, shmem_collect32, (void *, const void *, size_t, int, int, int, long *))
+SHMX_WEAK(void, shmem_collect64, (void *, const void *, size_t, int, int, int, long *))
+SHMX_WEAK(void *, shmem_malloc, (size_t))
+SHMX_WEAK(void *, shmem_align, (size_t, size_t))
+SHMX_WEAK(void, shmem_free, (void *))
+SHMX_WEAK(void *, shmem_realloc, (void *, size_t))
+SHMX_WEAK(void *, shmalloc, (size_t))
+SHMX_WEAK(void, shfree, (void *))
+SHMX_WEAK(void *, shrealloc, (void *, size_t))
+SHMX_WEAK(void *, shmemalign, (size_t, size_t))
+
+}  // extern "C"

@@ -31,49 +31,25 @@
 
 #include "internal.h"
 #include "shmem_reduce_mi355x.h"
+#include "state.h"
 
 namespace shmx {
 
-struct State {
-    bool inited = false;
-    int pe = 0;
-    int npes = 1;
-    int device = 0;
-    hipStream_t stream = nullptr;
-    ncclComm_t comm = nullptr;
-    int algo = SHMEMX_ALGO_AUTO;
-    // test hook ($SHMEMX_FORCE_COLLECTIVE=1): a 1-PE job still builds an RCCL
-    // communicator and runs the collective schedules, so a one-GPU box can
-    // execute every RCCL call of the path
-    bool force_collective = false;
-    // grow-only device workspaces
-    void *ws = nullptr;        // A2A shard receive area / GATHER sources
-    size_t ws_bytes = 0;
-    void *tmp = nullptr;       // overlap temporary (reduce-op.c:187-203)
-    size_t tmp_bytes = 0;
-    void *stage_src = nullptr; // host-resident endpoints
-    void *stage_tgt = nullptr;
-    size_t stage_bytes = 0;
-    hipStream_t h2d = nullptr;  // staging copy streams and their chunk events
-    hipStream_t d2h = nullptr;
-    std::vector<hipEvent_t> events;
-    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
-};
-
-static State g_state;
+State g_state;
 
 // Host-resident arrays move over PCIe in chunks of this size (pipelined).
 constexpr size_t kStageChunkBytes = size_t(16) << 20;
-static std::recursive_mutex g_mu;
+std::recursive_mutex g_mu;
 static thread_local int t_last_error = SHMEMX_OK;
 
-static int set_error(int e) {
+int set_error(int e) {
     t_last_error = e;
     return e;
 }
 
-// "%-8.8f PE %d: LEVEL: msg", the reference's trace line (utils/trace.c:400-431)
-static void trace(const char *level, const char *fmt, ...) {
+void clear_error() { t_last_error = SHMEMX_OK; }
+
+void trace(const char *level, const char *fmt, ...) {
     const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() -
                                                    g_state.t0).count();
     char msg[512];
@@ -85,21 +61,11 @@ static void trace(const char *level, const char *fmt, ...) {
     fflush(stderr);
 }
 
-[[noreturn]] static void fatal(const char *what, const char *detail) {
+[[noreturn]] void fatal(const char *what, const char *detail) {
     trace("FATAL", "%s: %s", what, detail);
     std::abort();
 }
 
-#define SHMX_HIP(call)                                                         \
-    do {                                                                     \
-        hipError_t e_ = (call);                                              \
-        if (e_ != hipSuccess) fatal(#call, hipGetErrorString(e_));           \
-    } while (0)
-#define SHMX_NCCL(call)                                                        \
-    do {                                                                     \
-        ncclResult_t r_ = (call);                                            \
-        if (r_ != ncclSuccess) fatal(#call, ncclGetErrorString(r_));         \
-    } while (0)
 
 static int env_int(const char *a, const char *b, int dflt) {
     for (const char *k : {a, b}) {
@@ -194,7 +160,7 @@ static int file_bootstrap(int pe, int npes, int device) {
     return rc;
 }
 
-static int ensure_init() {
+int ensure_init() {
     if (g_state.inited) return SHMEMX_OK;
     const int npes = env_int("SHMEM_NPES", "WORLD_SIZE", 1);
     if (npes != 1) return set_error(SHMEMX_ENOINIT);
@@ -205,7 +171,7 @@ static int ensure_init() {
 
 // ----------------------------------------------------------------- plans
 
-static bool is_member(int pe, int start, int logstride, int size, int *index) {
+bool is_member(int pe, int start, int logstride, int size, int *index) {
     const int step = 1 << logstride;
     if (pe < start || (pe - start) % step) return false;
     const int i = (pe - start) / step;
@@ -309,7 +275,7 @@ static int make_plan(int type, int op, int nreduce, int start, int logstride,
 
 // ------------------------------------------------------------- workspaces
 
-static void *grow(void *&buf, size_t &have, size_t need) {
+void *grow(void *&buf, size_t &have, size_t need) {
     if (need <= have) return buf;
     if (buf) {
         // the old buffer may still be in use on any caller stream
@@ -463,7 +429,7 @@ static int reduce_device(int type, int op, void *target, const void *source,
     return SHMEMX_OK;
 }
 
-static bool device_accessible(const void *ptr) {
+bool device_accessible(const void *ptr) {
     hipPointerAttribute_t attr;
     if (hipPointerGetAttributes(&attr, ptr) != hipSuccess) {
         (void)hipGetLastError();
@@ -475,7 +441,7 @@ static bool device_accessible(const void *ptr) {
 // Page-locked host memory (hipHostMalloc / hipHostRegister): DMA-able, so
 // chunked copies overlap; pageable memory is copied through HIP's own
 // staging, where chunking only adds overhead (measured).
-static bool host_pinned(const void *ptr) {
+bool host_pinned(const void *ptr) {
     hipPointerAttribute_t attr;
     if (hipPointerGetAttributes(&attr, ptr) != hipSuccess) {
         (void)hipGetLastError();
@@ -642,11 +608,13 @@ void pshmem_finalize(void) {
         ncclCommDestroy(g_state.comm);
         g_state.comm = nullptr;
     }
-    for (void **b : {&g_state.ws, &g_state.tmp, &g_state.stage_src, &g_state.stage_tgt}) {
+    for (void **b : {&g_state.ws, &g_state.tmp, &g_state.stage_src, &g_state.stage_tgt,
+                     &g_state.token, &g_state.cws_src, &g_state.cws_tgt}) {
         if (*b) (void)hipFree(*b);
         *b = nullptr;
     }
     g_state.ws_bytes = g_state.tmp_bytes = g_state.stage_bytes = 0;
+    g_state.token_bytes = g_state.cws_src_bytes = g_state.cws_tgt_bytes = 0;
     for (hipEvent_t e : g_state.events) (void)hipEventDestroy(e);
     g_state.events.clear();
     for (hipStream_t *st : {&g_state.h2d, &g_state.d2h}) {

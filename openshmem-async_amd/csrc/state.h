@@ -1,0 +1,73 @@
+// Runtime state shared by runtime.cpp (init, planner, reductions) and
+// collectives.cpp (barrier, broadcast, [f]collect, symmetric heap).
+// Internal to libshmem_reduce_mi355x.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <mutex>
+#include <vector>
+
+namespace shmx {
+
+struct State {
+    bool inited = false;
+    int pe = 0;
+    int npes = 1;
+    int device = 0;
+    hipStream_t stream = nullptr;
+    ncclComm_t comm = nullptr;
+    int algo = SHMEMX_ALGO_AUTO;
+    // test hook ($SHMEMX_FORCE_COLLECTIVE=1): a 1-PE job still builds an RCCL
+    // communicator and runs the collective schedules, so a one-GPU box can
+    // execute every RCCL call of the path
+    bool force_collective = false;
+    // grow-only device workspaces
+    void *ws = nullptr;        // A2A shard receive area / GATHER sources
+    size_t ws_bytes = 0;
+    void *tmp = nullptr;       // overlap temporary (reduce-op.c:187-203)
+    size_t tmp_bytes = 0;
+    void *stage_src = nullptr; // host-resident endpoints
+    void *stage_tgt = nullptr;
+    size_t stage_bytes = 0;
+    void *token = nullptr;     // barrier tokens / collect counts
+    size_t token_bytes = 0;
+    void *cws_src = nullptr;   // staging for host buffers of the other collectives
+    size_t cws_src_bytes = 0;
+    void *cws_tgt = nullptr;
+    size_t cws_tgt_bytes = 0;
+    hipStream_t h2d = nullptr;  // staging copy streams and their chunk events
+    hipStream_t d2h = nullptr;
+    std::vector<hipEvent_t> events;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+};
+
+extern State g_state;
+extern std::recursive_mutex g_mu;   // the reference's state is not thread-safe either
+
+int set_error(int e);               // thread-local last error (shmemx_reduce_last_error)
+void clear_error();
+// "%-8.8f PE %d: LEVEL: msg", the reference's trace line (utils/trace.c:400-431)
+void trace(const char *level, const char *fmt, ...);
+[[noreturn]] void fatal(const char *what, const char *detail);
+
+#define SHMX_HIP(call)                                                         \
+    do {                                                                     \
+        hipError_t e_ = (call);                                              \
+        if (e_ != hipSuccess) ::shmx::fatal(#call, hipGetErrorString(e_));   \
+    } while (0)
+#define SHMX_NCCL(call)                                                        \
+    do {                                                                     \
+        ncclResult_t r_ = (call);                                            \
+        if (r_ != ncclSuccess) ::shmx::fatal(#call, ncclGetErrorString(r_)); \
+    } while (0)
+
+int ensure_init();                  // single-PE auto-init; ENOINIT if npes > 1
+bool is_member(int pe, int start, int logstride, int size, int *index);
+bool device_accessible(const void *ptr);
+bool host_pinned(const void *ptr);
+void *grow(void *&buf, size_t &have, size_t need);   // grow-only device buffer
+
+}  // namespace shmx

@@ -98,6 +98,25 @@ def lib() -> ctypes.CDLL:
     L.shmemx_reduce_last_error.restype = i
     L.shmemx_reduce_error_string.argtypes = [i]
     L.shmemx_reduce_error_string.restype = ctypes.c_char_p
+    for bits in (32, 64):
+        for name in (f"shmem_broadcast{bits}", f"pshmem_broadcast{bits}"):
+            getattr(L, name).argtypes = [vp, vp, sz, i, i, i, i, vp]
+            getattr(L, name).restype = None
+        for kind in ("fcollect", "collect"):
+            for name in (f"shmem_{kind}{bits}", f"pshmem_{kind}{bits}"):
+                getattr(L, name).argtypes = [vp, vp, sz, i, i, i, vp]
+                getattr(L, name).restype = None
+    L.shmem_barrier.argtypes = [i, i, i, vp]
+    L.shmem_barrier.restype = None
+    L.shmem_barrier_all.restype = None
+    L.shmem_malloc.argtypes = [sz]
+    L.shmem_malloc.restype = vp
+    L.shmem_align.argtypes = [sz, sz]
+    L.shmem_align.restype = vp
+    L.shmem_realloc.argtypes = [vp, sz]
+    L.shmem_realloc.restype = vp
+    L.shmem_free.argtypes = [vp]
+    L.shmem_free.restype = None
     for t, o in REFERENCE_PAIRS:
         for prefix in ("shmem", "pshmem"):
             f = getattr(L, f"{prefix}_{t}_{o}_to_all")
@@ -252,3 +271,48 @@ def type_size(type_name: str) -> int:
 
 def op_on_device(type_name: str, op: str) -> bool:
     return bool(lib().shmemx_op_on_device(TYPES[type_name], OPS[op]))
+
+
+# ------------------------------------------- neighbouring collectives, heap
+def barrier(PE_start: int, logPE_stride: int, PE_size: int, pSync=None) -> None:
+    lib().shmem_barrier(PE_start, logPE_stride, PE_size, addr(pSync))
+
+
+def barrier_all() -> None:
+    lib().shmem_barrier_all()
+
+
+def broadcast(bits: int, target, source, nelems: int, PE_root: int, PE_start: int,
+              logPE_stride: int, PE_size: int, pSync=None) -> None:
+    """shmem_broadcast{32,64} (reference broadcast/broadcast.c)."""
+    getattr(lib(), f"shmem_broadcast{bits}")(addr(target), addr(source), nelems, PE_root,
+                                             PE_start, logPE_stride, PE_size, addr(pSync))
+
+
+def fcollect(bits: int, target, source, nelems: int, PE_start: int, logPE_stride: int,
+             PE_size: int, pSync=None) -> None:
+    getattr(lib(), f"shmem_fcollect{bits}")(addr(target), addr(source), nelems, PE_start,
+                                            logPE_stride, PE_size, addr(pSync))
+
+
+def collect(bits: int, target, source, nelems: int, PE_start: int, logPE_stride: int,
+            PE_size: int, pSync=None) -> None:
+    getattr(lib(), f"shmem_collect{bits}")(addr(target), addr(source), nelems, PE_start,
+                                           logPE_stride, PE_size, addr(pSync))
+
+
+def malloc(nbytes: int) -> int:
+    """shmem_malloc: symmetric HBM allocation (device address, 0 on failure)."""
+    return lib().shmem_malloc(nbytes) or 0
+
+
+def align(alignment: int, nbytes: int) -> int:
+    return lib().shmem_align(alignment, nbytes) or 0
+
+
+def realloc(ptr: int, nbytes: int) -> int:
+    return lib().shmem_realloc(ptr or None, nbytes) or 0
+
+
+def free(ptr: int) -> None:
+    lib().shmem_free(ptr or None)

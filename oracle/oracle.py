@@ -55,6 +55,11 @@ def lib() -> ctypes.CDLL:
         L.oracle_type_size.restype = ctypes.c_size_t
         L.oracle_op_valid.argtypes = [i, i]
         L.oracle_op_valid.restype = i
+        sz_t = ctypes.c_size_t
+        L.oracle_broadcast_sim.argtypes = [sz_t, i, i, i, i, i, sz_t, vp, sz_t, vp, sz_t]
+        L.oracle_broadcast_sim.restype = i
+        L.oracle_collect_sim.argtypes = [sz_t, i, i, i, i, ctypes.POINTER(sz_t), vp, sz_t, vp, sz_t]
+        L.oracle_collect_sim.restype = i
         L.oracle_fnv1a.argtypes = [vp, ctypes.c_size_t]
         L.oracle_fnv1a.restype = ctypes.c_uint64
         _lib = L
@@ -179,3 +184,33 @@ def value_hash(type_name: str, arr: np.ndarray) -> int:
     if type_name == "longdouble":
         a = np.ascontiguousarray(a.view(np.uint8).reshape(-1, a.itemsize)[:, :10])
     return int(lib().oracle_fnv1a(a.ctypes.data, a.nbytes))
+
+
+def broadcast_sim(srcs: np.ndarray, targets: np.ndarray, PE_root: int, PE_start: int,
+                  logPE_stride: int, PE_size: int) -> np.ndarray:
+    """shmem_broadcast{32,64} on every PE (srcs/targets: [npes, nelems])."""
+    srcs = np.ascontiguousarray(srcs)
+    out = np.ascontiguousarray(targets.copy())
+    npes, n = srcs.shape
+    rc = lib().oracle_broadcast_sim(srcs.itemsize, npes, PE_root, PE_start, logPE_stride, PE_size,
+                                    n, srcs.ctypes.data, srcs.strides[0], out.ctypes.data,
+                                    out.strides[0])
+    if rc:
+        raise ValueError("oracle_broadcast_sim rejected the arguments")
+    return out
+
+
+def collect_sim(srcs: np.ndarray, nelems, targets: np.ndarray, PE_start: int,
+                logPE_stride: int, PE_size: int) -> np.ndarray:
+    """shmem_[f]collect{32,64} on every PE.  srcs: [npes, maxn] (PE p uses
+    nelems[p] leading elements), targets: [npes, capacity]."""
+    srcs = np.ascontiguousarray(srcs)
+    out = np.ascontiguousarray(targets.copy())
+    npes = srcs.shape[0]
+    ne = (ctypes.c_size_t * npes)(*nelems)
+    rc = lib().oracle_collect_sim(srcs.itemsize, npes, PE_start, logPE_stride, PE_size, ne,
+                                  srcs.ctypes.data, srcs.strides[0], out.ctypes.data,
+                                  out.strides[0])
+    if rc:
+        raise ValueError("oracle_collect_sim rejected the arguments")
+    return out

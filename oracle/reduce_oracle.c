@@ -245,6 +245,49 @@ int oracle_reduce_sim(int type, int op, int npes, int PE_start,
     return 0;
 }
 
+/* ------------------------------------------- neighbouring collectives ---- */
+
+int oracle_broadcast_sim(size_t esize, int npes, int PE_root, int PE_start,
+                         int logPE_stride, int PE_size, size_t nelems,
+                         const void *sources, size_t src_stride,
+                         void *targets, size_t tgt_stride)
+{
+    if (orc_check_set(npes, PE_start, logPE_stride, PE_size, 0) || PE_root < 0 ||
+        PE_root >= PE_size)
+        return -1;
+    /* root = PE_root * step + PE_start (broadcast-linear.c:61); every other
+     * member gets the root's source with one getmem (:64-67)               */
+    const int root = orc_member(PE_start, logPE_stride, PE_root);
+    const char *src = (const char *)sources + (size_t)root * src_stride;
+    for (int m = 0; m < PE_size; ++m) {
+        const int pe = orc_member(PE_start, logPE_stride, m);
+        if (pe != root)
+            memcpy((char *)targets + (size_t)pe * tgt_stride, src, nelems * esize);
+    }
+    return 0;
+}
+
+int oracle_collect_sim(size_t esize, int npes, int PE_start, int logPE_stride,
+                       int PE_size, const size_t *nelems, const void *sources,
+                       size_t src_stride, void *targets, size_t tgt_stride)
+{
+    if (orc_check_set(npes, PE_start, logPE_stride, PE_size, 0)) return -1;
+    /* acc_off runs left to right through the set (collect-linear.c:83-110);
+     * each member puts its slice at that offset on every member (:112-124) */
+    size_t acc_off = 0;
+    for (int i = 0; i < PE_size; ++i) {
+        const int from = orc_member(PE_start, logPE_stride, i);
+        const size_t nb = nelems[from] * esize;
+        for (int m = 0; m < PE_size; ++m) {
+            const int to = orc_member(PE_start, logPE_stride, m);
+            memcpy((char *)targets + (size_t)to * tgt_stride + acc_off,
+                   (const char *)sources + (size_t)from * src_stride, nb);
+        }
+        acc_off += nb;
+    }
+    return 0;
+}
+
 /* ------------------------------------------------------------ inputs ---- */
 
 uint64_t oracle_splitmix64(uint64_t seed, uint64_t i)

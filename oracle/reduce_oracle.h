@@ -61,6 +61,22 @@ int oracle_reduce_fork(int type, int op, int npes, int PE_start,
                        int fill_kind, uint64_t base_seed, int reps,
                        int pin_base, double *times_out, uint64_t *hashes_out);
 
+/* The neighbouring collectives, byte-level restatements.
+ * PE p's source at sources + p * src_stride, PE p's target at
+ * targets + p * tgt_stride (bytes).  Only members' targets are written.     */
+/* broadcast-linear.c:54-74: every member but the root receives the root's
+ * nelems * esize bytes; the root's target is left alone. */
+int oracle_broadcast_sim(size_t esize, int npes, int PE_root, int PE_start,
+                         int logPE_stride, int PE_size, size_t nelems,
+                         const void *sources, size_t src_stride,
+                         void *targets, size_t tgt_stride);
+/* fcollect-linear.c:69-91 (nelems equal on all PEs) and collect-linear.c:
+ * 57-130 (per-PE nelems[p]): member i's source lands at the running byte
+ * offset sum_{j<i} nelems[member j] * esize of every member's target. */
+int oracle_collect_sim(size_t esize, int npes, int PE_start, int logPE_stride,
+                       int PE_size, const size_t *nelems, const void *sources,
+                       size_t src_stride, void *targets, size_t tgt_stride);
+
 /* splitmix64 stream: word i of seed s = splitmix64 output number i+1. */
 uint64_t oracle_splitmix64(uint64_t seed, uint64_t i);
 /* Fill `n` elements of `type` from splitmix64(seed, i).  fill_kind:
