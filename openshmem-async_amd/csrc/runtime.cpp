@@ -293,6 +293,27 @@ void *grow(void *&buf, size_t &have, size_t need) {
     return buf;
 }
 
+// The device workspaces (ws, tmp) are shared by every stream-ordered call:
+// a use on stream s waits for the previous use when that was on another
+// stream.  Skipped while s is being captured into a graph (a captured graph
+// lives on one stream; events recorded in a capture do not fire until replay).
+static bool capturing(hipStream_t s) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+}
+
+static void ws_acquire(hipStream_t s) {
+    if (g_state.ws_stream && g_state.ws_stream != s && !capturing(s))
+        SHMX_HIP(hipStreamWaitEvent(s, g_state.ws_event, 0));
+}
+
+static void ws_release(hipStream_t s) {
+    if (capturing(s)) return;
+    if (!g_state.ws_event) SHMX_HIP(hipEventCreateWithFlags(&g_state.ws_event, hipEventDisableTiming));
+    SHMX_HIP(hipEventRecord(g_state.ws_event, s));
+    g_state.ws_stream = s;
+}
+
 static bool overlap(const void *a, const void *b, size_t bytes) {
     const char *x = static_cast<const char *>(a), *y = static_cast<const char *>(b);
     return x != y && x < y + bytes && y < x + bytes;
@@ -318,6 +339,10 @@ static void fold_chain(int type, int op, void *out, const void **ins, int nins,
     }
 }
 
+static int reduce_exchange(int type, int op, char *tgt, const char *src, int nreduce,
+                           int start, int logstride, const shmemx_plan_t &p, hipStream_t s,
+                           bool &uses_ws);
+
 // The engine: device-resident target/source, stream-ordered.
 static int reduce_device(int type, int op, void *target, const void *source,
                          int nreduce, int start, int logstride, int size,
@@ -335,13 +360,28 @@ static int reduce_device(int type, int op, void *target, const void *source,
 
     // Partially overlapping target/source: reduce from a private copy of the
     // source (the reference's temporary target, reduce-op.c:187-203).
+    bool uses_ws = false;
     if (overlap(tgt, src, bytes)) {
         void *t = grow(g_state.tmp, g_state.tmp_bytes, bytes);
         if (!t) return set_error(SHMEMX_ENOMEM);
+        ws_acquire(s);
+        uses_ws = true;
         const void *in[1] = {src};
         fold_chain(type, op, t, in, 1, (size_t)nreduce, s);
         src = static_cast<const char *>(t);
     }
+    const int xrc = reduce_exchange(type, op, tgt, src, nreduce, start, logstride, p, s, uses_ws);
+    if (uses_ws) ws_release(s);
+    return xrc;
+}
+
+// The exchange + fold of reduce_device once the source is safe to read.
+static int reduce_exchange(int type, int op, char *tgt, const char *src, int nreduce,
+                           int start, int logstride, const shmemx_plan_t &p, hipStream_t s,
+                           bool &uses_ws) {
+    const int size = p.nmembers;
+    const size_t sz = (size_t)p.elem_size;
+    const size_t bytes = sz * (size_t)nreduce;
 
     const int P = size, m = p.member, step = 1 << logstride;
     if (P == 1 && !g_state.force_collective) {  // reduce-op.c:213-216, no peers: a copy
@@ -377,6 +417,8 @@ static int reduce_device(int type, int op, void *target, const void *source,
 
     char *ws = static_cast<char *>(grow(g_state.ws, g_state.ws_bytes, (size_t)p.ws_bytes));
     if (!ws) return set_error(SHMEMX_ENOMEM);
+    if (!uses_ws) ws_acquire(s);
+    uses_ws = true;
     const long long n = nreduce;
 
     if (p.algo == SHMEMX_ALGO_A2A) {
@@ -572,6 +614,10 @@ int reduce_on_stream(int type, int op, void *target, const void *source,
     t_last_error = SHMEMX_OK;
     if (int rc = ensure_init()) return rc;
     if (nreduce > 0 && (!target || !source)) return set_error(SHMEMX_EINVAL);
+    // the stream-ordered form takes device memory only (RCCL and the kernels
+    // dereference it); host arrays go through the blocking entry points
+    if (nreduce > 0 && (!device_accessible(target) || !device_accessible(source)))
+        return set_error(SHMEMX_EINVAL);
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : g_state.stream;
     return reduce_device(type, op, target, source, nreduce, start, logstride, size,
                          algo == SHMEMX_ALGO_AUTO ? g_state.algo : algo, s);

@@ -32,6 +32,8 @@ struct State {
     void *stage_src = nullptr; // host-resident endpoints
     void *stage_tgt = nullptr;
     size_t stage_bytes = 0;
+    hipEvent_t ws_event = nullptr;  // last use of ws/tmp, on stream ws_stream
+    hipStream_t ws_stream = nullptr;
     void *token = nullptr;     // barrier tokens / collect counts
     size_t token_bytes = 0;
     void *cws_src = nullptr;   // staging for host buffers of the other collectives

@@ -194,3 +194,20 @@ def test_host_staging_pipeline_many_chunks(cuda, shm, oracle, t):
     big = np.concatenate([src, src[:7]])
     shm.to_all(t, "sum", big[3:].ctypes.data, big.ctypes.data, n, 0, 0, 1)   # overlap
     assert big[3:3 + n].tobytes() == src.tobytes()
+
+
+def test_c_program_isx_verification(cuda, tmp_path):
+    """A plain C99 program (examples/isx_verify.c) linked against the library:
+    the reference's ISx verification (isx.c:615-624) with static host arrays,
+    plus double sum / long xor checks, run as its own process."""
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    libdir = os.path.join(repo, "openshmem-async_amd")
+    exe = tmp_path / "isx_verify"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(repo, "include"),
+                    os.path.join(repo, "examples", "isx_verify.c"), "-L", libdir,
+                    "-lshmem_reduce_mi355x", f"-Wl,-rpath,{libdir}", "-o", str(exe)], check=True)
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120, env=env)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "ISx verification passed" in out.stdout

@@ -207,3 +207,13 @@ def test_fork_harness_agrees_with_sim(oracle, s):
         want = oracle.value_hash("double", tg[p]) if p in mem else 0
         assert hashes[p] == want, p
     assert all(t > 0 for t in times)
+
+
+def test_config1_int_sum_1024_two_pes_fork(oracle):
+    """BASELINE.json configs[0]: shmem_int_sum_to_all, nreduce = 1024, 2 PEs
+    as 2 processes over shared memory (the reference's oshrun smp loopback
+    model, oshrun.in:97-98): both PEs hold the exact sum."""
+    times, hashes = oracle.reduce_fork("int", "sum", 2, 0, 0, 2, 1024, kind=1, reps=3)
+    srcs = oracle.sources("int", 1, 2, 1024)
+    want = (srcs[0].astype(np.int64) + srcs[1]).astype(np.int32)     # wraps like C
+    assert hashes[0] == hashes[1] == oracle.value_hash("int", want)
