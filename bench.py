@@ -156,6 +156,33 @@ def config_extras(world, stream, barrier, max_over_ranks):
     return out
 
 
+def latency_extras(world, barrier, max_over_ranks):
+    """Small-message latency of the blocking drop-in call (the ISx use:
+    shmem_longlong_sum_to_all with nreduce = 1, isx.c:617), host- and
+    device-resident, microseconds per call (max over ranks)."""
+    import numpy as np
+    out = {}
+    psync = np.full(128, -1, dtype=np.int64)
+    for n in (1, 64, 4096):
+        for where in ("host", "device"):
+            if where == "host":
+                src = np.arange(n, dtype=np.int64)
+                tgt = np.zeros(n, dtype=np.int64)
+            else:
+                src = torch.arange(n, dtype=torch.int64, device="cuda")
+                tgt = torch.zeros(n, dtype=torch.int64, device="cuda")
+            for _ in range(5):
+                shm.to_all("longlong", "sum", tgt, src, n, 0, 0, world, None, psync)
+            barrier()
+            reps = 200
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                shm.to_all("longlong", "sum", tgt, src, n, 0, 0, world, None, psync)
+            t = max_over_ranks((time.perf_counter() - t0) / reps)
+            out[f"longlong_sum_n{n}_{where}_us"] = round(t * 1e6, 1)
+    return out
+
+
 def time_region(fn, steps, stream, barrier):
     """Run fn() `steps` times on `stream`; returns (wall_s, event_s)."""
     barrier()
@@ -284,6 +311,7 @@ def main():
                 "us_per_call": round(e2 / k2 * 1e6, 2)}
             extras["host_resident_e2e"] = host_e2e(n)
             extras["configs"] = config_extras(world, stream, barrier, max_over_ranks)
+            extras["latency"] = latency_extras(world, barrier, max_over_ranks)
     else:
         t_call = ev / a.steps
         xgmi_bytes = 2 * (world - 1) / world * nbytes        # per GPU, RS + AG
@@ -311,6 +339,7 @@ def main():
                 except shm.ShmemError as e:
                     extras[f"algo_{alt}_GiBps"] = str(e)
             extras["configs"] = config_extras(world, stream, barrier, max_over_ranks)
+            extras["latency"] = latency_extras(world, barrier, max_over_ranks)
 
     cpu = None
     if world == 1 and rank == 0 and not a.no_cpu_baseline:

@@ -37,8 +37,10 @@ namespace shmx {
 
 State g_state;
 
-// Host-resident arrays move over PCIe in chunks of this size (pipelined).
+// Host-resident arrays move over PCIe in chunks of this size (pipelined);
+// up to kSmallHostBytes they bounce through page-locked buffers instead.
 constexpr size_t kStageChunkBytes = size_t(16) << 20;
+constexpr size_t kSmallHostBytes = size_t(256) << 10;
 std::recursive_mutex g_mu;
 static thread_local int t_last_error = SHMEMX_OK;
 
@@ -559,6 +561,37 @@ void reduce_blocking(int type, int op, void *target, const void *source,
         }
         g_state.stage_bytes = bytes;
     }
+    if (bytes <= kSmallHostBytes) {
+        // Small messages (the ISx nreduce = 1 case, isx.c:617): latency, not
+        // bandwidth.  Bounce through page-locked host buffers so both copies
+        // are plain DMA on the library stream, and wait once.
+        if (bytes > g_state.bounce_bytes) {
+            if (g_state.bounce) SHMX_HIP(hipHostFree(g_state.bounce));
+            g_state.bounce = nullptr;
+            g_state.bounce_bytes = 0;
+            if (hipHostMalloc(&g_state.bounce, 2 * kSmallHostBytes, hipHostMallocDefault) != hipSuccess) {
+                (void)hipGetLastError();
+                set_error(SHMEMX_ENOMEM);
+                return;
+            }
+            g_state.bounce_bytes = kSmallHostBytes;
+        }
+        char *bin = static_cast<char *>(g_state.bounce);
+        char *bout = bin + kSmallHostBytes;
+        const void *dsrc = source;
+        if (!sdev) {
+            std::memcpy(bin, source, bytes);
+            SHMX_HIP(hipMemcpyAsync(g_state.stage_src, bin, bytes, hipMemcpyHostToDevice, s));
+            dsrc = g_state.stage_src;
+        }
+        void *dtgt = tdev ? target : g_state.stage_tgt;
+        const int rc = reduce_device(type, op, dtgt, dsrc, nreduce, start, logstride, size,
+                                     g_state.algo, s);
+        if (!rc && !tdev) SHMX_HIP(hipMemcpyAsync(bout, dtgt, bytes, hipMemcpyDeviceToHost, s));
+        SHMX_HIP(hipStreamSynchronize(s));
+        if (!rc && !tdev) std::memcpy(target, bout, bytes);
+        return;
+    }
     if (!g_state.h2d) {
         SHMX_HIP(hipStreamCreateWithFlags(&g_state.h2d, hipStreamNonBlocking));
         SHMX_HIP(hipStreamCreateWithFlags(&g_state.d2h, hipStreamNonBlocking));
@@ -661,6 +694,9 @@ void pshmem_finalize(void) {
     }
     g_state.ws_bytes = g_state.tmp_bytes = g_state.stage_bytes = 0;
     g_state.token_bytes = g_state.cws_src_bytes = g_state.cws_tgt_bytes = 0;
+    if (g_state.bounce) (void)hipHostFree(g_state.bounce);
+    g_state.bounce = nullptr;
+    g_state.bounce_bytes = 0;
     for (hipEvent_t e : g_state.events) (void)hipEventDestroy(e);
     g_state.events.clear();
     for (hipStream_t *st : {&g_state.h2d, &g_state.d2h}) {

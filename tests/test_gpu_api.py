@@ -211,3 +211,20 @@ def test_c_program_isx_verification(cuda, tmp_path):
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120, env=env)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "ISx verification passed" in out.stdout
+
+
+@pytest.mark.parametrize("n", [1, 7, 4096, 32768])
+def test_host_small_messages_bounce_path(cuda, shm, oracle, n):
+    """Host arrays up to 256 KiB take the page-locked bounce path; mixed
+    host/device endpoints included."""
+    import torch
+    src = oracle.fill("int", 1, n, n)
+    tgt = np.zeros_like(src)
+    shm.to_all("int", "xor", tgt, src, n, 0, 0, 1)
+    assert shm.last_error() == 0 and tgt.tobytes() == src.tobytes()
+    d = torch.zeros(n, dtype=torch.int32, device="cuda")
+    shm.to_all("int", "max", d, src, n, 0, 0, 1)                 # host -> device
+    assert d.cpu().numpy().tobytes() == src.tobytes()
+    tgt[:] = 0
+    shm.to_all("int", "min", tgt, d, n, 0, 0, 1)                 # device -> host
+    assert tgt.tobytes() == src.tobytes()

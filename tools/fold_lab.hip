@@ -174,10 +174,67 @@ static int offsets_mode(size_t n) {
     return 0;
 }
 
+// Mode "pairs": separately allocated (acc, in) pairs in one process, and
+// pairs carved from one arena: is the rate a property of the allocation?
+static int pairs_mode(size_t n) {
+    const size_t nvec = n / 2, bytes = n * 8;
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto time_pair = [&](f64x2 *acc, const f64x2 *in) {
+        std::vector<float> ts;
+        for (int r = 0; r < 5; ++r) {
+            for (int w = 0; w < 2; ++w) L_strided<256, 4, 3>(acc, in, nvec, s);
+            CK(hipEventRecord(e0, s));
+            for (int i = 0; i < 20; ++i) L_strided<256, 4, 3>(acc, in, nvec, s);
+            CK(hipEventRecord(e1, s));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            ts.push_back(ms / 20);
+        }
+        std::sort(ts.begin(), ts.end());
+        return ts[2] * 1e3f;
+    };
+    std::vector<void *> ptrs;
+    for (int p = 0; p < 6; ++p) {
+        void *a, *b;
+        CK(hipMalloc(&a, bytes));
+        CK(hipMalloc(&b, bytes));
+        CK(hipMemset(a, 0, bytes));
+        CK(hipMemset(b, 0, bytes));
+        ptrs.push_back(a);
+        ptrs.push_back(b);
+        printf("separate pair %d  acc %p in %p  %8.2f us\n", p, a, b,
+               time_pair((f64x2 *)a, (const f64x2 *)b));
+    }
+    // cross pairs: acc of pair i with in of pair j
+    for (int p = 0; p < 6; ++p)
+        printf("cross acc%d in%d  %8.2f us\n", p, (p + 1) % 6,
+               time_pair((f64x2 *)ptrs[2 * p], (const f64x2 *)ptrs[2 * ((p + 1) % 6) + 1]));
+    for (void *q : ptrs) CK(hipFree(q));
+    // pairs carved from one 4 GiB arena at assorted offsets
+    char *arena;
+    CK(hipMalloc(&arena, size_t(4) << 30));
+    CK(hipMemset(arena, 0, size_t(4) << 30));
+    const size_t offs[][2] = {{0, 256ull << 20}, {512ull << 20, 1024ull << 20},
+                              {(3ull << 30), (1ull << 30) + (6ull << 20)},
+                              {(2ull << 30) + 4096, (600ull << 20)},
+                              {(1536ull << 20), (3ull << 30) + (512ull << 20)},
+                              {(2560ull << 20) + 65536, (100ull << 20)}};
+    for (auto &o : offs)
+        printf("arena acc+%zu MiB in+%zu MiB  %8.2f us\n", o[0] >> 20, o[1] >> 20,
+               time_pair((f64x2 *)(arena + o[0]), (const f64x2 *)(arena + o[1])));
+    return 0;
+}
+
 int main(int argc, char **argv) {
     const size_t n = argc > 1 ? strtoull(argv[1], 0, 10) : (32ull << 20);
     const int cold = argc > 2 ? atoi(argv[2]) : 0;
     if (cold == 2) return offsets_mode(n);
+    if (cold == 3) return pairs_mode(n);
     const size_t nvec = n / 2;
     f64x2 *acc, *in;
     double *scratch;
