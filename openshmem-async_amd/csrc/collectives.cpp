@@ -112,6 +112,7 @@ int barrier_impl(int start, int logstride, int size) {
     hipStream_t s = g_state.stream;
     // quiet: everything this PE enqueued before the barrier is complete
     SHMX_HIP(hipStreamSynchronize(s));
+    trace(LOG_BARRIER, "set (%d,%d,%d) member %d", start, logstride, size, si.m);
     if (!collective(si)) return SHMEMX_OK;
     char *tok = token_area(si.P);
     if (!tok) return set_error(SHMEMX_ENOMEM);
@@ -139,6 +140,8 @@ int broadcast_impl(size_t esize, void *target, const void *source, size_t nelems
     if (int rc = set_info(start, logstride, size, si)) return rc;
     if (root_idx < 0 || root_idx >= size) return set_error(SHMEMX_EINVAL);
     const size_t bytes = nelems * esize;
+    trace(LOG_BROADCAST, "%zu bytes from set member %d, set (%d,%d,%d) member %d", bytes, root_idx,
+          start, logstride, size, si.m);
     if (!bytes || !collective(si)) return SHMEMX_OK;  // the root's target is never written
     if ((si.m == root_idx && !source) || (si.m != root_idx && !target)) return set_error(SHMEMX_EINVAL);
     hipStream_t s = g_state.stream;
@@ -206,6 +209,8 @@ int collect_impl(size_t esize, void *target, const void *source, size_t nelems, 
     std::vector<size_t> off(si.P + 1, 0);
     for (int i = 0; i < si.P; ++i) off[i + 1] = off[i] + (size_t)counts[i] * esize;
     const size_t mine = (size_t)counts[si.m] * esize, total = off[si.P];
+    trace(LOG_COLLECT, "%s: %zu of %zu bytes at offset %zu, set (%d,%d,%d)",
+          fixed ? "fcollect" : "collect", mine, total, off[si.m], start, logstride, size);
     if (!total) return SHMEMX_OK;
     if (!target || (mine && !source)) return set_error(SHMEMX_EINVAL);
     DevBuf in = device_in(source, mine, g_state.cws_src, g_state.cws_src_bytes, s);
@@ -252,6 +257,7 @@ void *heap_alloc(size_t alignment, size_t bytes) {
     if (pad) u = (u + alignment - 1) & ~(uintptr_t)(alignment - 1);
     void *p = reinterpret_cast<void *>(u);
     g_heap[p] = Block{base, bytes};
+    trace(LOG_MEMORY, "shmem_malloc(%zu bytes, align %zu) = %p (HBM)", bytes, alignment, p);
     return p;
 }
 

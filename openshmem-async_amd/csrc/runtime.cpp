@@ -19,6 +19,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cctype>
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
@@ -51,7 +52,45 @@ int set_error(int e) {
 
 void clear_error() { t_last_error = SHMEMX_OK; }
 
-void trace(const char *level, const char *fmt, ...) {
+// Trace facility with the reference's interface (utils/trace.c:55-140,
+// 240-431): $SHMEM_LOG_LEVELS lists facilities (delimiters ",:;",
+// case-insensitive, "all"), $SHMEM_LOG_FILE redirects the output, FATAL is
+// always on; lines are "%-8.8f PE %d: LEVEL: msg" with seconds since start.
+static const char *const kLogNames[LOG_N] = {"FATAL", "INIT", "BARRIER", "BROADCAST",
+                                             "REDUCTION", "COLLECT", "MEMORY", "INFO"};
+
+struct LogState {
+    bool on[LOG_N] = {true};
+    FILE *out = stderr;
+    LogState() {
+        if (const char *levels = std::getenv("SHMEM_LOG_LEVELS")) {
+            std::string all(levels);
+            size_t pos = 0;
+            while (pos <= all.size()) {
+                const size_t end = all.find_first_of(",:;", pos);
+                std::string tok = all.substr(pos, end == std::string::npos ? std::string::npos : end - pos);
+                for (auto &c : tok) c = (char)std::toupper((unsigned char)c);
+                for (int i = 0; i < LOG_N; ++i)
+                    if (tok == "ALL" || tok == kLogNames[i]) on[i] = true;
+                if (end == std::string::npos) break;
+                pos = end + 1;
+            }
+        }
+        if (const char *f = std::getenv("SHMEM_LOG_FILE")) {
+            if (FILE *fp = std::fopen(f, "a")) out = fp;
+        }
+    }
+};
+
+static LogState &log_state() {
+    static LogState st;
+    return st;
+}
+
+bool log_enabled(int level) { return level >= 0 && level < LOG_N && log_state().on[level]; }
+
+void trace(int level, const char *fmt, ...) {
+    if (!log_enabled(level)) return;
     const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() -
                                                    g_state.t0).count();
     char msg[512];
@@ -59,15 +98,15 @@ void trace(const char *level, const char *fmt, ...) {
     va_start(ap, fmt);
     vsnprintf(msg, sizeof msg, fmt, ap);
     va_end(ap);
-    fprintf(stderr, "%-8.8f PE %d: %s: %s\n", t, g_state.pe, level, msg);
-    fflush(stderr);
+    FILE *out = log_state().out;
+    fprintf(out, "%-8.8f PE %d: %s: %s\n", t, g_state.pe, kLogNames[level], msg);
+    fflush(out);
 }
 
 [[noreturn]] void fatal(const char *what, const char *detail) {
-    trace("FATAL", "%s: %s", what, detail);
+    trace(LOG_FATAL, "%s: %s", what, detail);
     std::abort();
 }
-
 
 static int env_int(const char *a, const char *b, int dflt) {
     for (const char *k : {a, b}) {
@@ -119,6 +158,8 @@ static int init_locked(int pe, int npes, int device, const void *uid) {
     g_state.device = device;
     g_state.algo = parse_algo(std::getenv("SHMEM_REDUCE_ALGO"));
     g_state.inited = true;
+    trace(LOG_INIT, "PE %d of %d on HIP device %d%s", pe, npes, device,
+          g_state.comm ? ", RCCL communicator up" : "");
     return SHMEMX_OK;
 }
 
@@ -360,6 +401,17 @@ static int reduce_device(int type, int op, void *target, const void *source,
     char *tgt = static_cast<char *>(target);
     const char *src = static_cast<const char *>(source);
 
+    if (log_enabled(LOG_REDUCTION)) {
+        static const char *const algos[SHMEMX_NALGOS] = {"auto", "rccl", "a2a", "gather",
+                                                         "allreduce"};
+        trace(LOG_REDUCTION, "type %d op %d nreduce %d set (%d,%d,%d) member %d algo %s chunk %lld",
+              type, op, nreduce, start, logstride, size, p.member, algos[p.algo], p.chunk);
+        // the reference's own messages, reduce-op.c:199-210
+        trace(LOG_REDUCTION, overlap(tgt, src, bytes)
+                                 ? "target (%p) and source (%p, size %ld) overlap, using temporary target"
+                                 : "target (%p) and source (%p, size %ld) do not overlap",
+              target, source, (long)bytes);
+    }
     // Partially overlapping target/source: reduce from a private copy of the
     // source (the reference's temporary target, reduce-op.c:187-203).
     bool uses_ws = false;
@@ -506,12 +558,10 @@ void reduce_blocking(int type, int op, void *target, const void *source,
     std::lock_guard<std::recursive_mutex> lk(g_mu);
     t_last_error = SHMEMX_OK;
     if (ensure_init()) {
-        trace("FATAL", "reduction called before shmem_init with npes > 1");
+        trace(LOG_FATAL, "reduction called before shmem_init with npes > 1");
         return;
     }
     if (!op_on_device(type, op)) {
-        if (op_valid(type, op))
-            trace("FATAL", "type %d op %d (long double) is not implemented on the device in this build", type, op);
         set_error(op_valid(type, op) ? SHMEMX_ENOTSUP : SHMEMX_EINVAL);
         return;
     }

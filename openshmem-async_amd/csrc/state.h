@@ -53,8 +53,12 @@ extern std::recursive_mutex g_mu;   // the reference's state is not thread-safe 
 
 int set_error(int e);               // thread-local last error (shmemx_reduce_last_error)
 void clear_error();
-// "%-8.8f PE %d: LEVEL: msg", the reference's trace line (utils/trace.c:400-431)
-void trace(const char *level, const char *fmt, ...);
+// Trace facilities ($SHMEM_LOG_LEVELS, $SHMEM_LOG_FILE; utils/trace.c) and
+// the "%-8.8f PE %d: LEVEL: msg" line of utils/trace.c:400-431.
+enum { LOG_FATAL = 0, LOG_INIT, LOG_BARRIER, LOG_BROADCAST, LOG_REDUCTION, LOG_COLLECT,
+       LOG_MEMORY, LOG_INFO, LOG_N };
+bool log_enabled(int level);
+void trace(int level, const char *fmt, ...);
 [[noreturn]] void fatal(const char *what, const char *detail);
 
 #define SHMX_HIP(call)                                                         \

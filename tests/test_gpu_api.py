@@ -228,3 +228,29 @@ def test_host_small_messages_bounce_path(cuda, shm, oracle, n):
     tgt[:] = 0
     shm.to_all("int", "min", tgt, d, n, 0, 0, 1)                 # device -> host
     assert tgt.tobytes() == src.tobytes()
+
+
+def test_trace_facility(cuda, tmp_path):
+    """$SHMEM_LOG_LEVELS / $SHMEM_LOG_FILE as the reference's utils/trace.c:
+    facility names with ",:;" delimiters, the "%-8.8f PE %d: LEVEL: msg"
+    line, and the reference's own reduction messages (reduce-op.c:199-210)."""
+    import re
+    import subprocess
+    import sys
+    log = tmp_path / "shmem.log"
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys, numpy as np, torch; sys.path.insert(0, %r); import shmem_mi355x as s; "
+            "s.init(); a = np.arange(10.0); b = np.zeros(10); "
+            "s.to_all('double', 'sum', b, a, 10, 0, 0, 1); s.to_all('double', 'sum', a, a, 10, 0, 0, 1); "
+            "p = s.malloc(1 << 20); s.free(p); s.finalize()") % os.path.join(repo, "openshmem-async_amd")
+    env = dict(os.environ, SHMEM_LOG_LEVELS="reduction;Init,memory", SHMEM_LOG_FILE=str(log))
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr
+    text = log.read_text()
+    lines = text.strip().splitlines()
+    assert all(re.match(r"^\d+\.\d{8} PE 0: [A-Z]+: ", ln) for ln in lines), text
+    assert any(": INIT: PE 0 of 1" in ln for ln in lines)
+    assert any("do not overlap" in ln for ln in lines)
+    assert any(": MEMORY: shmem_malloc(1048576" in ln for ln in lines)
+    assert not any(": BARRIER: " in ln for ln in lines)          # not requested
