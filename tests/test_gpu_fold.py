@@ -238,3 +238,35 @@ def test_longdouble_x87_encodings(cuda, shm, oracle):
             torch.cuda.synchronize()
             got = from_dev(out, np.longdouble)
             assert same_bits(got, want), (op, order)
+
+
+def test_fold_fuzz_against_oracle(cuda, shm, oracle):
+    """400 random cases: type, op, 1..20 inputs, 0..70 000 elements, random
+    element offsets per array (same or different alignment mod 16), kind."""
+    import torch
+    rng = np.random.default_rng(20251015)
+    pairs = DEVICE_PAIRS
+    for case in range(400):
+        t, op = pairs[rng.integers(len(pairs))]
+        P = int(rng.integers(1, 21))
+        n = int(rng.integers(0, 70000)) if case % 4 else int(rng.integers(0, 300))
+        kind = int(rng.integers(0, 2))
+        srcs = oracle.sources(t, kind, P, n + 8, base_seed=int(rng.integers(1 << 40)))
+        offs = rng.integers(0, 4, size=P + 1) if case % 3 else np.full(P + 1, int(rng.integers(0, 4)))
+        dt = srcs.dtype
+        if dt.itemsize >= 16:
+            offs[:] = 0
+        view = np.stack([srcs[p][offs[p + 1]:offs[p + 1] + n] for p in range(P)])
+        want = oracle.reduce_sim(t, op, view, 0, 0, P)[0]
+        dev = [to_dev(torch, srcs[p]) for p in range(P)]
+        isz = dt.itemsize
+        ins = [d[offs[p + 1] * isz:(offs[p + 1] + n) * isz] if dt == np.longdouble
+               else d[offs[p + 1]:offs[p + 1] + n] for p, d in enumerate(dev)]
+        outbuf = to_dev(torch, np.zeros(n + 8, dtype=dt))
+        out = outbuf[offs[0] * isz:(offs[0] + n) * isz] if dt == np.longdouble \
+            else outbuf[offs[0]:offs[0] + n]
+        shm.fold_n(t, op, out, ins, n)
+        torch.cuda.synchronize()
+        got = from_dev(outbuf, dt)
+        assert same_bits(got[offs[0]:offs[0] + n], want), (case, t, op, P, n, list(offs))
+        assert not np.any(got[:offs[0]] != 0) and not np.any(got[offs[0] + n:] != 0), case
