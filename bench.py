@@ -286,6 +286,9 @@ def main():
         got = tgt[sample].cpu()
         tol = 2 * (world - 1) * 2.0 ** -53 * abs_sum
         ok = bool(((got - ref).abs() <= tol).all())
+        # the whole 32 Mi-element target must be identical on every PE
+        # (checksum of every PE's target, compared across the set)
+        ok = shm.verify("double", tgt, n, 0, 0, world) and ok
         ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
 
     if world == 1:

@@ -280,6 +280,16 @@ size_t shmemx_type_size(int type);
 int shmemx_op_valid(int type, int op);
 int shmemx_op_on_device(int type, int op);
 
+/* Position-aware 64-bit checksum of nelems elements (host or device memory;
+ * long double: value bytes only) — XOR over 8-byte words w_j of
+ * splitmix64-finalise(w_j + (j+1) * 0x9E3779B97F4A7C15); computed by a gfx950
+ * kernel (wave shuffle + LDS partials).  shmemx_verify: collective over the
+ * active set, *all_equal = 1 iff every member's target has the same checksum
+ * (what the A2A and RCCL algorithms guarantee after a reduction). */
+int shmemx_checksum(int type, const void *ptr, size_t nelems, unsigned long long *out);
+int shmemx_verify(int type, const void *target, int nreduce, int PE_start,
+                  int logPE_stride, int PE_size, int *all_equal);
+
 /* Last error of this thread and its text. */
 int shmemx_reduce_last_error(void);
 const char *shmemx_reduce_error_string(int err);

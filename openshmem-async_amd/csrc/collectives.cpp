@@ -236,6 +236,64 @@ int collect_impl(size_t esize, void *target, const void *source, size_t nelems, 
     return SHMEMX_OK;
 }
 
+// ------------------------------------------------------- checksum, verify
+int checksum_impl(int type, const void *ptr, size_t nelems, unsigned long long *out) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    clear_error();
+    if (int rc = ensure_init()) return rc;
+    if (!out || type_size(type) == 0) return set_error(SHMEMX_EINVAL);
+    hipStream_t s = g_state.stream;
+    const size_t bytes = nelems * type_size(type);
+    DevBuf in = device_in(ptr, bytes, g_state.cws_src, g_state.cws_src_bytes, s);
+    if (bytes && !in.dev) return set_error(SHMEMX_ENOMEM);
+    unsigned long long *dres = static_cast<unsigned long long *>(
+        grow(g_state.token, g_state.token_bytes, 4096));
+    if (!dres) return set_error(SHMEMX_ENOMEM);
+    if (launch_checksum(type, in.dev, nelems, dres, s) != hipSuccess) return set_error(SHMEMX_EINVAL);
+    SHMX_HIP(hipMemcpyAsync(out, dres, sizeof *out, hipMemcpyDeviceToHost, s));
+    SHMX_HIP(hipStreamSynchronize(s));
+    return SHMEMX_OK;
+}
+
+int verify_impl(int type, const void *target, int nreduce, int start, int logstride, int size,
+                int *all_equal) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    clear_error();
+    SetInfo si;
+    if (int rc = set_info(start, logstride, size, si)) return rc;
+    if (!all_equal || nreduce < 0) return set_error(SHMEMX_EINVAL);
+    unsigned long long mine = 0;
+    if (int rc = checksum_impl(type, target, (size_t)nreduce, &mine)) return rc;
+    std::vector<unsigned long long> all(si.P, mine);
+    if (collective(si)) {
+        hipStream_t s = g_state.stream;
+        unsigned long long *d = static_cast<unsigned long long *>(
+            grow(g_state.token, g_state.token_bytes, sizeof(unsigned long long) * (si.P + 8)));
+        if (!d) return set_error(SHMEMX_ENOMEM);
+        SHMX_HIP(hipMemcpyAsync(d + si.m, &mine, sizeof mine, hipMemcpyHostToDevice, s));
+        if (si.world) {
+            SHMX_NCCL(ncclAllGather(d + si.m, d, 1, ncclUint64, g_state.comm, s));
+        } else {
+            SHMX_NCCL(ncclGroupStart());
+            for (int i = 0; i < si.P; ++i) {
+                if (i == si.m) continue;
+                SHMX_NCCL(ncclSend(d + si.m, 1, ncclUint64, si.peer(i), g_state.comm, s));
+                SHMX_NCCL(ncclRecv(d + i, 1, ncclUint64, si.peer(i), g_state.comm, s));
+            }
+            SHMX_NCCL(ncclGroupEnd());
+        }
+        SHMX_HIP(hipMemcpyAsync(all.data(), d, sizeof(unsigned long long) * si.P,
+                                hipMemcpyDeviceToHost, s));
+        SHMX_HIP(hipStreamSynchronize(s));
+    }
+    int eq = 1;
+    for (unsigned long long v : all) eq &= v == mine;
+    *all_equal = eq;
+    trace(LOG_INFO, "verify: checksum %016llx, set (%d,%d,%d) %s", mine, start, logstride, size,
+          eq ? "consistent" : "INCONSISTENT");
+    return SHMEMX_OK;
+}
+
 // ---------------------------------------------------------- symmetric heap
 struct Block {
     void *base;
@@ -374,6 +432,15 @@ void *pshmem_realloc(void *ptr, size_t size) {
     }
     pshmem_barrier_all();
     return p;
+}
+
+int shmemx_checksum(int type, const void *ptr, size_t nelems, unsigned long long *out) {
+    return checksum_impl(type, ptr, nelems, out);
+}
+
+int shmemx_verify(int type, const void *target, int nreduce, int PE_start, int logPE_stride,
+                  int PE_size, int *all_equal) {
+    return verify_impl(type, target, nreduce, PE_start, logPE_stride, PE_size, all_equal);
 }
 
 void *pshmalloc(size_t size) { return pshmem_malloc(size); }

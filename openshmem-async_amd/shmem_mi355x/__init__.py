@@ -106,6 +106,10 @@ def lib() -> ctypes.CDLL:
             for name in (f"shmem_{kind}{bits}", f"pshmem_{kind}{bits}"):
                 getattr(L, name).argtypes = [vp, vp, sz, i, i, i, vp]
                 getattr(L, name).restype = None
+    L.shmemx_checksum.argtypes = [i, vp, sz, ctypes.POINTER(ctypes.c_ulonglong)]
+    L.shmemx_checksum.restype = i
+    L.shmemx_verify.argtypes = [i, vp, i, i, i, i, ctypes.POINTER(i)]
+    L.shmemx_verify.restype = i
     L.shmem_barrier.argtypes = [i, i, i, vp]
     L.shmem_barrier.restype = None
     L.shmem_barrier_all.restype = None
@@ -316,3 +320,20 @@ def realloc(ptr: int, nbytes: int) -> int:
 
 def free(ptr: int) -> None:
     lib().shmem_free(ptr or None)
+
+
+def checksum(type_name: str, ptr, nelems: int) -> int:
+    """shmemx_checksum: position-aware 64-bit checksum (gfx950 kernel)."""
+    out = ctypes.c_ulonglong(0)
+    _check(lib().shmemx_checksum(TYPES[type_name], addr(ptr), nelems, ctypes.byref(out)),
+           "shmemx_checksum")
+    return out.value
+
+
+def verify(type_name: str, target, nreduce: int, PE_start: int, logPE_stride: int,
+           PE_size: int) -> bool:
+    """shmemx_verify: do all members of the set hold the same target?"""
+    eq = ctypes.c_int(0)
+    _check(lib().shmemx_verify(TYPES[type_name], addr(target), nreduce, PE_start, logPE_stride,
+                               PE_size, ctypes.byref(eq)), "shmemx_verify")
+    return bool(eq.value)

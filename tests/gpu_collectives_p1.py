@@ -32,3 +32,7 @@ shm.barrier(0, 0, 1)
 shm.barrier_all()
 assert shm.last_error() == 0
 print("ok")
+# verify over a one-rank communicator (RCCL all-gather of the checksums)
+x = torch.arange(4097, dtype=torch.float64, device="cuda")
+assert shm.verify("double", x, 4097, 0, 0, 1)
+print("ok")

@@ -34,3 +34,29 @@ def value_bytes(a: np.ndarray) -> bytes:
 
 def same_bits(a: np.ndarray, b: np.ndarray) -> bool:
     return a.dtype == b.dtype and a.shape == b.shape and value_bytes(a) == value_bytes(b)
+
+
+def checksum64(a: np.ndarray) -> int:
+    """Host twin of shmemx_checksum (openshmem-async_amd/csrc/checksum.hip):
+    XOR over the little-endian 8-byte words w_j of the element bytes (long
+    double: 10 value bytes per 16-byte slot, the rest zero) of
+    splitmix64-finalise(w_j + (j + 1) * 0x9E3779B97F4A7C15)."""
+    a = np.ascontiguousarray(a)
+    b = a.view(np.uint8).reshape(-1)
+    if a.dtype == np.longdouble:
+        b = b.reshape(-1, 16).copy()
+        b[:, 10:] = 0
+        b = b.reshape(-1)
+    pad = (-len(b)) % 8
+    if pad:
+        b = np.concatenate([b, np.zeros(pad, np.uint8)])
+    w = b.view("<u8")
+    if len(w) == 0:
+        return 0
+    j = np.arange(1, len(w) + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = w + j * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return int(np.bitwise_xor.reduce(z))
