@@ -24,6 +24,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -42,6 +43,7 @@ State g_state;
 // up to kSmallHostBytes they bounce through page-locked buffers instead.
 constexpr size_t kStageChunkBytes = size_t(16) << 20;
 constexpr size_t kSmallHostBytes = size_t(256) << 10;
+constexpr size_t kRingSlots = 4;     // page-locked bounce slots per direction
 std::recursive_mutex g_mu;
 static thread_local int t_last_error = SHMEMX_OK;
 
@@ -552,6 +554,108 @@ bool host_pinned(const void *ptr) {
 // (used by entry.cpp; C++ linkage, not exported in the header)
 namespace shmx {
 
+// ------------------------------------------- page-locked ring, copy pool
+// Pageable host arrays (dlmalloc'd heaps, numpy) cannot be DMA'd
+// asynchronously; they go through kRingSlots page-locked slots per direction,
+// filled and emptied by a small pool of CPU threads, so the CPU copies of
+// one chunk overlap the PCIe transfers and device work of its neighbours.
+static bool ring_reserve(size_t slot_bytes) {
+    if (g_state.ring && g_state.ring_slot >= slot_bytes) return true;
+    if (g_state.ring) {
+        SHMX_HIP(hipDeviceSynchronize());
+        SHMX_HIP(hipHostFree(g_state.ring));
+        g_state.ring = nullptr;
+    }
+    if (hipHostMalloc(&g_state.ring, 2 * kRingSlots * slot_bytes, hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        g_state.ring = nullptr;
+        g_state.ring_slot = 0;
+        return false;
+    }
+    g_state.ring_slot = slot_bytes;
+    return true;
+}
+static char *ring_in(size_t slot) { return static_cast<char *>(g_state.ring) + slot * g_state.ring_slot; }
+static char *ring_out(size_t slot) {
+    return static_cast<char *>(g_state.ring) + (kRingSlots + slot) * g_state.ring_slot;
+}
+
+namespace {
+class CopyPool {
+  public:
+    CopyPool() {
+        unsigned hw = std::thread::hardware_concurrency();
+        nthreads_ = hw >= 16 ? 8 : (hw >= 4 ? hw / 2 : 1);
+        for (unsigned i = 1; i < nthreads_; ++i) workers_.emplace_back([this, i] { run(i); });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : workers_) t.join();
+    }
+    // memcpy split over the pool; returns when every piece is done
+    void copy(void *dst, const void *src, size_t bytes) {
+        if (bytes < (size_t(4) << 20) || nthreads_ == 1) {
+            std::memcpy(dst, src, bytes);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            dst_ = static_cast<char *>(dst);
+            src_ = static_cast<const char *>(src);
+            bytes_ = bytes;
+            pending_ = nthreads_ - 1;
+            ++gen_;
+        }
+        cv_.notify_all();
+        piece(0);
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [this] { return pending_ == 0; });
+    }
+
+  private:
+    void piece(unsigned i) {
+        const size_t per = (bytes_ / nthreads_ + 63) & ~size_t(63);
+        const size_t lo = std::min(bytes_, per * i), hi = std::min(bytes_, per * (i + 1));
+        if (hi > lo) std::memcpy(dst_ + lo, src_ + lo, hi - lo);
+    }
+    void run(unsigned i) {
+        unsigned long long seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+            }
+            piece(i);
+            {
+                std::lock_guard<std::mutex> lk(mu_);
+                if (--pending_ == 0) done_.notify_one();
+            }
+        }
+    }
+    unsigned nthreads_ = 1;
+    std::vector<std::thread> workers_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    bool stop_ = false;
+    unsigned long long gen_ = 0;
+    unsigned pending_ = 0;
+    char *dst_ = nullptr;
+    const char *src_ = nullptr;
+    size_t bytes_ = 0;
+};
+}  // namespace
+
+static void parallel_copy(void *dst, const void *src, size_t bytes) {
+    static CopyPool pool;
+    pool.copy(dst, src, bytes);
+}
+
 // The blocking entry point body: host- or device-resident arrays.
 void reduce_blocking(int type, int op, void *target, const void *source,
                      int nreduce, int start, int logstride, int size) {
@@ -652,39 +756,78 @@ void reduce_blocking(int type, int op, void *target, const void *source,
     if (chunk == 0) chunk = g;
     // a host target that partially overlaps the host source would be
     // overwritten under a later chunk's H2D: no pipelining then
-    if (!tdev && !sdev && overlap(target, source, bytes)) chunk = (size_t)nreduce;
-    if ((!tdev && !host_pinned(target)) || (!sdev && !host_pinned(source)))
-        chunk = (size_t)nreduce;
+    const bool host_overlap = !tdev && !sdev && overlap(target, source, bytes);
+    if (host_overlap) chunk = (size_t)nreduce;
     const size_t nchunks = ((size_t)nreduce + chunk - 1) / chunk;
-    while (g_state.events.size() < 2 * nchunks) {
+    // How each end reaches the device: directly (device memory), by DMA
+    // (page-locked host memory), or through the page-locked bounce ring
+    // (pageable memory: CPU copy by the worker pool, then DMA).
+    const bool in_bounce = !sdev && !host_pinned(source) && !host_overlap;
+    const bool out_bounce = !tdev && !host_pinned(target) && !host_overlap;
+    const size_t chunk_bytes = chunk * sz;
+    if ((in_bounce || out_bounce) && !ring_reserve(chunk_bytes)) {
+        set_error(SHMEMX_ENOMEM);
+        return;
+    }
+    while (g_state.events.size() < 2 * nchunks + 2 * kRingSlots) {
         hipEvent_t e;
         SHMX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         g_state.events.push_back(e);
     }
+    hipEvent_t *ev_chunk = g_state.events.data();             // 2 per chunk
+    hipEvent_t *ev_in_slot = ev_chunk + 2 * nchunks;          // ring slot free again
+    hipEvent_t *ev_out_slot = ev_in_slot + kRingSlots;        // ring slot filled
     char *hsrc = static_cast<char *>(const_cast<void *>(source));
     char *htgt = static_cast<char *>(target);
     char *ssrc = static_cast<char *>(g_state.stage_src);
     char *stgt = static_cast<char *>(g_state.stage_tgt);
+    size_t drained = 0;  // chunks copied out of the ring so far (out_bounce)
+    auto drain_one = [&]() {
+        const size_t j = drained++;
+        const size_t slot = j % kRingSlots;
+        const size_t cnt = std::min(chunk, (size_t)nreduce - j * chunk);
+        SHMX_HIP(hipEventSynchronize(ev_out_slot[slot]));
+        parallel_copy(htgt + j * chunk_bytes, ring_out(slot), cnt * sz);
+    };
     int rc = SHMEMX_OK;
     for (size_t k = 0; k < nchunks && !rc; ++k) {
-        const size_t off = k * chunk * sz;
+        const size_t off = k * chunk_bytes;
         const size_t cnt = std::min(chunk, (size_t)nreduce - k * chunk);
         const size_t b = cnt * sz;
+        const size_t slot = k % kRingSlots;
         const void *dsrc = hsrc + off;
         if (!sdev) {
-            SHMX_HIP(hipMemcpyAsync(ssrc + off, hsrc + off, b, hipMemcpyHostToDevice, g_state.h2d));
-            SHMX_HIP(hipEventRecord(g_state.events[2 * k], g_state.h2d));
-            SHMX_HIP(hipStreamWaitEvent(s, g_state.events[2 * k], 0));
+            const char *from = hsrc + off;
+            if (in_bounce) {
+                if (k >= kRingSlots) SHMX_HIP(hipEventSynchronize(ev_in_slot[slot]));
+                parallel_copy(ring_in(slot), hsrc + off, b);
+                from = ring_in(slot);
+            }
+            SHMX_HIP(hipMemcpyAsync(ssrc + off, from, b, hipMemcpyHostToDevice, g_state.h2d));
+            SHMX_HIP(hipEventRecord(ev_chunk[2 * k], g_state.h2d));
+            if (in_bounce) SHMX_HIP(hipEventRecord(ev_in_slot[slot], g_state.h2d));
+            SHMX_HIP(hipStreamWaitEvent(s, ev_chunk[2 * k], 0));
             dsrc = ssrc + off;
         }
         void *dtgt = tdev ? static_cast<void *>(htgt + off) : static_cast<void *>(stgt + off);
         rc = reduce_device(type, op, dtgt, dsrc, (int)cnt, start, logstride, size, g_state.algo, s);
         if (!rc && !tdev) {
-            SHMX_HIP(hipEventRecord(g_state.events[2 * k + 1], s));
-            SHMX_HIP(hipStreamWaitEvent(g_state.d2h, g_state.events[2 * k + 1], 0));
-            SHMX_HIP(hipMemcpyAsync(htgt + off, dtgt, b, hipMemcpyDeviceToHost, g_state.d2h));
+            SHMX_HIP(hipEventRecord(ev_chunk[2 * k + 1], s));
+            SHMX_HIP(hipStreamWaitEvent(g_state.d2h, ev_chunk[2 * k + 1], 0));
+            if (out_bounce) {
+                // the slot's previous chunk must be copied out before reuse
+                while (drained + kRingSlots <= k) drain_one();
+                SHMX_HIP(hipMemcpyAsync(ring_out(slot), dtgt, b, hipMemcpyDeviceToHost, g_state.d2h));
+                SHMX_HIP(hipEventRecord(ev_out_slot[slot], g_state.d2h));
+                // keep the CPU busy on the oldest finished chunk, one behind
+                if (k >= 1 && drained < k) drain_one();
+            } else {
+                SHMX_HIP(hipMemcpyAsync(htgt + off, dtgt, b, hipMemcpyDeviceToHost, g_state.d2h));
+            }
         }
     }
+    if (out_bounce && !rc)
+        while (drained < nchunks) drain_one();
     SHMX_HIP(hipStreamSynchronize(g_state.h2d));
     SHMX_HIP(hipStreamSynchronize(s));
     SHMX_HIP(hipStreamSynchronize(g_state.d2h));
@@ -744,6 +887,9 @@ void pshmem_finalize(void) {
     }
     g_state.ws_bytes = g_state.tmp_bytes = g_state.stage_bytes = 0;
     g_state.token_bytes = g_state.cws_src_bytes = g_state.cws_tgt_bytes = 0;
+    if (g_state.ring) (void)hipHostFree(g_state.ring);
+    g_state.ring = nullptr;
+    g_state.ring_slot = 0;
     if (g_state.bounce) (void)hipHostFree(g_state.bounce);
     g_state.bounce = nullptr;
     g_state.bounce_bytes = 0;

@@ -40,6 +40,8 @@ struct State {
     size_t cws_src_bytes = 0;
     void *cws_tgt = nullptr;
     size_t cws_tgt_bytes = 0;
+    void *ring = nullptr;      // page-locked bounce ring (large pageable arrays)
+    size_t ring_slot = 0;
     void *bounce = nullptr;    // page-locked host bounce buffers (small messages)
     size_t bounce_bytes = 0;
     hipStream_t h2d = nullptr;  // staging copy streams and their chunk events
