@@ -586,6 +586,8 @@ class CopyPool {
     CopyPool() {
         unsigned hw = std::thread::hardware_concurrency();
         nthreads_ = hw >= 16 ? 8 : (hw >= 4 ? hw / 2 : 1);
+        if (const char *e = std::getenv("SHMEMX_COPY_THREADS"))
+            nthreads_ = std::max(1, std::min(64, std::atoi(e)));
         for (unsigned i = 1; i < nthreads_; ++i) workers_.emplace_back([this, i] { run(i); });
     }
     ~CopyPool() {
@@ -752,7 +754,12 @@ void reduce_blocking(int type, int op, void *target, const void *source,
     }
     const size_t sz = type_size(type);
     const size_t g = sz >= 16 ? 1 : 16 / sz;
-    size_t chunk = ((kStageChunkBytes / sz) / g) * g;
+    static const size_t stage_chunk = [] {
+        const char *e = std::getenv("SHMEMX_STAGE_CHUNK_MB");
+        const int mb = e ? std::atoi(e) : 0;
+        return mb > 0 ? size_t(mb) << 20 : kStageChunkBytes;
+    }();
+    size_t chunk = ((stage_chunk / sz) / g) * g;
     if (chunk == 0) chunk = g;
     // a host target that partially overlaps the host source would be
     // overwritten under a later chunk's H2D: no pipelining then

@@ -1,0 +1,17 @@
+"""Host-resident end-to-end rate (32 Mi doubles, PE_size = 1) for one setting
+of SHMEMX_COPY_THREADS / SHMEMX_STAGE_CHUNK_MB (set by the caller)."""
+import os, statistics, sys, time
+import numpy as np, torch
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "openshmem-async_amd"))
+import shmem_mi355x as shm
+torch.cuda.set_device(0); shm.init_attr(0, 1, 0, None)
+n = 32 * 1024 * 1024
+src = np.random.default_rng(1).random(n) + 1; tgt = np.zeros(n)
+shm.to_all("double", "sum", tgt, src, n, 0, 0, 1)
+ts = []
+for _ in range(5):
+    t0 = time.perf_counter(); shm.to_all("double", "sum", tgt, src, n, 0, 0, 1); ts.append(time.perf_counter() - t0)
+t = statistics.median(ts)
+print(f"threads={os.environ.get('SHMEMX_COPY_THREADS','dflt')} chunkMB={os.environ.get('SHMEMX_STAGE_CHUNK_MB','dflt')} "
+      f"{t*1e3:.2f} ms {n*8/t/2**30:.1f} GiB/s ok={bool((tgt==src).all())}", flush=True)
