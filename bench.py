@@ -183,6 +183,48 @@ def latency_extras(world, barrier, max_over_ranks):
     return out
 
 
+def direct_extra(world, n, src, sp, stream, barrier, max_over_ranks, steps):
+    """SHMEMX_ALGO_DIRECT with source and target in the symmetric heap (HBM,
+    IPC-mapped): each PE's kernels read its peers' arrays over xGMI in place
+    (reduce-scatter then all-gather, both pulls).  Checked against the same
+    ULP bound as the main line and for cross-PE consistency."""
+    nbytes = n * 8
+    hs = ht = 0
+    try:
+        hs, ht = shm.malloc(nbytes), shm.malloc(nbytes)
+        if not hs or not ht:
+            return "shmem_malloc failed"
+        shm.memcpy(hs, src, nbytes)
+
+        def step():
+            shm.reduce_on_stream("double", "sum", ht, hs, n, 0, 0, world, "direct", sp)
+        for _ in range(2):
+            step()
+        w, _ = time_region(step, steps, stream, barrier)
+        w = max_over_ranks(w)
+        got = torch.empty(n, dtype=torch.float64, device="cuda")
+        shm.memcpy(got, ht, nbytes)
+        sample = torch.arange(0, n, max(1, n // 4096), device="cuda")
+        mine = src[sample].cpu()
+        import torch.distributed as dist
+        allv = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allv, mine)
+        ref = sum(allv[1:], allv[0].clone())
+        tol = 2 * (world - 1) * 2.0 ** -53 * sum((v.abs() for v in allv[1:]), allv[0].abs())
+        ok = bool(((got[sample].cpu() - ref).abs() <= tol).all())
+        ok = shm.verify("double", ht, n, 0, 0, world) and ok
+        ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
+        return {"GiBps": round(world * nbytes * steps / w / GiB, 2),
+                "ms_per_call": round(w / steps * 1e3, 3), "correct": ok}
+    except shm.ShmemError as e:
+        return str(e)
+    finally:
+        if ht:
+            shm.free(ht)
+        if hs:
+            shm.free(hs)
+
+
 def time_region(fn, steps, stream, barrier):
     """Run fn() `steps` times on `stream`; returns (wall_s, event_s)."""
     barrier()
@@ -208,6 +250,12 @@ def main():
         if world == 1 and a.gpus > 1:
             sys.exit("bench.py --gpus N>1 must be launched with torch.distributed.run")
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+    # SHMEMX_SHARE_GPU=1: every rank on device 0 (a rehearsal of the N > 1
+    # path on a one-GPU box, IPC transport only; never a reported number)
+    share = os.environ.get("SHMEMX_SHARE_GPU") == "1"
+    if share and os.environ.get("SHMEMX_TRANSPORT") != "ipc":
+        sys.exit("SHMEMX_SHARE_GPU=1 needs SHMEMX_TRANSPORT=ipc (RCCL refuses two ranks on one GPU)")
+    local = 0 if share else local
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
@@ -341,6 +389,8 @@ def main():
                     extras[f"algo_{alt}_GiBps"] = round(world * nbytes * k3 / w3 / GiB, 2)
                 except shm.ShmemError as e:
                     extras[f"algo_{alt}_GiBps"] = str(e)
+            extras["direct_heap"] = direct_extra(world, n, src, sp, stream, barrier, max_over_ranks,
+                                                 max(3, a.steps // 4))
             extras["configs"] = config_extras(world, stream, barrier, max_over_ranks)
             extras["latency"] = latency_extras(world, barrier, max_over_ranks)
 
@@ -356,7 +406,8 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
             "config": {"workload": workload, "nreduce": n, "type": "double", "op": "sum",
                        "PE_size": world, "algo": algo_used,
-                       "parallelism": f"one PE per GPU x{world}"},
+                       "parallelism": f"one PE per GPU x{world}",
+                       "transport": os.environ.get("SHMEMX_TRANSPORT", "rccl")},
             "roofline": roofline, "cpu_baseline": cpu, "correct": ok, "extras": extras,
         }
         print(json.dumps(line), flush=True)

@@ -201,10 +201,20 @@ enum {
  *           every PE gets the reference's PE_start result bit for bit
  *   GATHER  every PE receives every source and folds in its own reference
  *           order: bit-exact with the reference on EVERY PE, (P-1)x traffic
- *   ALLREDUCE  one ncclAllReduce (full set, RCCL-native pairs, as RCCL) */
+ *   ALLREDUCE  one ncclAllReduce (full set, RCCL-native pairs, as RCCL)
+ *   DIRECT  one HIP kernel per PE reads slice m of every member's source
+ *           straight from the peers' HBM (IPC-mapped symmetric heap, over
+ *           xGMI), folds in active-set order and stores the result into
+ *           every member's target; host barriers before and after (the
+ *           reference's two).  Any set of <= 16 PEs, any op, PE_start bits
+ *           on every PE.  Operands outside the symmetric heap are staged
+ *           through an IPC scratch region.  Host-synchronous.
+ * With $SHMEMX_TRANSPORT=ipc there is no RCCL communicator: AUTO means
+ * DIRECT, GATHER runs as a DIRECT-style kernel in each PE's own order, and
+ * RCCL / A2A / ALLREDUCE are ENOTSUP. */
 enum {
     SHMEMX_ALGO_AUTO = 0, SHMEMX_ALGO_RCCL, SHMEMX_ALGO_A2A,
-    SHMEMX_ALGO_GATHER, SHMEMX_ALGO_ALLREDUCE, SHMEMX_NALGOS
+    SHMEMX_ALGO_GATHER, SHMEMX_ALGO_ALLREDUCE, SHMEMX_ALGO_DIRECT, SHMEMX_NALGOS
 };
 
 /* Error codes returned by shmemx_* and stored for shmemx_reduce_last_error. */
@@ -220,7 +230,10 @@ enum {
 
 /* Bootstrap with a caller-distributed RCCL unique id (128 bytes): PE `pe` of
  * `npes` on HIP device `device` (-1: pe mod device count).  PE 0 creates the
- * id with shmemx_get_uniqueid() and the launcher broadcasts it. */
+ * id with shmemx_get_uniqueid() and the launcher broadcasts it.  The id also
+ * names the job's intra-node block (/dev/shm) that carries the symmetric-heap
+ * IPC handles and the host barrier; all PEs run on one node.
+ * $SHMEMX_TRANSPORT=ipc (set alike on every PE) skips RCCL entirely. */
 int shmemx_uniqueid_size(void);
 int shmemx_get_uniqueid(void *uid_out);
 int shmemx_init_attr(int pe, int npes, int device, const void *uid);
@@ -230,7 +243,7 @@ int shmemx_initialized(void);
 void *shmemx_get_stream(void);
 
 /* Algorithm used by the entry points (default AUTO, or $SHMEM_REDUCE_ALGO =
- * auto|rccl|a2a|gather|allreduce).  Returns the previous value. */
+ * auto|rccl|a2a|gather|allreduce|direct).  Returns the previous value. */
 int shmemx_set_algo(int algo);
 
 /* Stream-ordered reduction: enqueue on `stream` (hipStream_t; NULL = the
@@ -272,6 +285,12 @@ typedef struct {
 int shmemx_reduce_plan(int type, int op, int nreduce, int PE_start,
                        int logPE_stride, int PE_size, int pe, int npes,
                        int algo, shmemx_plan_t *plan);
+
+/* Address of the symmetric object `addr` (in this PE's symmetric heap) as
+ * mapped on this PE for PE `pe`'s copy — a device pointer a HIP kernel here
+ * can load from / store to over xGMI (the shmem_ptr idea, querying/ptr.c).
+ * NULL if `addr` is not in the heap segment or the peer is not mapped. */
+void *shmemx_heap_ptr(const void *addr, int pe);
 
 /* Element size in bytes of a SHMEMX_TYPE_* (0 if unknown); 1 if the
  * reference defines shmem_<type>_<op>_to_all (reduce-op.c:388-431);

@@ -17,10 +17,14 @@
 // OpenSHMEM, so no sub-communicator is needed).  Host buffers are staged
 // through device workspaces; pSync is never written.
 //
-// The symmetric heap is HBM: shmem_malloc returns device memory (hipMalloc),
-// collectively (a barrier_all follows, symmem.c:209), so a program keeps its
-// symmetric arrays resident on the GPU and the reductions take the
-// device-resident path.
+// The symmetric heap is HBM (heap.h): shmem_malloc returns device memory
+// from this PE's IPC-exported segment, collectively (a barrier_all follows,
+// symmem.c:209), so a program keeps its symmetric arrays resident on the GPU,
+// the reductions take the device-resident path, and the DIRECT algorithm
+// reads peers' copies in place.
+//
+// On the IPC transport ($SHMEMX_TRANSPORT=ipc, no RCCL communicator) the
+// barrier is the node block's host barrier (node.h).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -29,7 +33,9 @@
 #include <mutex>
 #include <vector>
 
+#include "heap.h"
 #include "internal.h"
+#include "node.h"
 #include "shmem_reduce_mi355x.h"
 #include "state.h"
 
@@ -54,11 +60,17 @@ int set_info(int start, int logstride, int size, SetInfo &si) {
     si.step = 1 << logstride;
     si.world = start == 0 && (logstride == 0 || size == 1) && size == g_state.npes;
     if (!is_member(g_state.pe, start, logstride, size, &si.m)) return set_error(SHMEMX_ENOTMEMBER);
-    if ((size > 1 || g_state.force_collective) && !g_state.comm) return set_error(SHMEMX_ENOINIT);
+    if ((size > 1 || g_state.force_collective) && !g_state.comm && !node::up())
+        return set_error(SHMEMX_ENOINIT);
     return SHMEMX_OK;
 }
 
 bool collective(const SetInfo &si) { return si.P > 1 || g_state.force_collective; }
+
+// Collectives other than the barrier and the reductions need RCCL for now.
+int need_rccl(const SetInfo &si) {
+    return collective(si) && !g_state.comm ? set_error(SHMEMX_ENOTSUP) : SHMEMX_OK;
+}
 
 // A device view of a possibly host-resident buffer.
 struct DevBuf {
@@ -114,6 +126,10 @@ int barrier_impl(int start, int logstride, int size) {
     SHMX_HIP(hipStreamSynchronize(s));
     trace(LOG_BARRIER, "set (%d,%d,%d) member %d", start, logstride, size, si.m);
     if (!collective(si)) return SHMEMX_OK;
+    if (!g_state.comm) {   // IPC transport
+        node::barrier(si.start, si.step, si.P);
+        return SHMEMX_OK;
+    }
     char *tok = token_area(si.P);
     if (!tok) return set_error(SHMEMX_ENOMEM);
     if (si.world) {
@@ -139,6 +155,7 @@ int broadcast_impl(size_t esize, void *target, const void *source, size_t nelems
     SetInfo si;
     if (int rc = set_info(start, logstride, size, si)) return rc;
     if (root_idx < 0 || root_idx >= size) return set_error(SHMEMX_EINVAL);
+    if (int rc = need_rccl(si)) return rc;
     const size_t bytes = nelems * esize;
     trace(LOG_BROADCAST, "%zu bytes from set member %d, set (%d,%d,%d) member %d", bytes, root_idx,
           start, logstride, size, si.m);
@@ -181,6 +198,7 @@ int collect_impl(size_t esize, void *target, const void *source, size_t nelems, 
     clear_error();
     SetInfo si;
     if (int rc = set_info(start, logstride, size, si)) return rc;
+    if (int rc = need_rccl(si)) return rc;
     hipStream_t s = g_state.stream;
     std::vector<long long> counts(si.P, (long long)nelems);
     if (!fixed && collective(si)) {
@@ -265,7 +283,15 @@ int verify_impl(int type, const void *target, int nreduce, int start, int logstr
     unsigned long long mine = 0;
     if (int rc = checksum_impl(type, target, (size_t)nreduce, &mine)) return rc;
     std::vector<unsigned long long> all(si.P, mine);
-    if (collective(si)) {
+    if (collective(si) && !g_state.comm) {
+        // IPC transport: the checksums travel in the node block's descriptors
+        node::Desc d;
+        d.aux = mine;
+        node::put_desc(d);
+        node::barrier(si.start, si.step, si.P);
+        for (int i = 0; i < si.P; ++i) all[i] = node::get_desc(si.peer(i)).aux;
+        node::barrier(si.start, si.step, si.P);   // all read before any descriptor changes
+    } else if (collective(si)) {
         hipStream_t s = g_state.stream;
         unsigned long long *d = static_cast<unsigned long long *>(
             grow(g_state.token, g_state.token_bytes, sizeof(unsigned long long) * (si.P + 8)));
@@ -295,39 +321,17 @@ int verify_impl(int type, const void *target, int nreduce, int start, int logstr
 }
 
 // ---------------------------------------------------------- symmetric heap
-struct Block {
-    void *base;
-    size_t bytes;
-};
-std::map<void *, Block> g_heap;   // user pointer -> allocation
-
 void *heap_alloc(size_t alignment, size_t bytes) {
     if (ensure_init()) return nullptr;
     if (!bytes) return nullptr;
-    const size_t pad = alignment > 256 ? alignment : 0;
-    void *base = nullptr;
-    if (hipMalloc(&base, bytes + pad) != hipSuccess) {
-        (void)hipGetLastError();
-        set_error(SHMEMX_ENOMEM);
-        return nullptr;
-    }
-    uintptr_t u = reinterpret_cast<uintptr_t>(base);
-    if (pad) u = (u + alignment - 1) & ~(uintptr_t)(alignment - 1);
-    void *p = reinterpret_cast<void *>(u);
-    g_heap[p] = Block{base, bytes};
+    void *p = heap::alloc(alignment, bytes);
+    if (!p) set_error(SHMEMX_ENOMEM);
     trace(LOG_MEMORY, "shmem_malloc(%zu bytes, align %zu) = %p (HBM)", bytes, alignment, p);
     return p;
 }
 
 void heap_free(void *p) {
-    auto it = g_heap.find(p);
-    if (it == g_heap.end()) {
-        set_error(SHMEMX_EINVAL);
-        return;
-    }
-    SHMX_HIP(hipDeviceSynchronize());
-    SHMX_HIP(hipFree(it->second.base));
-    g_heap.erase(it);
+    if (!heap::free(p)) set_error(SHMEMX_EINVAL);
 }
 
 }  // namespace
@@ -419,14 +423,14 @@ void *pshmem_realloc(void *ptr, size_t size) {
         pshmem_free(ptr);
         return nullptr;
     }
-    auto it = g_heap.find(ptr);
-    if (it == g_heap.end()) {
+    const size_t old_bytes = heap::size_of(ptr);
+    if (!old_bytes) {
         set_error(SHMEMX_EINVAL);
         return nullptr;
     }
     void *p = heap_alloc(0, size);
     if (p) {
-        const size_t keep = it->second.bytes < size ? it->second.bytes : size;
+        const size_t keep = old_bytes < size ? old_bytes : size;
         SHMX_HIP(hipMemcpy(p, ptr, keep, hipMemcpyDeviceToDevice));
         heap_free(ptr);
     }

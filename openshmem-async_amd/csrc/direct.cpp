@@ -1,0 +1,211 @@
+// DIRECT algorithm: the reference's reduction (reduce-op.c:169-260) as the
+// reference itself structures it — every PE reads its peers' symmetric
+// source arrays — but with the reads done by a HIP kernel straight out of
+// the peers' HBM over xGMI (IPC-mapped symmetric heap, node.h / heap.h)
+// instead of 64-element shmem_getmem round trips into pWrk, and the fold
+// fused into that same pass.
+//
+// Set order (SHMEMX_ALGO_DIRECT), two pull phases, no intermediate buffers:
+//   1. reduce-scatter: member m folds slice m of the array from all P
+//      sources in active-set order (PE_start first, as A2A does) into slice
+//      m of its own target — one kernel reading all P sources at once;
+//   2. all-gather: member m copies every other member's result slice from
+//      that member's target into its own — one kernel for all P-1 slices.
+// (P-1)/P of the array crosses xGMI in each phase, as reads only: a PE never
+// stores into another GPU's HBM, so no remote L2 can hold a stale copy of
+// what it later reads (peer data is read after the owner's kernel has ended
+// and a barrier, the usual P2P read discipline).  Every PE ends with the
+// reference's PE_start result.
+//
+// Own order (SHMEMX_ALGO_GATHER on the IPC transport): every PE folds the
+// whole array in its own reference order, src_me first, then the other
+// members ascending (reduce-op.c:219-248), reading (P-1) peer arrays: the
+// reference's per-PE bits on every PE.
+//
+// Synchronisation is the reference's: a barrier before the peers' sources
+// are read (reduce-op.c:217) and one after the targets are final (:250),
+// plus one between the two phases; host barriers over the node block.  Operands outside the symmetric heap (or
+// a source that partially overlaps its target) are staged through a per-PE
+// scratch region, also IPC-mapped, in chunks of half its size
+// ($SHMEMX_DIRECT_SCRATCH_MB, default 512; every PE must use the same value).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <vector>
+
+#include "heap.h"
+#include "internal.h"
+#include "node.h"
+#include "shmem_reduce_mi355x.h"
+#include "state.h"
+
+namespace shmx {
+
+namespace {
+
+constexpr size_t kDefaultScratchBytes = size_t(512) << 20;
+
+struct Scratch {
+    char *base = nullptr;
+    size_t bytes = 0;
+} g_scratch;
+
+bool ensure_scratch() {
+    if (g_scratch.base) return true;
+    size_t bytes = kDefaultScratchBytes;
+    if (const char *e = std::getenv("SHMEMX_DIRECT_SCRATCH_MB")) {
+        const long mb = std::atol(e);
+        if (mb > 0) bytes = size_t(mb) << 20;
+    }
+    void *p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    g_scratch.base = static_cast<char *>(p);
+    g_scratch.bytes = bytes;
+    node::publish(node::kScratch, p, bytes);   // peers map it after the next barrier
+    trace(LOG_MEMORY, "DIRECT scratch: %zu bytes of HBM at %p", bytes, p);
+    return true;
+}
+
+}  // namespace
+
+void direct_release() {
+    if (!g_scratch.base) return;
+    node::unpublish(node::kScratch);
+    (void)hipFree(g_scratch.base);
+    g_scratch = Scratch{};
+}
+
+int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int start,
+                  int logstride, const shmemx_plan_t &p, bool own_order, hipStream_t s) {
+    const int P = p.nmembers, m = p.member, step = 1 << logstride;
+    if (!node::up()) return set_error(SHMEMX_ENOTSUP);
+    if (stream_capturing(s)) return set_error(SHMEMX_ENOTSUP);   // host barriers inside
+    if (!own_order && P > kMaxFoldInputs) return set_error(SHMEMX_ENOTSUP);   // one gather launch
+    if (!ensure_scratch()) return set_error(SHMEMX_ENOMEM);
+    const size_t sz = (size_t)p.elem_size;
+    const size_t n = (size_t)nreduce;
+    const size_t bytes = n * sz;
+    const size_t g = sz >= 16 ? 1 : 16 / sz;
+    const size_t half = g_scratch.bytes / 2;
+    const size_t cmax = std::max(g, (half / sz) / g * g);   // elements per staged chunk
+    auto pe_of = [&](int i) { return start + i * step; };
+
+    // Where my operands live for the peers.  A source that partially
+    // overlaps the target (the reference's temporary, reduce-op.c:187-203)
+    // or that is outside the heap is staged; in own order every PE writes
+    // only its own target, so it needs staging only when the target aliases
+    // the source (peers still read the source).
+    node::Desc d;
+    uint64_t off = 0;
+    const bool partial = tgt != src && tgt < src + bytes && src < tgt + bytes;
+    const bool stage_src = partial || !heap::offset_of(src, bytes, &off);
+    if (stage_src) d.src = node::Loc{node::kScratch, 0};
+    else d.src = node::Loc{node::kHeap, off};
+    bool stage_tgt;
+    if (own_order) {
+        stage_tgt = tgt < src + bytes && src < tgt + bytes;   // any aliasing
+        d.tgt = node::Loc{};
+    } else {
+        stage_tgt = !heap::offset_of(tgt, bytes, &off);
+        if (stage_tgt) d.tgt = node::Loc{node::kScratch, half};
+        else d.tgt = node::Loc{node::kHeap, off};
+    }
+    // count: bit 0 "I stage through scratch", bit 1 "my target starts inside
+    // my source" — then chunks must run last to first, as memmove would, or
+    // a chunk's copy-out overwrites source elements of the next chunk
+    d.count = (stage_src || stage_tgt ? 1 : 0) | (partial && tgt > src ? 2 : 0);
+    node::put_desc(d);
+    SHMX_HIP(hipStreamSynchronize(s));   // my source is complete
+    node::barrier(start, step, P);       // reduce-op.c:217
+
+    // Every member reads the same descriptors, so all cut the same chunks
+    // and walk them in the same direction.
+    std::vector<node::Desc> desc(P);
+    bool chunked = false, backwards = false;
+    for (int i = 0; i < P; ++i) {
+        desc[i] = i == m ? d : node::get_desc(pe_of(i));
+        chunked |= (desc[i].count & 1) != 0;
+        backwards |= (desc[i].count & 2) != 0;
+    }
+    std::vector<char *> sbase(P), tbase(P);
+    for (int i = 0; i < P; ++i) {
+        char *b = node::peer_base(static_cast<node::Region>(desc[i].src.region), pe_of(i));
+        if (!b) fatal("DIRECT reduction", "a member's source region is not mapped");
+        sbase[i] = b + desc[i].src.off;
+        if (!own_order) {
+            char *t = node::peer_base(static_cast<node::Region>(desc[i].tgt.region), pe_of(i));
+            if (!t) fatal("DIRECT reduction", "a member's target region is not mapped");
+            tbase[i] = t + desc[i].tgt.off;
+        }
+    }
+    const size_t C = chunked ? cmax : std::max<size_t>(n, 1);
+    const size_t nchunks = (n + C - 1) / C;
+    char *const scratch_src = g_scratch.base;
+    char *const scratch_tgt = g_scratch.base + half;
+    std::vector<const void *> ins(P);
+    for (size_t j = 0; j < nchunks; ++j) {
+        const size_t k = backwards ? nchunks - 1 - j : j;
+        const size_t c0 = k * C, cnt = std::min(C, n - c0);
+        if (chunked) {
+            // the staged chunk in; the previous chunk's exit barrier has
+            // already seen every member done reading my scratch
+            if (stage_src)
+                SHMX_HIP(hipMemcpyAsync(scratch_src, src + c0 * sz, cnt * sz, hipMemcpyDeviceToDevice, s));
+            SHMX_HIP(hipStreamSynchronize(s));
+            node::barrier(start, step, P);
+        }
+        // a staged operand holds only the current chunk, at its region offset
+        auto at = [&](char *base, const node::Loc &l, size_t elem) {
+            return base + (l.region == node::kScratch ? elem - c0 : elem) * sz;
+        };
+        if (own_order) {
+            ins[0] = at(sbase[m], desc[m].src, c0);
+            int k2 = 1;
+            for (int i = 0; i < P; ++i)
+                if (i != m) ins[k2++] = at(sbase[i], desc[i].src, c0);
+            char *out = stage_tgt ? scratch_tgt : tgt + c0 * sz;
+            fold_chain(type, op, out, ins.data(), P, cnt, s);
+            SHMX_HIP(hipStreamSynchronize(s));
+            node::barrier(start, step, P);   // reduce-op.c:250: every target chunk final
+            if (stage_tgt)
+                SHMX_HIP(hipMemcpyAsync(tgt + c0 * sz, scratch_tgt, cnt * sz, hipMemcpyDeviceToDevice, s));
+            continue;
+        }
+        // set order: slice i of the chunk belongs to member i
+        size_t slice = (cnt + P - 1) / P;
+        slice = (slice + g - 1) / g * g;
+        auto lo_of = [&](int i) { return std::min(cnt, (size_t)i * slice); };
+        auto hi_of = [&](int i) { return std::min(cnt, (size_t)(i + 1) * slice); };
+        const size_t lo = lo_of(m), hi = hi_of(m);
+        // 1. my slice from every member's source, into my published target
+        if (hi > lo) {
+            for (int i = 0; i < P; ++i) ins[i] = at(sbase[i], desc[i].src, c0 + lo);
+            char *out = at(tbase[m], desc[m].tgt, c0 + lo);
+            SHMX_HIP(launch_fold(type, op, out, ins.data(), P, hi - lo, s));
+        }
+        SHMX_HIP(hipStreamSynchronize(s));
+        node::barrier(start, step, P);   // every member's slice is final
+        // 2. every other member's slice (and mine, if it was staged) into my target
+        std::vector<const void *> from;
+        std::vector<void *> to;
+        std::vector<size_t> len;
+        for (int i = 0; i < P; ++i) {
+            if (i == m && !stage_tgt) continue;
+            if (hi_of(i) <= lo_of(i)) continue;
+            from.push_back(at(tbase[i], desc[i].tgt, c0 + lo_of(i)));
+            to.push_back(tgt + (c0 + lo_of(i)) * sz);
+            len.push_back((hi_of(i) - lo_of(i)) * sz);
+        }
+        SHMX_HIP(launch_gather(from.data(), to.data(), len.data(), (int)from.size(), s));
+        SHMX_HIP(hipStreamSynchronize(s));
+        node::barrier(start, step, P);   // reduce-op.c:250: no member reads my slice any more
+    }
+    if (own_order && stage_tgt) SHMX_HIP(hipStreamSynchronize(s));
+    return SHMEMX_OK;
+}
+
+}  // namespace shmx

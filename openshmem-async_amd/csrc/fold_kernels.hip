@@ -423,25 +423,18 @@ bool op_valid(int type, int op) {
 
 bool op_on_device(int type, int op) { return op_valid(type, op); }
 
-hipError_t launch_fold(int type, int op, void *out, const void *const *ins,
-                       int nins, size_t n, hipStream_t stream) {
-    if (!op_on_device(type, op) || nins < 1 || nins > kMaxFoldInputs || !out)
-        return hipErrorInvalidValue;
-    if (n == 0) return hipSuccess;
+namespace {
+
+// Split n elements into scalar head, 16-B vector body and scalar tail, given
+// every array's address (the body only if all share one offset mod 16 that is
+// a whole number of elements), then dispatch on type.
+hipError_t dispatch(int type, int op, FoldArgs &a, const void *const *ptrs, int nptrs, size_t n,
+                    hipStream_t stream) {
     const size_t sz = type_size(type);
-    FoldArgs a{};
-    a.out = out;
-    a.nins = nins;
-    for (int k = 0; k < nins; ++k) {
-        if (!ins[k]) return hipErrorInvalidValue;
-        a.ins[k] = ins[k];
-    }
-    // Vector body only if every array sits at the same offset mod 16 and that
-    // offset is a whole number of elements.
-    const uintptr_t off = reinterpret_cast<uintptr_t>(out) & 15u;
+    const uintptr_t off = reinterpret_cast<uintptr_t>(ptrs[0]) & 15u;
     bool same = (off % sz) == 0;
-    for (int k = 0; k < nins && same; ++k)
-        same = (reinterpret_cast<uintptr_t>(ins[k]) & 15u) == off;
+    for (int k = 1; k < nptrs && same; ++k)
+        same = (reinterpret_cast<uintptr_t>(ptrs[k]) & 15u) == off;
     if (same) {
         size_t head = ((16 - off) & 15u) / sz;
         if (head > n) head = n;
@@ -466,6 +459,100 @@ hipError_t launch_fold(int type, int op, void *out, const void *const *ins,
     case SHMEMX_TYPE_COMPLEXF: return launch_cplx_ops<cplxf>(op, a, stream);
     default: return hipErrorInvalidValue;
     }
+}
+
+}  // namespace
+
+hipError_t launch_fold(int type, int op, void *out, const void *const *ins,
+                       int nins, size_t n, hipStream_t stream) {
+    if (!op_on_device(type, op) || nins < 1 || nins > kMaxFoldInputs || !out)
+        return hipErrorInvalidValue;
+    if (n == 0) return hipSuccess;
+    FoldArgs a{};
+    a.out = out;
+    a.nins = nins;
+    const void *ptrs[kMaxFoldInputs + 1];
+    ptrs[0] = out;
+    for (int k = 0; k < nins; ++k) {
+        if (!ins[k]) return hipErrorInvalidValue;
+        a.ins[k] = ins[k];
+        ptrs[k + 1] = ins[k];
+    }
+    return dispatch(type, op, a, ptrs, nins + 1, n, stream);
+}
+
+// ------------------------------------------------------------ gather copy
+// DIRECT's all-gather phase: up to kMaxFoldInputs byte ranges (each a slice
+// of a peer's result, read over xGMI) copied into this PE's target by ONE
+// launch, blockIdx.y = segment, so the reads from all peers are in flight at
+// once (one copy per peer would serialise the links).
+namespace {
+
+struct CopySeg {
+    const unsigned char *src;
+    unsigned char *dst;
+    size_t bytes;
+};
+struct GatherArgs {
+    CopySeg seg[kMaxFoldInputs];
+};
+
+constexpr int kGatherUnroll = 4;
+
+__global__ __launch_bounds__(kBlock) void gather_kernel(GatherArgs a) {
+    const CopySeg sg = a.seg[blockIdx.y];
+    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t nthr = (size_t)gridDim.x * kBlock;
+    const uintptr_t d = reinterpret_cast<uintptr_t>(sg.dst);
+    const uintptr_t s = reinterpret_cast<uintptr_t>(sg.src);
+    size_t head = (16 - (d & 15)) & 15;
+    if (head > sg.bytes) head = sg.bytes;
+    if (((s + head) & 15) != 0) {   // source and target disagree mod 16: bytes
+        for (size_t i = tid; i < sg.bytes; i += nthr) sg.dst[i] = sg.src[i];
+        return;
+    }
+    const size_t nvec = (sg.bytes - head) / 16;
+    const size_t tail0 = head + nvec * 16;
+    if (tid < head) sg.dst[tid] = sg.src[tid];
+    if (tid < sg.bytes - tail0) sg.dst[tail0 + tid] = sg.src[tail0 + tid];
+    const u32x4 *in = reinterpret_cast<const u32x4 *>(sg.src + head);
+    u32x4 *out = reinterpret_cast<u32x4 *>(sg.dst + head);
+    const size_t step = nthr * kGatherUnroll;
+    size_t v = (size_t)blockIdx.x * kBlock * kGatherUnroll + threadIdx.x;
+    for (; v + (size_t)(kGatherUnroll - 1) * kBlock < nvec; v += step) {
+        u32x4 x[kGatherUnroll];
+#pragma unroll
+        for (int u = 0; u < kGatherUnroll; ++u) x[u] = __builtin_nontemporal_load(in + v + u * kBlock);
+#pragma unroll
+        for (int u = 0; u < kGatherUnroll; ++u) __builtin_nontemporal_store(x[u], out + v + u * kBlock);
+    }
+    for (int u = 0; u < kGatherUnroll; ++u) {
+        const size_t w = v + (size_t)u * kBlock;
+        if (w < nvec) __builtin_nontemporal_store(__builtin_nontemporal_load(in + w), out + w);
+    }
+}
+
+}  // namespace
+
+hipError_t launch_gather(const void *const *srcs, void *const *dsts, const size_t *bytes, int nseg,
+                         hipStream_t stream) {
+    if (nseg < 0 || nseg > kMaxFoldInputs) return hipErrorInvalidValue;
+    GatherArgs a{};
+    size_t most = 0;
+    int k = 0;
+    for (int i = 0; i < nseg; ++i) {
+        if (!bytes[i]) continue;
+        if (!srcs[i] || !dsts[i]) return hipErrorInvalidValue;
+        a.seg[k++] = CopySeg{static_cast<const unsigned char *>(srcs[i]),
+                             static_cast<unsigned char *>(dsts[i]), bytes[i]};
+        most = bytes[i] > most ? bytes[i] : most;
+    }
+    if (!k) return hipSuccess;
+    size_t bx = (most / 16 + (size_t)kBlock * kGatherUnroll - 1) / ((size_t)kBlock * kGatherUnroll);
+    if (bx < 1) bx = 1;
+    if (bx > 65535) bx = 65535;
+    hipLaunchKernelGGL(gather_kernel, dim3((unsigned)bx, (unsigned)k), dim3(kBlock), 0, stream, a);
+    return hipGetLastError();
 }
 
 }  // namespace shmx

@@ -1,0 +1,122 @@
+// The symmetric heap on HBM (heap.h): one segment per PE, exported over IPC.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <map>
+
+#include "heap.h"
+#include "node.h"
+#include "shmem_reduce_mi355x.h"
+#include "state.h"
+
+namespace shmx {
+namespace heap {
+
+namespace {
+
+// The reference's default is 32 MiB (comms-shared.h:74) for a host heap; an
+// MI355X PE has 288 GB of HBM, and the heap holds whole reduction operands.
+constexpr uint64_t kDefaultHeapBytes = uint64_t(4) << 30;
+
+struct Private {
+    void *base;     // what hipMalloc returned
+    size_t bytes;   // what the caller asked for
+};
+
+struct Heap {
+    char *base = nullptr;     // the segment (nullptr until the first allocation)
+    bool failed = false;      // the segment could not be allocated
+    Arena arena;
+    std::map<void *, Private> priv;   // blocks outside the segment
+} g_heap;
+
+bool ensure_segment() {
+    if (g_heap.base) return true;
+    if (g_heap.failed) return false;
+    uint64_t bytes = kDefaultHeapBytes;
+    if (const char *e = std::getenv("SHMEM_SYMMETRIC_HEAP_SIZE")) {
+        if (!parse_size(e, &bytes) || bytes == 0)
+            fatal("shmem_malloc", "unusable SHMEM_SYMMETRIC_HEAP_SIZE");
+    }
+    bytes = (bytes + (uint64_t(1) << 21) - 1) & ~((uint64_t(1) << 21) - 1);   // 2 MiB pages
+    void *p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        g_heap.failed = true;
+        trace(LOG_MEMORY, "symmetric heap segment of %llu bytes not available",
+              (unsigned long long)bytes);
+        return false;
+    }
+    g_heap.base = static_cast<char *>(p);
+    g_heap.arena.reset(bytes);
+    node::publish(node::kHeap, p, bytes);   // peers map it after the allocation's barrier
+    trace(LOG_MEMORY, "symmetric heap segment: %llu bytes of HBM at %p", (unsigned long long)bytes, p);
+    return true;
+}
+
+bool in_segment(const void *p) {
+    const char *c = static_cast<const char *>(p);
+    return g_heap.base && c >= g_heap.base && c < g_heap.base + g_heap.arena.capacity();
+}
+
+}  // namespace
+
+void *alloc(size_t alignment, size_t bytes) {
+    if (!bytes) return nullptr;
+    if (ensure_segment()) {
+        const uint64_t off = g_heap.arena.alloc(bytes, alignment ? alignment : 1);
+        if (off != Arena::kNone) return g_heap.base + off;
+    }
+    // Outside the segment: a private block.  Every PE makes the same choice,
+    // since the segment's state is the same on every PE.
+    const size_t pad = alignment > 256 ? alignment : 0;
+    void *base = nullptr;
+    if (hipMalloc(&base, bytes + pad) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    uintptr_t u = reinterpret_cast<uintptr_t>(base);
+    if (pad) u = (u + alignment - 1) & ~(uintptr_t)(alignment - 1);
+    void *p = reinterpret_cast<void *>(u);
+    g_heap.priv[p] = Private{base, bytes};
+    return p;
+}
+
+bool free(void *p) {
+    if (in_segment(p)) return g_heap.arena.free((uint64_t)(static_cast<char *>(p) - g_heap.base));
+    auto it = g_heap.priv.find(p);
+    if (it == g_heap.priv.end()) return false;
+    SHMX_HIP(hipDeviceSynchronize());
+    SHMX_HIP(hipFree(it->second.base));
+    g_heap.priv.erase(it);
+    return true;
+}
+
+size_t size_of(const void *p) {
+    if (in_segment(p)) return g_heap.arena.size_of((uint64_t)(static_cast<const char *>(p) - g_heap.base));
+    auto it = g_heap.priv.find(const_cast<void *>(p));
+    return it == g_heap.priv.end() ? 0 : it->second.bytes;
+}
+
+bool offset_of(const void *p, size_t bytes, uint64_t *off) {
+    if (!in_segment(p)) return false;
+    const uint64_t o = (uint64_t)(static_cast<const char *>(p) - g_heap.base);
+    if (bytes > g_heap.arena.capacity() - o) return false;
+    *off = o;
+    return true;
+}
+
+void release_all() {
+    for (auto &kv : g_heap.priv) (void)hipFree(kv.second.base);
+    if (g_heap.base) {
+        node::unpublish(node::kHeap);
+        (void)hipFree(g_heap.base);
+    }
+    g_heap.priv.clear();
+    g_heap.base = nullptr;
+    g_heap.failed = false;
+    g_heap.arena.reset(0);
+}
+
+}  // namespace heap
+}  // namespace shmx

@@ -1,0 +1,61 @@
+// The symmetric heap on HBM (memory/symmem.c:168-227, memalloc.c:64-146).
+//
+// One device segment per PE, sized by $SHMEM_SYMMETRIC_HEAP_SIZE (the
+// reference's variable and unit syntax, utils/unitparse.c:102-135), carved by
+// a deterministic first-fit allocator: identical collective call sequences
+// give identical offsets on every PE, so an address in this PE's heap names
+// the same object at the same offset in every other PE's heap — the
+// reference's symmetric-address rule (comms-inline.h:514-545).  The segment
+// is exported over IPC (node.h), so kernels reach a peer's copy over xGMI.
+// Requests the segment cannot hold fall back to private hipMalloc blocks
+// (still HBM, still usable by every algorithm, but not peer-addressable).
+//
+// Internal to libshmem_reduce_mi355x.so.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <map>
+
+namespace shmx {
+namespace heap {
+
+// The segment allocator alone (arena.cpp), host-only and testable without a
+// GPU (tests/native/test_heap.cpp): offsets within [0, capacity).
+class Arena {
+  public:
+    static constexpr uint64_t kGranule = 256;   // every block starts 256-B aligned
+    static constexpr uint64_t kNone = ~uint64_t(0);
+    explicit Arena(uint64_t capacity = 0) { reset(capacity); }
+    void reset(uint64_t capacity);
+    // offset of a new block of `bytes` aligned to `alignment` (a power of
+    // two), or kNone if it does not fit
+    uint64_t alloc(uint64_t bytes, uint64_t alignment);
+    uint64_t size_of(uint64_t off) const;   // requested size of the live block at off, or 0
+    bool free(uint64_t off);
+    uint64_t capacity() const { return capacity_; }
+    uint64_t free_bytes() const;
+    size_t live_blocks() const { return used_.size(); }
+
+  private:
+    struct Used {
+        uint64_t start, len, bytes;   // extent [start, start + len) holds the block
+    };
+    uint64_t capacity_ = 0;
+    std::map<uint64_t, uint64_t> free_;   // start -> length, coalesced
+    std::map<uint64_t, Used> used_;       // user offset -> extent
+};
+
+// $SHMEM_SYMMETRIC_HEAP_SIZE syntax: digits with an optional k/m/g/t/p/e
+// (powers of 1024); false if malformed.
+bool parse_size(const char *s, uint64_t *bytes);
+
+void *alloc(size_t alignment, size_t bytes);   // local part of shmem_malloc/align
+bool free(void *p);
+size_t size_of(const void *p);                  // 0 if not a heap block
+// Offset of [p, p + bytes) inside this PE's segment; false if not inside it.
+bool offset_of(const void *p, size_t bytes, uint64_t *off);
+void release_all();                             // shmem_finalize
+
+}  // namespace heap
+}  // namespace shmx

@@ -27,6 +27,11 @@ bool op_on_device(int type, int op);   // this build has a HIP kernel for it
 hipError_t launch_fold(int type, int op, void *out, const void *const *ins,
                        int nins, size_t n, hipStream_t stream);
 
+// Copy nseg (<= kMaxFoldInputs) byte ranges srcs[i] -> dsts[i] in one launch
+// (DIRECT all-gather: the peers' result slices, read concurrently).
+hipError_t launch_gather(const void *const *srcs, void *const *dsts, const size_t *bytes, int nseg,
+                         hipStream_t stream);
+
 // Position-aware 64-bit checksum of n elements of `type` at device address
 // ptr (16-byte aligned) into *out (device memory), stream-ordered.
 hipError_t launch_checksum(int type, const void *ptr, size_t n, unsigned long long *out,

@@ -1,0 +1,194 @@
+// Intra-node shared block, host barrier and IPC peer mappings (node.h).
+#include "node.h"
+
+#include <fcntl.h>
+#include <sched.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "state.h"
+
+namespace shmx {
+namespace node {
+
+namespace {
+
+struct RegionSlot {
+    hipIpcMemHandle_t handle;
+    uint64_t bytes;
+    std::atomic<uint64_t> gen;   // 0 = never published
+};
+
+struct PeSlot {
+    RegionSlot region[kNumRegions];
+    Desc desc;
+};
+
+struct Shared {
+    PeSlot pe[kMaxPes];
+    // flag[to][from]: barriers `from` has entered together with `to`
+    std::atomic<uint64_t> flag[kMaxPes][kMaxPes];
+};
+static_assert(std::atomic<uint64_t>::is_always_lock_free, "lock-free 64-bit atomics needed");
+
+struct Mapping {
+    char *base = nullptr;
+    uint64_t gen = 0;
+    uint64_t bytes = 0;
+};
+
+struct Node {
+    Shared *sh = nullptr;
+    std::string name;
+    int pe = 0, npes = 0;
+    uint64_t entered[kMaxPes] = {};     // barriers entered with each peer
+    char *own[kNumRegions] = {};
+    Mapping peer[kNumRegions][kMaxPes];
+} g_node;
+
+double barrier_timeout_s() {
+    static const double t = [] {
+        const char *e = std::getenv("SHMEMX_BARRIER_TIMEOUT");
+        const double v = e ? std::atof(e) : 0.0;
+        return v > 0 ? v : 600.0;
+    }();
+    return t;
+}
+
+void close_peer(Region r, int q) {
+    Mapping &mp = g_node.peer[r][q];
+    if (mp.base) (void)hipIpcCloseMemHandle(mp.base);
+    mp = Mapping{};
+}
+
+}  // namespace
+
+bool up() { return g_node.sh != nullptr; }
+
+bool attach(int pe, int npes, const void *key, size_t keylen) {
+    if (g_node.sh) return true;
+    if (npes < 1 || npes > kMaxPes || pe < 0 || pe >= npes) return false;
+    // FNV-1a of the job id: a fresh name per job, so no stale block is reused
+    uint64_t h = 1469598103934665603ull;
+    const unsigned char *k = static_cast<const unsigned char *>(key);
+    for (size_t i = 0; i < keylen; ++i) h = (h ^ k[i]) * 1099511628211ull;
+    char name[64];
+    snprintf(name, sizeof name, "/shmemx_node_%016llx", (unsigned long long)h);
+    const int fd = shm_open(name, O_RDWR | O_CREAT, 0600);
+    if (fd < 0) return false;
+    // every PE sizes it; a fresh object reads as zeros
+    if (ftruncate(fd, sizeof(Shared)) != 0) {
+        close(fd);
+        return false;
+    }
+    void *p = mmap(nullptr, sizeof(Shared), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) return false;
+    g_node.sh = static_cast<Shared *>(p);
+    g_node.name = name;
+    g_node.pe = pe;
+    g_node.npes = npes;
+    std::memset(g_node.entered, 0, sizeof g_node.entered);
+    trace(LOG_INIT, "node block %s attached (%zu bytes)", name, sizeof(Shared));
+    return true;
+}
+
+void detach(bool unlink_name) {
+    if (!g_node.sh) return;
+    for (int r = 0; r < kNumRegions; ++r)
+        for (int q = 0; q < kMaxPes; ++q) close_peer(static_cast<Region>(r), q);
+    munmap(g_node.sh, sizeof(Shared));
+    if (unlink_name) shm_unlink(g_node.name.c_str());
+    g_node = Node{};
+}
+
+void barrier(int start, int step, int P) {
+    Shared *sh = g_node.sh;
+    if (!sh || P <= 1) return;
+    const int me = g_node.pe;
+    for (int i = 0; i < P; ++i) {
+        const int q = start + i * step;
+        if (q == me) continue;
+        ++g_node.entered[q];
+        sh->flag[q][me].fetch_add(1, std::memory_order_acq_rel);
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < P; ++i) {
+        const int q = start + i * step;
+        if (q == me) continue;
+        unsigned spins = 0;
+        while (sh->flag[me][q].load(std::memory_order_acquire) < g_node.entered[q]) {
+            if (++spins < 256) continue;
+            sched_yield();
+            if ((spins & 1023) == 0 &&
+                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() >
+                    barrier_timeout_s()) {
+                char why[96];
+                snprintf(why, sizeof why, "PE %d never reached the barrier", q);
+                fatal("node barrier", why);
+            }
+        }
+    }
+}
+
+void publish(Region r, void *base, size_t bytes) {
+    if (!g_node.sh) return;
+    RegionSlot &s = g_node.sh->pe[g_node.pe].region[r];
+    SHMX_HIP(hipIpcGetMemHandle(&s.handle, base));
+    s.bytes = bytes;
+    s.gen.fetch_add(1, std::memory_order_release);
+    g_node.own[r] = static_cast<char *>(base);
+}
+
+void unpublish(Region r) {
+    if (!g_node.sh) return;
+    g_node.own[r] = nullptr;
+}
+
+char *peer_base(Region r, int q) {
+    if (!g_node.sh || q < 0 || q >= g_node.npes) return nullptr;
+    if (q == g_node.pe) return g_node.own[r];
+    RegionSlot &s = g_node.sh->pe[q].region[r];
+    const uint64_t gen = s.gen.load(std::memory_order_acquire);
+    if (gen == 0) return nullptr;
+    Mapping &mp = g_node.peer[r][q];
+    if (mp.base && mp.gen == gen) return mp.base;
+    close_peer(r, q);
+    void *p = nullptr;
+    hipError_t e = hipIpcOpenMemHandle(&p, s.handle, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        trace(LOG_MEMORY, "hipIpcOpenMemHandle(PE %d, region %d) failed: %s", q, (int)r,
+              hipGetErrorString(e));
+        return nullptr;
+    }
+    mp.base = static_cast<char *>(p);
+    mp.gen = gen;
+    mp.bytes = s.bytes;
+    trace(LOG_MEMORY, "mapped PE %d's %s (%llu bytes) at %p", q, r == kHeap ? "heap" : "scratch",
+          (unsigned long long)s.bytes, p);
+    return mp.base;
+}
+
+size_t peer_bytes(Region r, int q) {
+    if (!g_node.sh || q < 0 || q >= g_node.npes) return 0;
+    return g_node.sh->pe[q].region[r].bytes;
+}
+
+void put_desc(const Desc &d) {
+    if (g_node.sh) g_node.sh->pe[g_node.pe].desc = d;   // published by the next barrier
+}
+
+Desc get_desc(int q) {
+    return g_node.sh ? g_node.sh->pe[q].desc : Desc{};
+}
+
+}  // namespace node
+}  // namespace shmx

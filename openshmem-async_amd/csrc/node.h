@@ -1,0 +1,67 @@
+// Intra-node layer: what the reference gets from GASNet's segment table and
+// active messages (comms/gasnet/comms-inline.h:722-801, barrier-linear.c),
+// rebuilt for "one PE per GPU, all GPUs in one node":
+//
+//   * a small POSIX shared-memory block per job (/dev/shm), named from the
+//     job's unique id, holding per-PE IPC handles of two device regions (the
+//     symmetric heap segment and a DIRECT-algorithm scratch region), per-call
+//     descriptors, and pairwise barrier counters;
+//   * a host barrier over any active set (PE_start, logPE_stride, PE_size);
+//   * peer mappings of those regions (hipIpcOpenMemHandle), so a HIP kernel
+//     on this GPU loads from and stores to another PE's HBM over xGMI, the
+//     way the reference's shmem_getmem reads a peer's symmetric segment.
+//
+// Internal to libshmem_reduce_mi355x.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace shmx {
+namespace node {
+
+constexpr int kMaxPes = 64;
+enum Region { kHeap = 0, kScratch = 1, kNumRegions = 2 };
+
+// Where a PE's operand of the current call lives: in one of its regions at
+// an offset (peer-addressable), or nowhere (count only).
+struct Loc {
+    int32_t region = -1;   // kHeap, kScratch, or -1
+    uint64_t off = 0;
+};
+
+// Per-call descriptor a PE publishes before the entry barrier of a
+// collective; members read each other's after it.
+struct Desc {
+    Loc src, tgt;
+    int64_t count = 0;     // elements or bytes this PE contributes (collect)
+    uint64_t aux = 0;      // checksum (verify)
+};
+
+// Attach the job's shared block; `key` is the job's unique id (every PE
+// passes the same bytes).  Returns false (and leaves the layer down) on any
+// OS error.
+bool attach(int pe, int npes, const void *key, size_t keylen);
+void detach(bool unlink_name);
+bool up();
+
+// Host barrier among the members start + i*step, i < P (the caller is one of
+// them).  Aborts after $SHMEMX_BARRIER_TIMEOUT seconds (default 600).
+void barrier(int start, int step, int P);
+
+// Publish one of this PE's device regions (base, bytes); bumps its generation.
+void publish(Region r, void *base, size_t bytes);
+void unpublish(Region r);
+// Base of PE `pe`'s region as mapped here (own base for pe == me); nullptr
+// if the peer has not published it.  Opens / re-opens the IPC mapping when
+// the peer's generation changed.
+char *peer_base(Region r, int pe);
+size_t peer_bytes(Region r, int pe);
+
+void put_desc(const Desc &d);
+Desc get_desc(int pe);
+
+}  // namespace node
+}  // namespace shmx

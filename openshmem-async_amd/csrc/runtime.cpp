@@ -31,7 +31,11 @@
 #include <thread>
 #include <vector>
 
+#include <fcntl.h>
+
+#include "heap.h"
 #include "internal.h"
+#include "node.h"
 #include "shmem_reduce_mi355x.h"
 #include "state.h"
 
@@ -127,7 +131,24 @@ static int parse_algo(const char *s) {
     if (v == "a2a") return SHMEMX_ALGO_A2A;
     if (v == "gather") return SHMEMX_ALGO_GATHER;
     if (v == "allreduce") return SHMEMX_ALGO_ALLREDUCE;
+    if (v == "direct") return SHMEMX_ALGO_DIRECT;
     return SHMEMX_ALGO_AUTO;
+}
+
+static bool ipc_transport_env() {
+    const char *t = std::getenv("SHMEMX_TRANSPORT");
+    return t && std::string(t) == "ipc";
+}
+
+// A job id: RCCL's unique id, or 128 random bytes on the IPC transport
+// (which never starts RCCL).
+static bool make_uid(ncclUniqueId *id) {
+    if (!ipc_transport_env()) return ncclGetUniqueId(id) == ncclSuccess;
+    const int fd = open("/dev/urandom", O_RDONLY);
+    if (fd < 0) return false;
+    const bool ok = read(fd, id, sizeof *id) == (ssize_t)sizeof *id;
+    close(fd);
+    return ok;
 }
 
 static int init_locked(int pe, int npes, int device, const void *uid) {
@@ -145,23 +166,30 @@ static int init_locked(int pe, int npes, int device, const void *uid) {
     // streams must be synchronised by the caller, as for any HIP library.
     SHMX_HIP(hipStreamCreate(&g_state.stream));
     g_state.force_collective = env_int("SHMEMX_FORCE_COLLECTIVE", nullptr, 0) != 0;
-    if (npes > 1) {
-        if (!uid) return set_error(SHMEMX_EINVAL);
+    g_state.ipc_only = ipc_transport_env();
+    if (npes > 1 || g_state.force_collective) {
         ncclUniqueId id;
-        std::memcpy(&id, uid, sizeof id);
-        SHMX_NCCL(ncclCommInitRank(&g_state.comm, npes, id, pe));
-    } else if (g_state.force_collective) {
-        ncclUniqueId id;
-        SHMX_NCCL(ncclGetUniqueId(&id));
-        SHMX_NCCL(ncclCommInitRank(&g_state.comm, 1, id, 0));
+        if (npes > 1) {
+            if (!uid) return set_error(SHMEMX_EINVAL);
+            std::memcpy(&id, uid, sizeof id);
+        } else if (!make_uid(&id)) {
+            fatal("shmem_init", "cannot make a job id");
+        }
+        if (!g_state.ipc_only) SHMX_NCCL(ncclCommInitRank(&g_state.comm, npes, id, pe));
+        // the intra-node block (symmetric-heap IPC handles, host barrier):
+        // required on the IPC transport, an extra (DIRECT) otherwise
+        if (!node::attach(pe, npes, &id, sizeof id)) {
+            if (g_state.ipc_only) fatal("shmem_init", "cannot attach the intra-node block (/dev/shm)");
+            trace(LOG_INIT, "no intra-node block: the DIRECT algorithm is unavailable");
+        }
     }
     g_state.pe = pe;
     g_state.npes = npes;
     g_state.device = device;
     g_state.algo = parse_algo(std::getenv("SHMEM_REDUCE_ALGO"));
     g_state.inited = true;
-    trace(LOG_INIT, "PE %d of %d on HIP device %d%s", pe, npes, device,
-          g_state.comm ? ", RCCL communicator up" : "");
+    trace(LOG_INIT, "PE %d of %d on HIP device %d%s%s", pe, npes, device,
+          g_state.comm ? ", RCCL communicator up" : "", node::up() ? ", node block up" : "");
     return SHMEMX_OK;
 }
 
@@ -178,7 +206,7 @@ static int file_bootstrap(int pe, int npes, int device) {
     ncclUniqueId id;
     const time_t started = time(nullptr);
     if (pe == 0) {
-        SHMX_NCCL(ncclGetUniqueId(&id));
+        if (!make_uid(&id)) fatal("shmem_init", "cannot make a job id");
         const std::string tmp = path + ".tmp." + std::to_string(getpid());
         FILE *f = fopen(tmp.c_str(), "wb");
         if (!f || fwrite(&id, sizeof id, 1, f) != 1) fatal("shmem_init", "cannot write bootstrap file");
@@ -280,11 +308,16 @@ static int make_plan(int type, int op, int nreduce, int start, int logstride,
     const int sz = (int)type_size(type);
     const long long g = sz >= 16 ? 1 : 16 / sz;  // elements per 16-byte granule
     const bool world = start == 0 && (logstride == 0 || size == 1) && size == npes;
-    if (algo == SHMEMX_ALGO_AUTO)
-        algo = (world && rccl_native(type, op)) ? SHMEMX_ALGO_RCCL : SHMEMX_ALGO_A2A;
+    if (algo == SHMEMX_ALGO_AUTO) {
+        if (g_state.ipc_only) algo = SHMEMX_ALGO_DIRECT;
+        else algo = (world && rccl_native(type, op)) ? SHMEMX_ALGO_RCCL : SHMEMX_ALGO_A2A;
+    }
     if ((algo == SHMEMX_ALGO_RCCL || algo == SHMEMX_ALGO_ALLREDUCE) &&
         !(world && rccl_native(type, op)))
         return SHMEMX_ENOTSUP;
+    if (g_state.ipc_only && algo != SHMEMX_ALGO_DIRECT && algo != SHMEMX_ALGO_GATHER)
+        return SHMEMX_ENOTSUP;   // no RCCL communicator on the IPC transport
+    if (algo == SHMEMX_ALGO_DIRECT && size > kMaxFoldInputs) return SHMEMX_ENOTSUP;
     p->algo = algo;
     p->member = m;
     p->nmembers = P;
@@ -310,9 +343,14 @@ static int make_plan(int type, int op, int nreduce, int start, int logstride,
         p->ws_bytes = c * P * sz;
         break;
     }
-    default:  // GATHER
+    case SHMEMX_ALGO_DIRECT: {   // slice per member; no workspace
+        long long c = (n + P - 1) / P;
+        p->chunk = (c + g - 1) / g * g;
+        break;
+    }
+    default:  // GATHER (IPC transport: read in place, no workspace)
         p->chunk = n;
-        p->ws_bytes = n * P * sz;
+        p->ws_bytes = g_state.ipc_only ? 0 : n * P * sz;
         break;
     }
     return SHMEMX_OK;
@@ -342,18 +380,18 @@ void *grow(void *&buf, size_t &have, size_t need) {
 // a use on stream s waits for the previous use when that was on another
 // stream.  Skipped while s is being captured into a graph (a captured graph
 // lives on one stream; events recorded in a capture do not fire until replay).
-static bool capturing(hipStream_t s) {
+bool stream_capturing(hipStream_t s) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
 }
 
 static void ws_acquire(hipStream_t s) {
-    if (g_state.ws_stream && g_state.ws_stream != s && !capturing(s))
+    if (g_state.ws_stream && g_state.ws_stream != s && !stream_capturing(s))
         SHMX_HIP(hipStreamWaitEvent(s, g_state.ws_event, 0));
 }
 
 static void ws_release(hipStream_t s) {
-    if (capturing(s)) return;
+    if (stream_capturing(s)) return;
     if (!g_state.ws_event) SHMX_HIP(hipEventCreateWithFlags(&g_state.ws_event, hipEventDisableTiming));
     SHMX_HIP(hipEventRecord(g_state.ws_event, s));
     g_state.ws_stream = s;
@@ -369,8 +407,8 @@ static long long count_of(long long n, long long chunk, int i) {
     return std::max(0LL, std::min(chunk, n - lo));
 }
 
-static void fold_chain(int type, int op, void *out, const void **ins, int nins,
-                       size_t n, hipStream_t s) {
+void fold_chain(int type, int op, void *out, const void **ins, int nins, size_t n,
+                hipStream_t s) {
     // Left fold in groups of kMaxFoldInputs: out = fold(ins[0..15]);
     // out = fold(out, ins[16..30]); ... (same order as one long fold).
     int done = std::min(nins, kMaxFoldInputs);
@@ -397,7 +435,18 @@ static int reduce_device(int type, int op, void *target, const void *source,
                        g_state.npes, algo, &p);
     if (rc) return set_error(rc);
     if (nreduce == 0) return SHMEMX_OK;
-    if (size > 1 && !g_state.comm) return set_error(SHMEMX_ENOINIT);
+    const bool collective = size > 1 || g_state.force_collective;
+    const bool over_ipc = p.algo == SHMEMX_ALGO_DIRECT ||
+                          (p.algo == SHMEMX_ALGO_GATHER && g_state.ipc_only);
+    if (collective && over_ipc) {
+        if (log_enabled(LOG_REDUCTION))
+            trace(LOG_REDUCTION, "type %d op %d nreduce %d set (%d,%d,%d) member %d algo %s",
+                  type, op, nreduce, start, logstride, size, p.member,
+                  p.algo == SHMEMX_ALGO_DIRECT ? "direct" : "gather (ipc)");
+        return direct_reduce(type, op, static_cast<char *>(target), static_cast<const char *>(source),
+                             nreduce, start, logstride, p, p.algo == SHMEMX_ALGO_GATHER, s);
+    }
+    if (collective && !g_state.comm) return set_error(SHMEMX_ENOINIT);
     const size_t sz = (size_t)p.elem_size;
     const size_t bytes = sz * (size_t)nreduce;
     char *tgt = static_cast<char *>(target);
@@ -405,7 +454,7 @@ static int reduce_device(int type, int op, void *target, const void *source,
 
     if (log_enabled(LOG_REDUCTION)) {
         static const char *const algos[SHMEMX_NALGOS] = {"auto", "rccl", "a2a", "gather",
-                                                         "allreduce"};
+                                                         "allreduce", "direct"};
         trace(LOG_REDUCTION, "type %d op %d nreduce %d set (%d,%d,%d) member %d algo %s chunk %lld",
               type, op, nreduce, start, logstride, size, p.member, algos[p.algo], p.chunk);
         // the reference's own messages, reduce-op.c:199-210
@@ -883,6 +932,11 @@ void pshmem_finalize(void) {
     std::lock_guard<std::recursive_mutex> lk(g_mu);
     if (!g_state.inited) return;
     (void)hipStreamSynchronize(g_state.stream);
+    // collective: no PE frees memory its peers may still be reading
+    if (node::up()) node::barrier(0, 1, g_state.npes);
+    heap::release_all();
+    direct_release();
+    node::detach(g_state.pe == 0);
     if (g_state.comm) {
         ncclCommDestroy(g_state.comm);
         g_state.comm = nullptr;
@@ -924,7 +978,7 @@ int shmemx_uniqueid_size(void) { return (int)sizeof(ncclUniqueId); }
 int shmemx_get_uniqueid(void *uid_out) {
     if (!uid_out) return set_error(SHMEMX_EINVAL);
     ncclUniqueId id;
-    if (ncclGetUniqueId(&id) != ncclSuccess) return set_error(SHMEMX_EDEVICE);
+    if (!make_uid(&id)) return set_error(SHMEMX_EDEVICE);
     std::memcpy(uid_out, &id, sizeof id);
     return SHMEMX_OK;
 }
@@ -935,6 +989,16 @@ int shmemx_init_attr(int pe, int npes, int device, const void *uid) {
 }
 
 int shmemx_initialized(void) { return g_state.inited ? 1 : 0; }
+
+void *shmemx_heap_ptr(const void *addr, int pe) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    if (!g_state.inited || pe < 0 || pe >= g_state.npes) return nullptr;
+    uint64_t off = 0;
+    if (!heap::offset_of(addr, 1, &off)) return nullptr;
+    if (pe == g_state.pe) return const_cast<void *>(addr);
+    char *b = node::peer_base(node::kHeap, pe);
+    return b ? b + off : nullptr;
+}
 
 void *shmemx_get_stream(void) {
     std::lock_guard<std::recursive_mutex> lk(g_mu);

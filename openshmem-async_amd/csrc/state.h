@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include "shmem_reduce_mi355x.h"
+
 #include <chrono>
 #include <mutex>
 #include <vector>
@@ -20,6 +22,9 @@ struct State {
     hipStream_t stream = nullptr;
     ncclComm_t comm = nullptr;
     int algo = SHMEMX_ALGO_AUTO;
+    // $SHMEMX_TRANSPORT=ipc: no RCCL communicator; every collective runs over
+    // the node block and IPC-mapped HBM (node.h, direct.cpp)
+    bool ipc_only = false;
     // test hook ($SHMEMX_FORCE_COLLECTIVE=1): a 1-PE job still builds an RCCL
     // communicator and runs the collective schedules, so a one-GPU box can
     // execute every RCCL call of the path
@@ -79,5 +84,13 @@ bool is_member(int pe, int start, int logstride, int size, int *index);
 bool device_accessible(const void *ptr);
 bool host_pinned(const void *ptr);
 void *grow(void *&buf, size_t &have, size_t need);   // grow-only device buffer
+bool stream_capturing(hipStream_t s);
+// out = left fold of ins[0..nins) in groups of kMaxFoldInputs (any nins)
+void fold_chain(int type, int op, void *out, const void **ins, int nins, size_t n, hipStream_t s);
+// DIRECT algorithm (direct.cpp); own_order: every PE folds in its own
+// reference order (GATHER semantics on the IPC transport)
+int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int start,
+                  int logstride, const shmemx_plan_t &p, bool own_order, hipStream_t s);
+void direct_release();
 
 }  // namespace shmx

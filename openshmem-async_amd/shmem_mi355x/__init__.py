@@ -24,7 +24,7 @@ LIB_PATH = os.path.join(os.path.dirname(_HERE), "libshmem_reduce_mi355x.so")
 TYPES = {"short": 0, "int": 1, "long": 2, "longlong": 3, "float": 4,
          "double": 5, "longdouble": 6, "complexd": 7, "complexf": 8}
 OPS = {"sum": 0, "prod": 1, "and": 2, "or": 3, "xor": 4, "min": 5, "max": 6}
-ALGOS = {"auto": 0, "rccl": 1, "a2a": 2, "gather": 3, "allreduce": 4}
+ALGOS = {"auto": 0, "rccl": 1, "a2a": 2, "gather": 3, "allreduce": 4, "direct": 5}
 ERRORS = {0: "OK", 1: "EINVAL", 2: "ENOTMEMBER", 3: "ENOTSUP", 4: "ENOINIT",
           5: "ENOMEM", 6: "EDEVICE"}
 
@@ -115,6 +115,8 @@ def lib() -> ctypes.CDLL:
     L.shmem_barrier_all.restype = None
     L.shmem_malloc.argtypes = [sz]
     L.shmem_malloc.restype = vp
+    L.shmemx_heap_ptr.argtypes = [vp, i]
+    L.shmemx_heap_ptr.restype = vp
     L.shmem_align.argtypes = [sz, sz]
     L.shmem_align.restype = vp
     L.shmem_realloc.argtypes = [vp, sz]
@@ -303,6 +305,29 @@ def collect(bits: int, target, source, nelems: int, PE_start: int, logPE_stride:
             PE_size: int, pSync=None) -> None:
     getattr(lib(), f"shmem_collect{bits}")(addr(target), addr(source), nelems, PE_start,
                                            logPE_stride, PE_size, addr(pSync))
+
+
+def heap_ptr(address: int, pe: int) -> int:
+    """shmemx_heap_ptr: PE `pe`'s copy of a symmetric-heap address, as mapped
+    on this PE (0 if not mapped)."""
+    return lib().shmemx_heap_ptr(address, pe) or 0
+
+
+_hip = None
+
+
+def memcpy(dst, src, nbytes: int) -> None:
+    """hipMemcpy(kind = default) between any host/device addresses (heap
+    pointers are plain device addresses, not tensors)."""
+    global _hip
+    if _hip is None:
+        lib()   # torch's HIP runtime first
+        _hip = ctypes.CDLL("libamdhip64.so.7")
+        _hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        _hip.hipMemcpy.restype = ctypes.c_int
+    rc = _hip.hipMemcpy(addr(dst), addr(src), nbytes, 4)   # hipMemcpyDefault
+    if rc != 0:
+        raise ShmemError(6, f"hipMemcpy failed ({rc})")
 
 
 def malloc(nbytes: int) -> int:

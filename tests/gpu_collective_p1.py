@@ -17,11 +17,11 @@ import shmem_mi355x as shm  # noqa: E402
 assert os.environ.get("SHMEMX_FORCE_COLLECTIVE") == "1"
 torch.cuda.set_device(0)
 shm.init_attr(0, 1, 0, None)
-for t, op, algos in [("double", "sum", ("rccl", "allreduce", "a2a", "gather")),
-                     ("int", "max", ("rccl", "allreduce", "a2a", "gather")),
-                     ("long", "xor", ("a2a", "gather")),
-                     ("complexf", "prod", ("a2a", "gather")),
-                     ("longdouble", "min", ("a2a", "gather"))]:
+for t, op, algos in [("double", "sum", ("rccl", "allreduce", "a2a", "gather", "direct")),
+                     ("int", "max", ("rccl", "allreduce", "a2a", "gather", "direct")),
+                     ("long", "xor", ("a2a", "gather", "direct")),
+                     ("complexf", "prod", ("a2a", "gather", "direct")),
+                     ("longdouble", "min", ("a2a", "gather", "direct"))]:
     for n in (1, 7, 4103, 1 << 20):
         src = oracle.fill(t, 1, 3, n)
         for algo in algos:

@@ -1,0 +1,175 @@
+"""One PE of test_gpu_ipc.py: P of these processes share the box's one GPU on
+the IPC transport ($SHMEMX_TRANSPORT=ipc: no RCCL, the node block's host
+barrier, symmetric heap segments mapped into each other over IPC), so the
+multi-PE reduction path runs for real across processes — every member's
+kernel reads the other members' HBM.
+
+    SHMEM_PE=p SHMEM_NPES=P SHMEM_BOOTSTRAP_FILE=f python gpu_ipc_child.py OUT.json SCENARIO
+
+Checks every result against the oracle restatement of reduce-op.c on the
+same seeded inputs (all PEs' sources are reproducible from the seeds), and
+writes {"pe", "fails", "ncases"} to OUT.json.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(REPO, "openshmem-async_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import oracle  # noqa: E402
+import shmem_mi355x as shm  # noqa: E402
+from gpu_util import same_bits, to_dev  # noqa: E402
+
+out_path, scenario = sys.argv[1], sys.argv[2]
+pe, npes = int(os.environ["SHMEM_PE"]), int(os.environ["SHMEM_NPES"])
+torch.cuda.set_device(0)
+shm.init()
+assert shm.my_pe() == pe and shm.n_pes() == npes
+fails = []
+ncases = 0
+
+
+def member(start, log, size):
+    step = 1 << log
+    return pe >= start and (pe - start) % step == 0 and (pe - start) // step < size
+
+
+def active_sets():
+    s = [(0, 0, npes), (npes - 1, 0, 1)]
+    if npes >= 3:
+        s += [(1, 0, npes - 1), (0, 1, (npes + 1) // 2)]
+    if npes >= 4:
+        s += [(1, 1, npes // 2)]
+    return s
+
+
+def expected(t, op, srcs, st, algo):
+    start, log, size = st
+    ref = oracle.reduce_sim(t, op, srcs, start, log, size)
+    # DIRECT: PE_start's fold order on every member; GATHER: each PE's own
+    return ref[start] if algo in ("auto", "direct") else ref[pe]
+
+
+def read(ptr, t, n):
+    a = np.empty(n, oracle.NP_DTYPE[t])
+    if n:
+        shm.memcpy(a, ptr, a.nbytes)
+    return a
+
+
+def run_case(t, op, n, st, algo, mode, seed):
+    """One collective call; every PE runs the same sequence, non-members skip."""
+    global ncases
+    srcs = oracle.sources(t, 1, npes, n, base_seed=seed)
+    if not member(*st):
+        return
+    ncases += 1
+    mine = np.ascontiguousarray(srcs[pe])
+    want = expected(t, op, srcs, st, algo)
+    sz = mine.itemsize
+    tag = f"{t} {op} n={n} set={st} algo={algo} mode={mode}"
+    if mode == "host":
+        tgt = np.zeros_like(mine)
+        src = mine.copy()
+        shm.set_algo(algo)
+        shm.to_all(t, op, tgt, src, n, *st)
+        shm.set_algo("auto")
+        got = tgt
+    elif mode == "device":
+        s, d = to_dev(torch, mine), to_dev(torch, np.zeros_like(mine))
+        torch.cuda.synchronize()
+        shm.reduce_on_stream(t, op, d, s, n, *st, algo)
+        torch.cuda.synchronize()
+        got = d.cpu().numpy().view(mine.dtype) if t == "longdouble" else d.cpu().numpy()
+    else:
+        # symmetric heap: SRC/TGT are heap blocks, identical offsets on all PEs
+        src_p = HEAP_SRC
+        if mode == "heap":
+            tgt_p = HEAP_TGT
+        elif mode == "inplace":
+            tgt_p = src_p
+        else:  # "overlap": target = source + 3 elements (partial overlap)
+            tgt_p = src_p + 3 * sz
+        if n:
+            shm.memcpy(src_p, mine, mine.nbytes)
+        if mode == "heap" and n:
+            shm.memcpy(tgt_p, np.full(mine.nbytes, 0xAB, np.uint8), mine.nbytes)
+        shm.reduce_on_stream(t, op, tgt_p, src_p, n, *st, algo)
+        torch.cuda.synchronize()
+        got = read(tgt_p, t, n)
+    if not same_bits(got, want):
+        w = 10 if t == "longdouble" else sz
+        a = got.view(np.uint8).reshape(n, -1)[:, :w]
+        b = want.view(np.uint8).reshape(n, -1)[:, :w]
+        bad = np.flatnonzero((a != b).any(axis=1))
+        fails.append(f"{tag}: {len(bad)} elements differ, first at {bad[:4].tolist()}")
+    if shm.last_error():
+        fails.append(f"{tag}: last_error {shm.last_error()}")
+
+
+CAP = 1 << 23   # bytes per heap operand
+HEAP_SRC = shm.malloc(CAP + 64)
+HEAP_TGT = shm.malloc(CAP)
+assert HEAP_SRC and HEAP_TGT, "shmem_malloc failed"
+for q in range(npes):
+    if not shm.heap_ptr(HEAP_SRC, q):
+        fails.append(f"heap_ptr(SRC, {q}) is NULL")
+
+seed = 0x1000
+if scenario == "full":
+    # every reference pair, every active set, both IPC algorithms, heap operands
+    for (t, op) in shm.REFERENCE_PAIRS:
+        for st in active_sets():
+            for algo in ("direct", "gather"):
+                seed += 1
+                run_case(t, op, 1013, st, algo, "heap", seed)
+    # operand placement: heap, in place, partial overlap, torch device, host
+    for t, op in (("double", "sum"), ("long", "xor"), ("longdouble", "max"), ("complexf", "prod"),
+                  ("short", "min")):
+        for mode in ("inplace", "overlap", "device", "host"):
+            for algo in ("direct", "gather"):
+                seed += 1
+                run_case(t, op, 4103, (0, 0, npes), algo, mode, seed)
+    for n in (0, 1, 2, 63, 65, 1 << 20):
+        seed += 1
+        run_case("double", "sum", n, (0, 0, npes), "auto", "heap", seed)
+    # put through heap_ptr, then a barrier: PE q's slot p holds p + 1
+    slots = np.zeros(npes, np.int64)
+    shm.memcpy(HEAP_TGT, slots, slots.nbytes)
+    shm.barrier_all()
+    for q in range(npes):
+        shm.memcpy(shm.heap_ptr(HEAP_TGT, q) + 8 * pe, np.array([pe + 1], np.int64), 8)
+    shm.barrier_all()
+    got = read(HEAP_TGT, "long", npes)
+    if list(got) != list(range(1, npes + 1)):
+        fails.append(f"heap_ptr puts + barrier_all: {list(got)}")
+    # subset barriers interleaved with world ones (pairwise counters)
+    for st in active_sets():
+        if member(*st):
+            shm.barrier(*st)
+        shm.barrier_all()
+elif scenario == "chunk":
+    # $SHMEMX_DIRECT_SCRATCH_MB=1: staged operands go through the scratch in
+    # 512 KiB chunks, so these take several chunks per call
+    for t, op in (("double", "sum"), ("long", "xor"), ("longdouble", "max"), ("int", "prod")):
+        for mode in ("device", "inplace", "overlap"):
+            for algo in ("direct", "gather"):
+                seed += 1
+                run_case(t, op, 200003 if t != "longdouble" else 70001, (0, 0, npes), algo, mode, seed)
+        for st in active_sets():
+            seed += 1
+            run_case(t, op, 150001, st, "direct", "device", seed)
+else:
+    raise SystemExit(f"unknown scenario {scenario}")
+
+shm.free(HEAP_TGT)
+shm.free(HEAP_SRC)
+shm.finalize()
+with open(out_path, "w") as f:
+    json.dump({"pe": pe, "fails": fails, "ncases": ncases}, f)

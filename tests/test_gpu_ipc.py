@@ -1,0 +1,70 @@
+"""Multi-process reductions on one GPU over the IPC transport (DIRECT and
+own-order GATHER), checked against the oracle restatement of reduce-op.c.
+
+P processes (one PE each) share the box's GPU; with $SHMEMX_TRANSPORT=ipc the
+library starts no RCCL communicator (RCCL refuses two ranks on one device),
+so everything that crosses PEs — the symmetric heap's IPC mappings, the
+DIRECT kernels that read and write the other PEs' HBM, the host barrier over
+the node block, staging through the IPC scratch — runs for real across
+processes.  See tests/gpu_ipc_child.py for the cases.
+"""
+import json
+import os
+import signal
+import subprocess
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def run_pes(tmp_path, npes, scenario, extra_env=None, timeout=900):
+    boot = str(tmp_path / "uid")
+    procs = []
+    for pe in range(npes):
+        env = dict(os.environ, SHMEM_PE=str(pe), SHMEM_NPES=str(npes), LOCAL_RANK="0",
+                   SHMEM_BOOTSTRAP_FILE=boot, SHMEMX_TRANSPORT="ipc",
+                   SHMEMX_BARRIER_TIMEOUT="300")
+        env.pop("RANK", None)
+        env.pop("WORLD_SIZE", None)
+        env.update(extra_env or {})
+        out = str(tmp_path / f"pe{pe}.json")
+        log = open(tmp_path / f"pe{pe}.log", "w")
+        procs.append((subprocess.Popen([sys.executable, os.path.join(HERE, "gpu_ipc_child.py"), out,
+                                        scenario], env=env, stdout=log, stderr=subprocess.STDOUT,
+                                       start_new_session=True), out, log))
+    reports = []
+    try:
+        for p, out, log in procs:
+            rc = p.wait(timeout=timeout)
+            log.close()
+            text = open(log.name).read()
+            assert rc == 0, f"PE exited {rc}:\n{text[-3000:]}"
+            with open(out) as f:
+                reports.append(json.load(f))
+    finally:
+        for p, _, _ in procs:
+            if p.poll() is None:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+    return reports
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("npes", [2, 4])
+def test_ipc_transport_all_pairs_sets_placements(tmp_path, npes):
+    reports = run_pes(tmp_path, npes, "full")
+    assert sorted(r["pe"] for r in reports) == list(range(npes))
+    for r in reports:
+        assert r["ncases"] > 0
+        assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
+
+
+@pytest.mark.gpu
+def test_ipc_direct_staged_in_chunks(tmp_path):
+    # a 1 MiB scratch: every staged operand crosses several chunks per call
+    reports = run_pes(tmp_path, 3, "chunk", {"SHMEMX_DIRECT_SCRATCH_MB": "1"})
+    for r in reports:
+        assert r["ncases"] > 0
+        assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
