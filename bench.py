@@ -298,7 +298,8 @@ def main():
         alg_bytes = 3 * nbytes                 # read acc, read in, write acc
         algo_used = "fold"
     else:
-        workload = f"shmem_double_sum_to_all on {world} PEs (one per GPU), RCCL over xGMI"
+        over = "IPC transport, all ranks on one GPU (rehearsal)" if share else "RCCL over xGMI"
+        workload = f"shmem_double_sum_to_all on {world} PEs (one per GPU), {over}"
         algo_used = a.algo
 
         def step():

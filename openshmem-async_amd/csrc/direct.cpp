@@ -45,6 +45,16 @@ namespace shmx {
 namespace {
 
 constexpr size_t kDefaultScratchBytes = size_t(512) << 20;
+constexpr size_t kDefaultOneShotBytes = size_t(256) << 10;
+
+// Arrays up to this size take the one-shot path ($SHMEMX_DIRECT_ONESHOT_KB).
+size_t oneshot_bytes() {
+    static const size_t b = [] {
+        const char *e = std::getenv("SHMEMX_DIRECT_ONESHOT_KB");
+        return e ? size_t(std::atol(e)) << 10 : kDefaultOneShotBytes;
+    }();
+    return b;
+}
 
 struct Scratch {
     char *base = nullptr;
@@ -93,12 +103,19 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     const size_t half = g_scratch.bytes / 2;
     const size_t cmax = std::max(g, (half / sz) / g * g);   // elements per staged chunk
     auto pe_of = [&](int i) { return start + i * step; };
+    // Small arrays: one shot — every member folds the whole array itself (in
+    // set order, so all agree) and writes only its own target: one kernel
+    // and two barriers instead of two kernels and three.  Same decision on
+    // every member (n is collective).
+    const bool one_shot = !own_order && bytes <= oneshot_bytes();
+    const bool local_write = own_order || one_shot;
 
     // Where my operands live for the peers.  A source that partially
     // overlaps the target (the reference's temporary, reduce-op.c:187-203)
-    // or that is outside the heap is staged; in own order every PE writes
-    // only its own target, so it needs staging only when the target aliases
-    // the source (peers still read the source).
+    // or that is outside the heap is staged.  When each PE writes only its
+    // own target, the target needs staging only if it aliases the source
+    // (the peers still read the source); otherwise the peers read my result
+    // slice from it, so it must be in the heap or staged.
     node::Desc d;
     uint64_t off = 0;
     const bool partial = tgt != src && tgt < src + bytes && src < tgt + bytes;
@@ -106,7 +123,7 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     if (stage_src) d.src = node::Loc{node::kScratch, 0};
     else d.src = node::Loc{node::kHeap, off};
     bool stage_tgt;
-    if (own_order) {
+    if (local_write) {
         stage_tgt = tgt < src + bytes && src < tgt + bytes;   // any aliasing
         d.tgt = node::Loc{};
     } else {
@@ -119,7 +136,11 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     // a chunk's copy-out overwrites source elements of the next chunk
     d.count = (stage_src || stage_tgt ? 1 : 0) | (partial && tgt > src ? 2 : 0);
     node::put_desc(d);
-    SHMX_HIP(hipStreamSynchronize(s));   // my source is complete
+    // One chunk (n <= cmax, known alike everywhere): stage it right away.
+    const bool single = n <= cmax;
+    if (single && stage_src)
+        SHMX_HIP(hipMemcpyAsync(g_scratch.base, src, bytes, hipMemcpyDeviceToDevice, s));
+    SHMX_HIP(hipStreamSynchronize(s));   // my source (and its staging) is complete
     node::barrier(start, step, P);       // reduce-op.c:217
 
     // Every member reads the same descriptors, so all cut the same chunks
@@ -134,11 +155,11 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     std::vector<char *> sbase(P), tbase(P);
     for (int i = 0; i < P; ++i) {
         char *b = node::peer_base(static_cast<node::Region>(desc[i].src.region), pe_of(i));
-        if (!b) fatal("DIRECT reduction", "a member's source region is not mapped");
+        if (!b) fatal("DIRECT reduction: a member's source region is not mapped", node::last_ipc_error());
         sbase[i] = b + desc[i].src.off;
-        if (!own_order) {
+        if (!local_write) {
             char *t = node::peer_base(static_cast<node::Region>(desc[i].tgt.region), pe_of(i));
-            if (!t) fatal("DIRECT reduction", "a member's target region is not mapped");
+            if (!t) fatal("DIRECT reduction: a member's target region is not mapped", node::last_ipc_error());
             tbase[i] = t + desc[i].tgt.off;
         }
     }
@@ -150,7 +171,7 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     for (size_t j = 0; j < nchunks; ++j) {
         const size_t k = backwards ? nchunks - 1 - j : j;
         const size_t c0 = k * C, cnt = std::min(C, n - c0);
-        if (chunked) {
+        if (chunked && !single) {
             // the staged chunk in; the previous chunk's exit barrier has
             // already seen every member done reading my scratch
             if (stage_src)
@@ -162,20 +183,22 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
         auto at = [&](char *base, const node::Loc &l, size_t elem) {
             return base + (l.region == node::kScratch ? elem - c0 : elem) * sz;
         };
-        if (own_order) {
-            ins[0] = at(sbase[m], desc[m].src, c0);
-            int k2 = 1;
+        if (local_write) {
+            // own order: src_me first, then the others ascending
+            // (reduce-op.c:219-248); one shot: set order
+            int k2 = 0;
+            if (own_order) ins[k2++] = at(sbase[m], desc[m].src, c0);
             for (int i = 0; i < P; ++i)
-                if (i != m) ins[k2++] = at(sbase[i], desc[i].src, c0);
+                if (!own_order || i != m) ins[k2++] = at(sbase[i], desc[i].src, c0);
             char *out = stage_tgt ? scratch_tgt : tgt + c0 * sz;
             fold_chain(type, op, out, ins.data(), P, cnt, s);
             SHMX_HIP(hipStreamSynchronize(s));
-            node::barrier(start, step, P);   // reduce-op.c:250: every target chunk final
+            node::barrier(start, step, P);   // reduce-op.c:250: no member reads my source any more
             if (stage_tgt)
                 SHMX_HIP(hipMemcpyAsync(tgt + c0 * sz, scratch_tgt, cnt * sz, hipMemcpyDeviceToDevice, s));
             continue;
         }
-        // set order: slice i of the chunk belongs to member i
+        // two shots: slice i of the chunk belongs to member i
         size_t slice = (cnt + P - 1) / P;
         slice = (slice + g - 1) / g * g;
         auto lo_of = [&](int i) { return std::min(cnt, (size_t)i * slice); };
@@ -204,7 +227,7 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
         SHMX_HIP(hipStreamSynchronize(s));
         node::barrier(start, step, P);   // reduce-op.c:250: no member reads my slice any more
     }
-    if (own_order && stage_tgt) SHMX_HIP(hipStreamSynchronize(s));
+    if (local_write && stage_tgt) SHMX_HIP(hipStreamSynchronize(s));
     return SHMEMX_OK;
 }
 

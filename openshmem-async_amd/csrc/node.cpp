@@ -62,6 +62,8 @@ double barrier_timeout_s() {
     return t;
 }
 
+char g_ipc_error[160] = "no IPC error";
+
 void close_peer(Region r, int q) {
     Mapping &mp = g_node.peer[r][q];
     if (mp.base) (void)hipIpcCloseMemHandle(mp.base);
@@ -157,7 +159,11 @@ char *peer_base(Region r, int q) {
     if (q == g_node.pe) return g_node.own[r];
     RegionSlot &s = g_node.sh->pe[q].region[r];
     const uint64_t gen = s.gen.load(std::memory_order_acquire);
-    if (gen == 0) return nullptr;
+    if (gen == 0) {
+        snprintf(g_ipc_error, sizeof g_ipc_error, "PE %d has not published its %s", q,
+                 r == kHeap ? "heap" : "scratch");
+        return nullptr;
+    }
     Mapping &mp = g_node.peer[r][q];
     if (mp.base && mp.gen == gen) return mp.base;
     close_peer(r, q);
@@ -165,8 +171,9 @@ char *peer_base(Region r, int q) {
     hipError_t e = hipIpcOpenMemHandle(&p, s.handle, hipIpcMemLazyEnablePeerAccess);
     if (e != hipSuccess) {
         (void)hipGetLastError();
-        trace(LOG_MEMORY, "hipIpcOpenMemHandle(PE %d, region %d) failed: %s", q, (int)r,
-              hipGetErrorString(e));
+        snprintf(g_ipc_error, sizeof g_ipc_error, "hipIpcOpenMemHandle(PE %d, %s, gen %llu): %s", q,
+                 r == kHeap ? "heap" : "scratch", (unsigned long long)gen, hipGetErrorString(e));
+        trace(LOG_MEMORY, "%s", g_ipc_error);
         return nullptr;
     }
     mp.base = static_cast<char *>(p);
@@ -176,6 +183,8 @@ char *peer_base(Region r, int q) {
           (unsigned long long)s.bytes, p);
     return mp.base;
 }
+
+const char *last_ipc_error() { return g_ipc_error; }
 
 size_t peer_bytes(Region r, int q) {
     if (!g_node.sh || q < 0 || q >= g_node.npes) return 0;

@@ -59,6 +59,7 @@ void unpublish(Region r);
 // the peer's generation changed.
 char *peer_base(Region r, int pe);
 size_t peer_bytes(Region r, int pe);
+const char *last_ipc_error();   // why the last peer_base() returned nullptr
 
 void put_desc(const Desc &d);
 Desc get_desc(int pe);

@@ -182,6 +182,10 @@ static int init_locked(int pe, int npes, int device, const void *uid) {
             if (g_state.ipc_only) fatal("shmem_init", "cannot attach the intra-node block (/dev/shm)");
             trace(LOG_INIT, "no intra-node block: the DIRECT algorithm is unavailable");
         }
+        // ncclCommInitRank makes the RCCL init collective; the IPC transport
+        // gets the same from a first barrier (so a bootstrap file is only
+        // removed once every PE has read it)
+        if (g_state.ipc_only) node::barrier(0, 1, npes);
     }
     g_state.pe = pe;
     g_state.npes = npes;

@@ -74,6 +74,7 @@ def run_case(t, op, n, st, algo, mode, seed):
     want = expected(t, op, srcs, st, algo)
     sz = mine.itemsize
     tag = f"{t} {op} n={n} set={st} algo={algo} mode={mode}"
+    print(tag, flush=True)   # progress, in the PE's log
     if mode == "host":
         tgt = np.zeros_like(mine)
         src = mine.copy()

@@ -25,7 +25,7 @@ def run_pes(tmp_path, npes, scenario, extra_env=None, timeout=900):
     for pe in range(npes):
         env = dict(os.environ, SHMEM_PE=str(pe), SHMEM_NPES=str(npes), LOCAL_RANK="0",
                    SHMEM_BOOTSTRAP_FILE=boot, SHMEMX_TRANSPORT="ipc",
-                   SHMEMX_BARRIER_TIMEOUT="300")
+                   SHMEMX_BARRIER_TIMEOUT="120")
         env.pop("RANK", None)
         env.pop("WORLD_SIZE", None)
         env.update(extra_env or {})
@@ -36,11 +36,15 @@ def run_pes(tmp_path, npes, scenario, extra_env=None, timeout=900):
                                        start_new_session=True), out, log))
     reports = []
     try:
+        rcs = [p.wait(timeout=timeout) for p, _, _ in procs]
+        if any(rcs):
+            tails = []
+            for (p, _, log), rc in zip(procs, rcs):
+                log.close()
+                tails.append(f"--- PE {procs.index((p, _, log))} exit {rc}:\n" + open(log.name).read()[-1500:])
+            raise AssertionError("\n".join(tails))
         for p, out, log in procs:
-            rc = p.wait(timeout=timeout)
             log.close()
-            text = open(log.name).read()
-            assert rc == 0, f"PE exited {rc}:\n{text[-3000:]}"
             with open(out) as f:
                 reports.append(json.load(f))
     finally:
@@ -53,8 +57,12 @@ def run_pes(tmp_path, npes, scenario, extra_env=None, timeout=900):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("npes", [2, 4])
-def test_ipc_transport_all_pairs_sets_placements(tmp_path, npes):
-    reports = run_pes(tmp_path, npes, "full")
+@pytest.mark.parametrize("shots", ["auto", "two"])
+def test_ipc_transport_all_pairs_sets_placements(tmp_path, npes, shots):
+    # "auto": arrays up to 256 KiB take DIRECT's one-shot path; "two": every
+    # size takes reduce-scatter + all-gather
+    env = {"SHMEMX_DIRECT_ONESHOT_KB": "0"} if shots == "two" else {}
+    reports = run_pes(tmp_path, npes, "full", env)
     assert sorted(r["pe"] for r in reports) == list(range(npes))
     for r in reports:
         assert r["ncases"] > 0
