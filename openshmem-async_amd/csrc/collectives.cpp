@@ -67,10 +67,6 @@ int set_info(int start, int logstride, int size, SetInfo &si) {
 
 bool collective(const SetInfo &si) { return si.P > 1 || g_state.force_collective; }
 
-// Collectives other than the barrier and the reductions need RCCL for now.
-int need_rccl(const SetInfo &si) {
-    return collective(si) && !g_state.comm ? set_error(SHMEMX_ENOTSUP) : SHMEMX_OK;
-}
 
 // A device view of a possibly host-resident buffer.
 struct DevBuf {
@@ -155,13 +151,15 @@ int broadcast_impl(size_t esize, void *target, const void *source, size_t nelems
     SetInfo si;
     if (int rc = set_info(start, logstride, size, si)) return rc;
     if (root_idx < 0 || root_idx >= size) return set_error(SHMEMX_EINVAL);
-    if (int rc = need_rccl(si)) return rc;
     const size_t bytes = nelems * esize;
     trace(LOG_BROADCAST, "%zu bytes from set member %d, set (%d,%d,%d) member %d", bytes, root_idx,
           start, logstride, size, si.m);
     if (!bytes || !collective(si)) return SHMEMX_OK;  // the root's target is never written
     if ((si.m == root_idx && !source) || (si.m != root_idx && !target)) return set_error(SHMEMX_EINVAL);
     hipStream_t s = g_state.stream;
+    if (!g_state.comm)   // IPC transport
+        return ipc_broadcast(static_cast<char *>(target), static_cast<const char *>(source), bytes,
+                             root_idx, si.start, si.step, si.P, si.m, s);
     const int root = si.peer(root_idx);
     const bool is_root = si.m == root_idx;
     DevBuf in, out;
@@ -198,8 +196,16 @@ int collect_impl(size_t esize, void *target, const void *source, size_t nelems, 
     clear_error();
     SetInfo si;
     if (int rc = set_info(start, logstride, size, si)) return rc;
-    if (int rc = need_rccl(si)) return rc;
     hipStream_t s = g_state.stream;
+    if (collective(si) && !g_state.comm) {   // IPC transport
+        if (nelems && !source) return set_error(SHMEMX_EINVAL);
+        size_t total = 0;
+        const int rc = ipc_collect(static_cast<char *>(target), static_cast<const char *>(source), esize,
+                                   nelems, si.start, si.step, si.P, si.m, &total, s);
+        trace(LOG_COLLECT, "%s over IPC: %zu bytes mine, %zu in all, set (%d,%d,%d)",
+              fixed ? "fcollect" : "collect", nelems * esize, total, start, logstride, size);
+        return rc;
+    }
     std::vector<long long> counts(si.P, (long long)nelems);
     if (!fixed && collective(si)) {
         // every member's count (the reference passes it down a chain of

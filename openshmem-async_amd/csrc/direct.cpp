@@ -82,6 +82,12 @@ bool ensure_scratch() {
 
 }  // namespace
 
+char *ipc_scratch(size_t *bytes) {
+    if (!ensure_scratch()) return nullptr;
+    *bytes = g_scratch.bytes;
+    return g_scratch.base;
+}
+
 void direct_release() {
     if (!g_scratch.base) return;
     node::unpublish(node::kScratch);

@@ -92,5 +92,14 @@ void fold_chain(int type, int op, void *out, const void **ins, int nins, size_t 
 int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int start,
                   int logstride, const shmemx_plan_t &p, bool own_order, hipStream_t s);
 void direct_release();
+// This PE's IPC scratch region (allocated and published on first use).
+char *ipc_scratch(size_t *bytes);
+// Broadcast and [f]collect on the IPC transport (ipc_coll.cpp): members pull
+// from the root's / each other's heap or scratch over IPC mappings.  target
+// and source are device pointers (the caller stages host buffers).
+int ipc_broadcast(char *target, const char *source, size_t bytes, int root_idx, int start,
+                  int step, int P, int m, hipStream_t s);
+int ipc_collect(char *target, const char *source, size_t esize, size_t nelems, int start,
+                int step, int P, int m, size_t *total_out, hipStream_t s);
 
 }  // namespace shmx

@@ -114,6 +114,73 @@ def run_case(t, op, n, st, algo, mode, seed):
         fails.append(f"{tag}: last_error {shm.last_error()}")
 
 
+def place(arr, mode, heap_ptr):
+    """arr in `mode` memory: (handle passed to the library, reader)."""
+    if mode == "host":
+        a = arr.copy()
+        return a, lambda: a
+    if mode == "device":
+        t = torch.from_numpy(arr.copy()).cuda()
+        torch.cuda.synchronize()
+        return t, lambda: t.cpu().numpy()
+    if arr.nbytes:
+        shm.memcpy(heap_ptr, arr, arr.nbytes)
+    return heap_ptr, lambda: read_raw(heap_ptr, arr.dtype, arr.size)
+
+
+def read_raw(ptr, dtype, n):
+    a = np.empty(n, dtype)
+    if n:
+        shm.memcpy(a, ptr, a.nbytes)
+    return a
+
+
+def run_bcast(bits, n, root, st, mode, seed):
+    """shmem_broadcast{32,64}; every non-root member gets the root's source,
+    the root's target is untouched (broadcast-linear.c:54-74)."""
+    global ncases
+    dt = np.int32 if bits == 32 else np.int64
+    rng = np.random.default_rng(seed)
+    srcs = rng.integers(-2**31, 2**31 - 1, size=(npes, n)).astype(dt)
+    tgts = np.full((npes, n), -7, dt)
+    if not member(*st):
+        return
+    ncases += 1
+    want = oracle.broadcast_sim(srcs, tgts, root, *st)[pe]
+    src, _ = place(srcs[pe], mode, HEAP_SRC)
+    tgt, get = place(tgts[pe], mode, HEAP_TGT)
+    print(f"broadcast{bits} n={n} root={root} set={st} mode={mode}", flush=True)
+    shm.broadcast(bits, tgt, src, n, root, *st)
+    torch.cuda.synchronize()
+    if not np.array_equal(get(), want) or shm.last_error():
+        fails.append(f"broadcast{bits} n={n} root={root} set={st} mode={mode} err={shm.last_error()}")
+
+
+def run_collect(bits, counts, st, mode, seed):
+    """shmem_fcollect (equal counts) / shmem_collect: member i's source lands
+    at the running offset (fcollect-linear.c:69-91, collect-linear.c:57-130)."""
+    global ncases
+    dt = np.int32 if bits == 32 else np.int64
+    fixed = len(set(counts)) == 1
+    rng = np.random.default_rng(seed)
+    maxn = max(counts)
+    srcs = rng.integers(-2**31, 2**31 - 1, size=(npes, maxn)).astype(dt)
+    cap = sum(counts) + 5
+    tgts = np.full((npes, cap), -7, dt)
+    if not member(*st):
+        return
+    ncases += 1
+    want = oracle.collect_sim(srcs, counts, tgts, *st)[pe]
+    src, _ = place(np.ascontiguousarray(srcs[pe, :counts[pe]]), mode, HEAP_SRC)
+    tgt, get = place(tgts[pe], mode, HEAP_TGT)
+    kind = "fcollect" if fixed else "collect"
+    print(f"{kind}{bits} counts={counts} set={st} mode={mode}", flush=True)
+    getattr(shm, kind)(bits, tgt, src, counts[pe], *st)
+    torch.cuda.synchronize()
+    if not np.array_equal(get(), want) or shm.last_error():
+        fails.append(f"{kind}{bits} counts={counts} set={st} mode={mode} err={shm.last_error()}")
+
+
 CAP = 1 << 23   # bytes per heap operand
 HEAP_SRC = shm.malloc(CAP + 64)
 HEAP_TGT = shm.malloc(CAP)
@@ -150,6 +217,19 @@ if scenario == "full":
     got = read(HEAP_TGT, "long", npes)
     if list(got) != list(range(1, npes + 1)):
         fails.append(f"heap_ptr puts + barrier_all: {list(got)}")
+    # the neighbouring collectives over IPC, against their oracles
+    for st in active_sets():
+        size = st[2]
+        for mode in ("heap", "device", "host"):
+            for bits in (32, 64):
+                seed += 1
+                run_bcast(bits, 1031, seed % size, st, mode, seed)
+                seed += 1
+                run_collect(bits, [517] * npes, st, mode, seed)
+                seed += 1
+                run_collect(bits, [(37 * (q + 1)) % 101 for q in range(npes)], st, mode, seed)
+    seed += 1
+    run_collect(64, [0] * npes, (0, 0, npes), "device", seed)
     # subset barriers interleaved with world ones (pairwise counters)
     for st in active_sets():
         if member(*st):
@@ -166,6 +246,14 @@ elif scenario == "chunk":
         for st in active_sets():
             seed += 1
             run_case(t, op, 150001, st, "direct", "device", seed)
+    # broadcast / collect through several scratch rounds (1 MiB scratch)
+    for mode in ("device", "host", "heap"):
+        seed += 1
+        run_bcast(64, 300001, 1, (0, 0, npes), mode, seed)
+        seed += 1
+        run_collect(64, [100003, 30001, 0][:npes] + [7] * max(0, npes - 3), (0, 0, npes), mode, seed)
+        seed += 1
+        run_collect(32, [150001] * npes, (0, 0, npes), mode, seed)
 else:
     raise SystemExit(f"unknown scenario {scenario}")
 
