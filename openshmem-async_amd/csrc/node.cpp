@@ -102,12 +102,17 @@ bool attach(int pe, int npes, const void *key, size_t keylen) {
     return true;
 }
 
-void detach(bool unlink_name) {
+void unlink_name() {
+    if (g_node.sh && !g_node.name.empty()) shm_unlink(g_node.name.c_str());
+    g_node.name.clear();
+}
+
+void detach(bool unlink) {
     if (!g_node.sh) return;
     for (int r = 0; r < kNumRegions; ++r)
         for (int q = 0; q < kMaxPes; ++q) close_peer(static_cast<Region>(r), q);
+    if (unlink) unlink_name();
     munmap(g_node.sh, sizeof(Shared));
-    if (unlink_name) shm_unlink(g_node.name.c_str());
     g_node = Node{};
 }
 

@@ -44,7 +44,8 @@ struct Desc {
 // passes the same bytes).  Returns false (and leaves the layer down) on any
 // OS error.
 bool attach(int pe, int npes, const void *key, size_t keylen);
-void detach(bool unlink_name);
+void detach(bool unlink);
+void unlink_name();   // the block stays mapped; the /dev/shm name goes
 bool up();
 
 // Host barrier among the members start + i*step, i < P (the caller is one of

@@ -178,14 +178,31 @@ static int init_locked(int pe, int npes, int device, const void *uid) {
         if (!g_state.ipc_only) SHMX_NCCL(ncclCommInitRank(&g_state.comm, npes, id, pe));
         // the intra-node block (symmetric-heap IPC handles, host barrier):
         // required on the IPC transport, an extra (DIRECT) otherwise
-        if (!node::attach(pe, npes, &id, sizeof id)) {
-            if (g_state.ipc_only) fatal("shmem_init", "cannot attach the intra-node block (/dev/shm)");
-            trace(LOG_INIT, "no intra-node block: the DIRECT algorithm is unavailable");
+        bool attached = node::attach(pe, npes, &id, sizeof id);
+        if (!attached && g_state.ipc_only) fatal("shmem_init", "cannot attach the intra-node block (/dev/shm)");
+        if (g_state.comm && npes > 1) {
+            // every PE must have the block, or none uses it
+            int *flag = nullptr;
+            SHMX_HIP(hipMalloc(&flag, sizeof(int)));
+            const int mine = attached ? 1 : 0;
+            SHMX_HIP(hipMemcpyAsync(flag, &mine, sizeof mine, hipMemcpyHostToDevice, g_state.stream));
+            SHMX_NCCL(ncclAllReduce(flag, flag, 1, ncclInt32, ncclMin, g_state.comm, g_state.stream));
+            int all = 0;
+            SHMX_HIP(hipMemcpyAsync(&all, flag, sizeof all, hipMemcpyDeviceToHost, g_state.stream));
+            SHMX_HIP(hipStreamSynchronize(g_state.stream));
+            SHMX_HIP(hipFree(flag));
+            if (attached && !all) node::detach(false);
+            attached = all != 0;
         }
-        // ncclCommInitRank makes the RCCL init collective; the IPC transport
-        // gets the same from a first barrier (so a bootstrap file is only
-        // removed once every PE has read it)
-        if (g_state.ipc_only) node::barrier(0, 1, npes);
+        if (!attached) trace(LOG_INIT, "no intra-node block: the DIRECT algorithm is unavailable");
+        // Every PE is attached after a first barrier (it also makes the IPC
+        // transport's init collective, like ncclCommInitRank, so a bootstrap
+        // file is removed only once every PE has read it); the name can go
+        // then, so a job that dies leaves nothing in /dev/shm.
+        if (attached) {
+            node::barrier(0, 1, npes);
+            if (pe == 0) node::unlink_name();
+        }
     }
     g_state.pe = pe;
     g_state.npes = npes;

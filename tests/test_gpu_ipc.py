@@ -76,3 +76,34 @@ def test_ipc_direct_staged_in_chunks(tmp_path):
     for r in reports:
         assert r["ncases"] > 0
         assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
+
+
+@pytest.mark.gpu
+def test_isx_c_program_four_pes(tmp_path):
+    """The C99 ISx verification program (examples/isx_verify.c: the
+    reference's known-answer check, isx.c:615-624, on static host arrays) as
+    four PE processes, shmem_init bootstrapping through a file."""
+    repo = os.path.dirname(HERE)
+    libdir = os.path.join(repo, "openshmem-async_amd")
+    exe = tmp_path / "isx_verify"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(repo, "include"),
+                    os.path.join(repo, "examples", "isx_verify.c"), "-L", libdir,
+                    "-lshmem_reduce_mi355x", f"-Wl,-rpath,{libdir}", "-o", str(exe)], check=True)
+    npes, procs = 4, []
+    for pe in range(npes):
+        env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE")}
+        env.update(SHMEM_PE=str(pe), SHMEM_NPES=str(npes), LOCAL_RANK="0",
+                   SHMEM_BOOTSTRAP_FILE=str(tmp_path / "uid"), SHMEMX_TRANSPORT="ipc",
+                   SHMEMX_BARRIER_TIMEOUT="120")
+        procs.append(subprocess.Popen([str(exe)], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True, start_new_session=True))
+    try:
+        outs = [p.communicate(timeout=300)[0] for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+    for pe, (p, out) in enumerate(zip(procs, outs)):
+        assert p.returncode == 0, f"PE {pe}: {out[-2000:]}"
+        assert f"PE {pe} of {npes}: ISx verification passed" in out
