@@ -29,6 +29,7 @@ import json
 import os
 import statistics
 import sys
+import threading
 import time
 
 import torch
@@ -52,6 +53,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=20)
     ap.add_argument("--extras", type=int, default=1, help="also time the other algorithms / API forms")
+    ap.add_argument("--extras-timeout", type=float, default=300.0,
+                    help="seconds the extras may take before the line is printed without the rest")
     return ap.parse_args()
 
 
@@ -349,21 +352,6 @@ def main():
                     "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
                     "avg_launch_us": round(t_launch * 1e6, 2),
                     "kernel": "fold_kernel<double,SUM,2 inputs>"}
-        if a.extras:
-            # the drop-in call itself at PE_size = 1 (copy semantics, reduce-op.c:213-216)
-            def api_step():
-                shm.reduce_on_stream("double", "sum", tgt, src, n, 0, 0, 1, "auto", sp)
-            for _ in range(3):
-                api_step()
-            w2, e2 = time_region(api_step, max(5, a.steps // 2), stream, barrier)
-            k2 = max(5, a.steps // 2)
-            extras["api_pe_size_1"] = {
-                "GiBps": round(nbytes * k2 / w2 / GiB, 1),
-                "hbm_GBps": round(2 * nbytes / (e2 / k2) / 1e9, 1),
-                "us_per_call": round(e2 / k2 * 1e6, 2)}
-            extras["host_resident_e2e"] = host_e2e(n)
-            extras["configs"] = config_extras(world, stream, barrier, max_over_ranks)
-            extras["latency"] = latency_extras(world, barrier, max_over_ranks)
     else:
         t_call = ev / a.steps
         xgmi_bytes = 2 * (world - 1) / world * nbytes        # per GPU, RS + AG
@@ -375,11 +363,74 @@ def main():
                     "avg_launch_us": round(t_call * 1e6, 2),
                     "busbw_GBps": round(achieved, 1),
                     "algbw_GiBps": round(nbytes / t_call / GiB, 2)}
+
+    cpu = None
+    if world == 1 and rank == 0 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(n, a.cpu_reps)
+
+    line = {
+        "metric": "GiB/s device-resident shmem_double_sum_to_all, nreduce=32Mi, 1/2/4/8 GPUs",
+        "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": workload, "nreduce": n, "type": "double", "op": "sum",
+                   "PE_size": world, "algo": algo_used,
+                   "parallelism": f"one PE per GPU x{world}",
+                   "transport": os.environ.get("SHMEMX_TRANSPORT", "rccl")},
+        "roofline": roofline, "cpu_baseline": cpu, "correct": ok, "extras": extras,
+    }
+    emitted = threading.Lock()
+
+    def emit(note=None):
+        """Print the one JSON line (rank 0), at most once."""
+        if not emitted.acquire(blocking=False):
+            return
+        if note:
+            line["extras"] = dict(extras, note=note)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+
+    # The headline is measured and checked by now.  The extras below exercise
+    # other algorithms and API forms; a hang among them must not cost the
+    # line: after --extras-timeout seconds every rank prints what it has
+    # (rank 0) and leaves.
+    def watchdog():
+        emit(f"extras stopped after {a.extras_timeout} s (timeout)")
+        os._exit(0 if ok else 1)
+    timer = threading.Timer(a.extras_timeout, watchdog)
+    timer.daemon = True
+    timer.start()
+
+    def guarded(name, fn):
+        try:
+            extras[name] = fn()
+        except Exception as e:   # noqa: BLE001 — an extra never costs the headline
+            extras[name] = f"error: {type(e).__name__}: {e}"
+
+    if world == 1:
         if a.extras:
-            for alt in ("rccl", "allreduce", "a2a", "gather"):
-                if alt == algo_used:
-                    continue
-                def alt_step(alt=alt):
+            # the drop-in call itself at PE_size = 1 (copy semantics, reduce-op.c:213-216)
+            def api_pe_size_1():
+                def api_step():
+                    shm.reduce_on_stream("double", "sum", tgt, src, n, 0, 0, 1, "auto", sp)
+                for _ in range(3):
+                    api_step()
+                k2 = max(5, a.steps // 2)
+                w2, e2 = time_region(api_step, k2, stream, barrier)
+                return {"GiBps": round(nbytes * k2 / w2 / GiB, 1),
+                        "hbm_GBps": round(2 * nbytes / (e2 / k2) / 1e9, 1),
+                        "us_per_call": round(e2 / k2 * 1e6, 2)}
+            guarded("api_pe_size_1", api_pe_size_1)
+            guarded("host_resident_e2e", lambda: host_e2e(n))
+            guarded("configs", lambda: config_extras(world, stream, barrier, max_over_ranks))
+            guarded("latency", lambda: latency_extras(world, barrier, max_over_ranks))
+    elif a.extras:
+        for alt in ("rccl", "allreduce", "a2a", "gather"):
+            if alt == algo_used:
+                continue
+
+            def alt_rate(alt=alt):
+                def alt_step():
                     shm.reduce_on_stream("double", "sum", tgt, src, n, 0, 0, world, alt, sp)
                 try:
                     for _ in range(2):
@@ -387,31 +438,17 @@ def main():
                     k3 = max(3, a.steps // 4)
                     w3, _ = time_region(alt_step, k3, stream, barrier)
                     w3 = max_over_ranks(w3)
-                    extras[f"algo_{alt}_GiBps"] = round(world * nbytes * k3 / w3 / GiB, 2)
+                    return round(world * nbytes * k3 / w3 / GiB, 2)
                 except shm.ShmemError as e:
-                    extras[f"algo_{alt}_GiBps"] = str(e)
-            extras["direct_heap"] = direct_extra(world, n, src, sp, stream, barrier, max_over_ranks,
-                                                 max(3, a.steps // 4))
-            extras["configs"] = config_extras(world, stream, barrier, max_over_ranks)
-            extras["latency"] = latency_extras(world, barrier, max_over_ranks)
+                    return str(e)
+            guarded(f"algo_{alt}_GiBps", alt_rate)
+        guarded("direct_heap", lambda: direct_extra(world, n, src, sp, stream, barrier,
+                                                    max_over_ranks, max(3, a.steps // 4)))
+        guarded("configs", lambda: config_extras(world, stream, barrier, max_over_ranks))
+        guarded("latency", lambda: latency_extras(world, barrier, max_over_ranks))
 
-    cpu = None
-    if world == 1 and rank == 0 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(n, a.cpu_reps)
-
-    if rank == 0:
-        line = {
-            "metric": "GiB/s device-resident shmem_double_sum_to_all, nreduce=32Mi, 1/2/4/8 GPUs",
-            "value": round(value, 2), "unit": "GiB/s", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": workload, "nreduce": n, "type": "double", "op": "sum",
-                       "PE_size": world, "algo": algo_used,
-                       "parallelism": f"one PE per GPU x{world}",
-                       "transport": os.environ.get("SHMEMX_TRANSPORT", "rccl")},
-            "roofline": roofline, "cpu_baseline": cpu, "correct": ok, "extras": extras,
-        }
-        print(json.dumps(line), flush=True)
+    timer.cancel()
+    emit()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

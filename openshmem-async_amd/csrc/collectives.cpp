@@ -118,10 +118,14 @@ int barrier_impl(int start, int logstride, int size) {
     SetInfo si;
     if (int rc = set_info(start, logstride, size, si)) return rc;
     hipStream_t s = g_state.stream;
-    // quiet: everything this PE enqueued before the barrier is complete
+    // quiet: everything this PE enqueued before the barrier is complete, and
+    // (system-scope fence on every XCD) visible to the peers, whose stores
+    // through shmemx_heap_ptr this GPU will then not see through stale lines
+    const bool coll = collective(si);
+    if (coll && si.P > 1) SHMX_HIP(launch_sys_fence(s));
     SHMX_HIP(hipStreamSynchronize(s));
     trace(LOG_BARRIER, "set (%d,%d,%d) member %d", start, logstride, size, si.m);
-    if (!collective(si)) return SHMEMX_OK;
+    if (!coll) return SHMEMX_OK;
     if (!g_state.comm) {   // IPC transport
         node::barrier(si.start, si.step, si.P);
         return SHMEMX_OK;

@@ -12,10 +12,11 @@
 //   2. all-gather: member m copies every other member's result slice from
 //      that member's target into its own — one kernel for all P-1 slices.
 // (P-1)/P of the array crosses xGMI in each phase, as reads only: a PE never
-// stores into another GPU's HBM, so no remote L2 can hold a stale copy of
-// what it later reads (peer data is read after the owner's kernel has ended
-// and a barrier, the usual P2P read discipline).  Every PE ends with the
-// reference's PE_start result.
+// stores into another GPU's HBM.  Peer data is read only after the owner's
+// kernel has ended, a system-scope fence has run on every XCD of the owner
+// (its L2 written back) and of the reader (stale peer lines dropped), and a
+// barrier has passed (node_sync).  Every PE ends with the reference's
+// PE_start result.
 //
 // Own order (SHMEMX_ALGO_GATHER on the IPC transport): every PE folds the
 // whole array in its own reference order, src_me first, then the other
@@ -24,14 +25,17 @@
 //
 // Synchronisation is the reference's: a barrier before the peers' sources
 // are read (reduce-op.c:217) and one after the targets are final (:250),
-// plus one between the two phases; host barriers over the node block.  Operands outside the symmetric heap (or
-// a source that partially overlaps its target) are staged through a per-PE
-// scratch region, also IPC-mapped, in chunks of half its size
-// ($SHMEMX_DIRECT_SCRATCH_MB, default 512; every PE must use the same value).
+// plus one between the two phases; host barriers over the node block.
+// Operands outside the symmetric heap (or a source that partially overlaps
+// its target) are staged through a per-PE scratch region, also IPC-mapped,
+// in chunks of half its size ($SHMEMX_DIRECT_SCRATCH_MB, default 512; every
+// PE must use the same value).  A peer region that cannot be mapped fails
+// the call with ENOTSUP on every member alike (map_members).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdlib>
+#include <unordered_set>
 #include <vector>
 
 #include "heap.h"
@@ -80,7 +84,48 @@ bool ensure_scratch() {
     return true;
 }
 
+// Open (or reuse) the mappings of every region the members' descriptors name.
+// The first time a set meets a given combination of region generations, the
+// members vote (node::agree), so a mapping that fails on one PE fails the
+// call on all of them alike; the combinations that passed are remembered, and
+// every member decides identically whether to vote (same set, same
+// descriptors, same generations from the shared block).
+std::unordered_set<uint64_t> g_voted;
+
+bool map_members(const std::vector<node::Desc> &desc, bool local_write, int start, int step,
+                 int P) {
+    uint64_t key = 1469598103934665603ull;
+    auto mix = [&key](uint64_t v) { key = (key ^ v) * 1099511628211ull; };
+    mix((uint64_t)start);
+    mix((uint64_t)step);
+    mix((uint64_t)P);
+    bool ok = true;
+    for (int i = 0; i < P; ++i) {
+        const int pe = start + i * step;
+        for (int k = 0; k < (local_write ? 1 : 2); ++k) {
+            const node::Region r = static_cast<node::Region>(k == 0 ? desc[i].src.region
+                                                                   : desc[i].tgt.region);
+            mix((uint64_t)r);
+            mix(node::region_gen(r, pe));
+            ok &= node::peer_base(r, pe) != nullptr;
+        }
+    }
+    if (g_voted.count(key)) {   // every member mapped these before
+        if (!ok) fatal("DIRECT reduction: a peer region mapped before is gone", node::last_ipc_error());
+        return true;
+    }
+    if (!node::agree(start, step, P, ok)) return false;
+    g_voted.insert(key);
+    return true;
+}
+
 }  // namespace
+
+void node_sync(int start, int step, int P, hipStream_t s) {
+    if (P > 1) SHMX_HIP(launch_sys_fence(s));
+    SHMX_HIP(hipStreamSynchronize(s));
+    node::barrier(start, step, P);
+}
 
 char *ipc_scratch(size_t *bytes) {
     if (!ensure_scratch()) return nullptr;
@@ -146,8 +191,7 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     const bool single = n <= cmax;
     if (single && stage_src)
         SHMX_HIP(hipMemcpyAsync(g_scratch.base, src, bytes, hipMemcpyDeviceToDevice, s));
-    SHMX_HIP(hipStreamSynchronize(s));   // my source (and its staging) is complete
-    node::barrier(start, step, P);       // reduce-op.c:217
+    node_sync(start, step, P, s);   // my source (and its staging) is complete; reduce-op.c:217
 
     // Every member reads the same descriptors, so all cut the same chunks
     // and walk them in the same direction.
@@ -158,16 +202,17 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
         chunked |= (desc[i].count & 1) != 0;
         backwards |= (desc[i].count & 2) != 0;
     }
+    if (!map_members(desc, local_write, start, step, P)) {
+        trace(LOG_REDUCTION, "DIRECT: a member could not map a peer region (%s)", node::last_ipc_error());
+        return set_error(SHMEMX_ENOTSUP);
+    }
     std::vector<char *> sbase(P), tbase(P);
     for (int i = 0; i < P; ++i) {
-        char *b = node::peer_base(static_cast<node::Region>(desc[i].src.region), pe_of(i));
-        if (!b) fatal("DIRECT reduction: a member's source region is not mapped", node::last_ipc_error());
-        sbase[i] = b + desc[i].src.off;
-        if (!local_write) {
-            char *t = node::peer_base(static_cast<node::Region>(desc[i].tgt.region), pe_of(i));
-            if (!t) fatal("DIRECT reduction: a member's target region is not mapped", node::last_ipc_error());
-            tbase[i] = t + desc[i].tgt.off;
-        }
+        sbase[i] = node::peer_base(static_cast<node::Region>(desc[i].src.region), pe_of(i)) +
+                   desc[i].src.off;
+        if (!local_write)
+            tbase[i] = node::peer_base(static_cast<node::Region>(desc[i].tgt.region), pe_of(i)) +
+                       desc[i].tgt.off;
     }
     const size_t C = chunked ? cmax : std::max<size_t>(n, 1);
     const size_t nchunks = (n + C - 1) / C;
@@ -182,8 +227,7 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
             // already seen every member done reading my scratch
             if (stage_src)
                 SHMX_HIP(hipMemcpyAsync(scratch_src, src + c0 * sz, cnt * sz, hipMemcpyDeviceToDevice, s));
-            SHMX_HIP(hipStreamSynchronize(s));
-            node::barrier(start, step, P);
+            node_sync(start, step, P, s);
         }
         // a staged operand holds only the current chunk, at its region offset
         auto at = [&](char *base, const node::Loc &l, size_t elem) {
@@ -198,8 +242,7 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
                 if (!own_order || i != m) ins[k2++] = at(sbase[i], desc[i].src, c0);
             char *out = stage_tgt ? scratch_tgt : tgt + c0 * sz;
             fold_chain(type, op, out, ins.data(), P, cnt, s);
-            SHMX_HIP(hipStreamSynchronize(s));
-            node::barrier(start, step, P);   // reduce-op.c:250: no member reads my source any more
+            node_sync(start, step, P, s);   // reduce-op.c:250: no member reads my source any more
             if (stage_tgt)
                 SHMX_HIP(hipMemcpyAsync(tgt + c0 * sz, scratch_tgt, cnt * sz, hipMemcpyDeviceToDevice, s));
             continue;
@@ -216,8 +259,7 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
             char *out = at(tbase[m], desc[m].tgt, c0 + lo);
             SHMX_HIP(launch_fold(type, op, out, ins.data(), P, hi - lo, s));
         }
-        SHMX_HIP(hipStreamSynchronize(s));
-        node::barrier(start, step, P);   // every member's slice is final
+        node_sync(start, step, P, s);   // every member's slice is final
         // 2. every other member's slice (and mine, if it was staged) into my target
         std::vector<const void *> from;
         std::vector<void *> to;
@@ -230,8 +272,7 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
             len.push_back((hi_of(i) - lo_of(i)) * sz);
         }
         SHMX_HIP(launch_gather(from.data(), to.data(), len.data(), (int)from.size(), s));
-        SHMX_HIP(hipStreamSynchronize(s));
-        node::barrier(start, step, P);   // reduce-op.c:250: no member reads my slice any more
+        node_sync(start, step, P, s);   // reduce-op.c:250: no member reads my slice any more
     }
     if (local_write && stage_tgt) SHMX_HIP(hipStreamSynchronize(s));
     return SHMEMX_OK;

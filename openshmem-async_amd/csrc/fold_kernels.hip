@@ -532,7 +532,21 @@ __global__ __launch_bounds__(kBlock) void gather_kernel(GatherArgs a) {
     }
 }
 
+// Workgroups are dispatched round-robin over the 8 XCDs, so 64 one-wave
+// blocks put 8 on every XCD; the fence of any one of them covers that XCD's
+// L2 (the per-XCD L2s are not coherent with each other or with the peers).
+constexpr int kFenceBlocks = 64;
+
+__global__ __launch_bounds__(64) void sys_fence_kernel() {
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");   // system scope
+}
+
 }  // namespace
+
+hipError_t launch_sys_fence(hipStream_t stream) {
+    hipLaunchKernelGGL(sys_fence_kernel, dim3(kFenceBlocks), dim3(64), 0, stream);
+    return hipGetLastError();
+}
 
 hipError_t launch_gather(const void *const *srcs, void *const *dsts, const size_t *bytes, int nseg,
                          hipStream_t stream) {

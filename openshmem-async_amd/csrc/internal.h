@@ -32,6 +32,13 @@ hipError_t launch_fold(int type, int op, void *out, const void *const *ins,
 hipError_t launch_gather(const void *const *srcs, void *const *dsts, const size_t *bytes, int nseg,
                          hipStream_t stream);
 
+// System-scope release + acquire on every XCD's L2 (buffer_wbl2 sc0 sc1 +
+// buffer_inv sc0 sc1 from blocks spread over all 8 XCDs), stream-ordered:
+// this GPU's writes become visible to peers reading its HBM over xGMI, and
+// no line of a peer's memory cached here survives into the next kernel.
+// Enqueued before every host barrier that hands data between GPUs.
+hipError_t launch_sys_fence(hipStream_t stream);
+
 // Position-aware 64-bit checksum of n elements of `type` at device address
 // ptr (16-byte aligned) into *out (device memory), stream-ordered.
 hipError_t launch_checksum(int type, const void *ptr, size_t n, unsigned long long *out,

@@ -72,8 +72,7 @@ int ipc_broadcast(char *target, const char *source, size_t bytes, int root_idx, 
     node::put_desc(d);
     const bool single = bytes <= half;
     if (root && staged && single) SHMX_HIP(hipMemcpyAsync(scr, source, bytes, hipMemcpyDefault, s));
-    SHMX_HIP(hipStreamSynchronize(s));
-    node::barrier(start, step, P);
+    node_sync(start, step, P, s);
     const int root_pe = start + root_idx * step;
     const node::Desc rd = root ? d : node::get_desc(root_pe);
     const bool chunked = rd.count != 0;
@@ -86,8 +85,7 @@ int ipc_broadcast(char *target, const char *source, size_t bytes, int root_idx, 
         const size_t cnt = std::min(C, bytes - c0);
         if (chunked && !single) {
             if (root) SHMX_HIP(hipMemcpyAsync(scr, source + c0, cnt, hipMemcpyDefault, s));
-            SHMX_HIP(hipStreamSynchronize(s));
-            node::barrier(start, step, P);
+            node_sync(start, step, P, s);
         }
         if (!root) {
             std::vector<const void *> from{rbase + (chunked ? 0 : c0)};
@@ -95,8 +93,7 @@ int ipc_broadcast(char *target, const char *source, size_t bytes, int root_idx, 
             std::vector<size_t> len{cnt};
             pull(from, to, len, s);
         }
-        SHMX_HIP(hipStreamSynchronize(s));
-        node::barrier(start, step, P);   // the root's copy is no longer read
+        node_sync(start, step, P, s);   // the root's copy is no longer read
     }
     if (tstaged) {
         SHMX_HIP(hipMemcpyAsync(target, dst, bytes, hipMemcpyDeviceToHost, s));
@@ -122,8 +119,7 @@ int ipc_collect(char *target, const char *source, size_t esize, size_t nelems, i
     // a staged source that fits is staged now (it is its own round 0)
     const bool prestaged = staged && mine <= half;
     if (prestaged) SHMX_HIP(hipMemcpyAsync(scr, source, mine, hipMemcpyDefault, s));
-    SHMX_HIP(hipStreamSynchronize(s));
-    node::barrier(start, step, P);
+    node_sync(start, step, P, s);
 
     std::vector<node::Desc> desc(P);
     std::vector<size_t> len(P), offs(P + 1, 0);
@@ -155,8 +151,7 @@ int ipc_collect(char *target, const char *source, size_t esize, size_t nelems, i
         if (r > 0 || late_stage) {
             if (staged && !prestaged && mine > r * H)
                 SHMX_HIP(hipMemcpyAsync(scr, source + r * H, std::min(H, mine - r * H), hipMemcpyDefault, s));
-            SHMX_HIP(hipStreamSynchronize(s));
-            node::barrier(start, step, P);
+            node_sync(start, step, P, s);
         }
         std::vector<const void *> from;
         std::vector<void *> to;
@@ -168,8 +163,7 @@ int ipc_collect(char *target, const char *source, size_t esize, size_t nelems, i
             n.push_back(std::min(H, len[i] - r * H));
         }
         pull(from, to, n, s);
-        SHMX_HIP(hipStreamSynchronize(s));
-        node::barrier(start, step, P);   // nobody reads this round's copies any more
+        node_sync(start, step, P, s);   // nobody reads this round's copies any more
     }
     if (tstaged) {
         SHMX_HIP(hipMemcpyAsync(target, dst, total, hipMemcpyDeviceToHost, s));

@@ -29,6 +29,7 @@ struct RegionSlot {
 struct PeSlot {
     RegionSlot region[kNumRegions];
     Desc desc;
+    std::atomic<int> vote;   // agree()
 };
 
 struct Shared {
@@ -190,6 +191,23 @@ char *peer_base(Region r, int q) {
 }
 
 const char *last_ipc_error() { return g_ipc_error; }
+
+uint64_t region_gen(Region r, int q) {
+    if (!g_node.sh || q < 0 || q >= g_node.npes) return 0;
+    return g_node.sh->pe[q].region[r].gen.load(std::memory_order_acquire);
+}
+
+bool agree(int start, int step, int P, bool ok) {
+    Shared *sh = g_node.sh;
+    if (!sh || P <= 1) return ok;
+    sh->pe[g_node.pe].vote.store(ok ? 1 : 0, std::memory_order_release);
+    barrier(start, step, P);
+    bool all = true;
+    for (int i = 0; i < P; ++i)
+        all &= sh->pe[start + i * step].vote.load(std::memory_order_acquire) != 0;
+    barrier(start, step, P);   // every vote is read before any member votes again
+    return all;
+}
 
 size_t peer_bytes(Region r, int q) {
     if (!g_node.sh || q < 0 || q >= g_node.npes) return 0;

@@ -62,6 +62,15 @@ char *peer_base(Region r, int pe);
 size_t peer_bytes(Region r, int pe);
 const char *last_ipc_error();   // why the last peer_base() returned nullptr
 
+// Generation of PE `pe`'s region (0 = never published); a mapping opened at
+// one generation stays valid until the owner publishes again.
+uint64_t region_gen(Region r, int pe);
+
+// Collective AND of `ok` over the set (two barriers): every member returns
+// the same answer, so a failure on one PE (say, an IPC mapping it could not
+// open) turns into the same error return on all of them instead of a hang.
+bool agree(int start, int step, int P, bool ok);
+
 void put_desc(const Desc &d);
 Desc get_desc(int pe);
 

@@ -94,6 +94,9 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
 void direct_release();
 // This PE's IPC scratch region (allocated and published on first use).
 char *ipc_scratch(size_t *bytes);
+// Hand data between the members' GPUs: system-scope fence on every XCD
+// (launch_sys_fence), wait for stream s, then the host barrier over the set.
+void node_sync(int start, int step, int P, hipStream_t s);
 // Broadcast and [f]collect on the IPC transport (ipc_coll.cpp): members pull
 // from the root's / each other's heap or scratch over IPC mappings.  target
 // and source are device pointers (the caller stages host buffers).

@@ -5,7 +5,9 @@
 //   * the barrier property: every member arrived before any member leaves;
 //   * descriptor exchange: after the entry barrier every member reads every
 //     other member's descriptor of THIS call (then an exit barrier, as
-//     shmemx_verify does).
+//     shmemx_verify does);
+//   * node::agree: every member gets the AND of the members' votes (the
+//     collective failure path of DIRECT's peer mappings).
 // No GPU: only the shared block, the pairwise counters and the descriptors.
 #include <sys/mman.h>
 #include <sys/wait.h>
@@ -74,6 +76,13 @@ int main(int argc, char **argv) {
                     if (shmx::node::get_desc(q).aux != (uint64_t)c * 1000 + q) bad = 2;
                 }
                 shmx::node::barrier(s.start, s.step, s.size);
+                if (c % 3 == 0) {
+                    // collective AND: on some calls the last member votes no
+                    const bool last = idx / s.step == s.size - 1;
+                    const bool no = c % 2 == 0 && last;
+                    const bool want = !(c % 2 == 0);
+                    if (shmx::node::agree(s.start, s.step, s.size, !no) != want) bad = 3;
+                }
             }
             shmx::node::barrier(0, 1, npes);
             shmx::node::detach(pe == 0);
