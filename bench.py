@@ -98,14 +98,18 @@ def cpu_baseline(n: int, reps: int):
 def host_e2e(n: int):
     """The north-star end-to-end rate: source/target in HOST memory (the
     reference's symmetric heap), blocking shmem_double_sum_to_all at
-    PE_size = 1 = H2D + device path + D2H.  Pageable (numpy) and pinned."""
+    PE_size = 1 = H2D + device path + D2H.  Pageable (numpy), the same numpy
+    arrays page-locked once with shmemx_host_register, and torch pinned."""
     import numpy as np
     res = {}
     psync = np.full(128, -1, dtype=np.int64)
-    for kind in ("pageable", "pinned"):
-        if kind == "pageable":
+    for kind in ("pageable", "registered", "pinned"):
+        if kind in ("pageable", "registered"):
             src = np.random.default_rng(1).random(n) + 1.0
             tgt = np.zeros(n)
+            if kind == "registered":   # shmemx_host_register, once, as on the heap segment
+                shm.host_register(src, src.nbytes)
+                shm.host_register(tgt, tgt.nbytes)
         else:
             src = torch.rand(n, dtype=torch.float64).pin_memory()
             tgt = torch.zeros(n, dtype=torch.float64).pin_memory()
@@ -117,6 +121,9 @@ def host_e2e(n: int):
             ts.append(time.perf_counter() - t0)
         t = statistics.median(ts)
         ok = bool((np.asarray(tgt) == np.asarray(src)).all())
+        if kind == "registered":
+            shm.host_unregister(src)
+            shm.host_unregister(tgt)
         res[kind] = {"GiBps": round(n * 8 / t / GiB, 2), "ms_per_call": round(t * 1e3, 2),
                      "correct": ok}
     return res
@@ -291,10 +298,27 @@ def main():
     torch.cuda.synchronize()
 
     extras = {}
+    # The operands live in the symmetric heap (shmem_malloc, one HBM segment
+    # per PE), as the reference's source/target are symmetric objects carved
+    # from its heap (memory/symmem.c:168-227).  Heap blocks also give the
+    # fold a steady 122 us, where separately allocated torch tensors land on
+    # a slow physical pairing now and then (129 us; profiles/r01_placement_*).
+    heap_blocks = [shm.malloc(nbytes) for _ in range(2)]
+    use_heap = max_over_ranks(0.0 if all(heap_blocks) else 1.0) == 0.0
+
+    def arr(t, k):
+        """Address of the k-th operand, holding t's values."""
+        if not use_heap:
+            return t
+        torch.cuda.synchronize()
+        shm.memcpy(heap_blocks[k], t, nbytes)
+        return heap_blocks[k]
+
     if world == 1:
         workload = "local reduce (fold acc = acc + in) of shmem_double_sum_to_all, 1 PE"
-        acc = src.clone()
-        inp = torch.rand(n, dtype=torch.float64, device="cuda", generator=g) + 1.0
+        inp_t = torch.rand(n, dtype=torch.float64, device="cuda", generator=g) + 1.0
+        acc = arr(src.clone(), 0)
+        inp = arr(inp_t, 1)
 
         def step():
             shm.fold("double", "sum", acc, inp, n, sp)
@@ -304,9 +328,11 @@ def main():
         over = "IPC transport, all ranks on one GPU (rehearsal)" if share else "RCCL over xGMI"
         workload = f"shmem_double_sum_to_all on {world} PEs (one per GPU), {over}"
         algo_used = a.algo
+        src_a = arr(src, 0)
+        tgt_a = heap_blocks[1] if use_heap else tgt
 
         def step():
-            shm.reduce_on_stream("double", "sum", tgt, src, n, 0, 0, world, algo_used, sp)
+            shm.reduce_on_stream("double", "sum", tgt_a, src_a, n, 0, 0, world, algo_used, sp)
         alg_bytes = None
 
     for _ in range(a.warmup):
@@ -320,12 +346,17 @@ def main():
 
     # correctness guard on what was timed
     if world == 1:
-        chk = src.clone()
-        torch.cuda.synchronize()          # clone ran on torch's stream, fold runs on sp
+        # one more step on the very arrays that were timed, from a known acc
+        chk = arr(src.clone(), 0)
+        torch.cuda.synchronize()
         shm.fold("double", "sum", chk, inp, n, sp)
         torch.cuda.synchronize()
-        ok = torch.equal(chk, src + inp)
+        got = torch.empty_like(src)
+        shm.memcpy(got, chk, nbytes)
+        ok = torch.equal(got, src + inp_t)
     else:
+        if use_heap:
+            shm.memcpy(tgt, tgt_a, nbytes)
         sample = torch.arange(0, n, max(1, n // 4096), device="cuda")
         mine = src[sample].cpu()
         allv = [torch.empty_like(mine) for _ in range(world)]
@@ -376,7 +407,8 @@ def main():
         "config": {"workload": workload, "nreduce": n, "type": "double", "op": "sum",
                    "PE_size": world, "algo": algo_used,
                    "parallelism": f"one PE per GPU x{world}",
-                   "transport": os.environ.get("SHMEMX_TRANSPORT", "rccl")},
+                   "transport": os.environ.get("SHMEMX_TRANSPORT", "rccl"),
+                   "arrays": "symmetric heap (shmem_malloc, HBM)" if use_heap else "hipMalloc (torch)"},
         "roofline": roofline, "cpu_baseline": cpu, "correct": ok, "extras": extras,
     }
     emitted = threading.Lock()
@@ -449,6 +481,9 @@ def main():
 
     timer.cancel()
     emit()
+    for blk in heap_blocks:
+        if blk:
+            shm.free(blk)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -292,6 +292,16 @@ int shmemx_reduce_plan(int type, int op, int nreduce, int PE_start,
  * NULL if `addr` is not in the heap segment or the peer is not mapped. */
 void *shmemx_heap_ptr(const void *addr, int pe);
 
+/* Page-lock a host range that will be handed to the entry points — the
+ * reference's symmetric heap segment, posix_memalign'd once at start-up
+ * (comms-inline.h:752-769) and handed to shmemi_mem_init (:794).  Host
+ * targets/sources inside it then take the pinned H2D/reduce/D2H pipeline
+ * instead of the pageable bounce ring.  SHMEMX_OK, or SHMEMX_EDEVICE when HIP
+ * refuses (the range stays pageable and still works).  Unregister before the
+ * range is freed. */
+int shmemx_host_register(void *base, size_t bytes);
+int shmemx_host_unregister(void *base);
+
 /* Element size in bytes of a SHMEMX_TYPE_* (0 if unknown); 1 if the
  * reference defines shmem_<type>_<op>_to_all (reduce-op.c:388-431);
  * 1 if this build runs that pair on the GPU. */

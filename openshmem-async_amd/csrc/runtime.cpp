@@ -1021,6 +1021,30 @@ void *shmemx_heap_ptr(const void *addr, int pe) {
     return b ? b + off : nullptr;
 }
 
+int shmemx_host_register(void *base, size_t bytes) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    clear_error();
+    if (!base || !bytes) return set_error(SHMEMX_EINVAL);
+    if (int rc = ensure_init()) return set_error(rc);
+    if (hipHostRegister(base, bytes, hipHostRegisterDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return set_error(SHMEMX_EDEVICE);
+    }
+    trace(LOG_MEMORY, "host range %p (%zu bytes) page-locked", base, bytes);
+    return SHMEMX_OK;
+}
+
+int shmemx_host_unregister(void *base) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    clear_error();
+    if (!base) return set_error(SHMEMX_EINVAL);
+    if (hipHostUnregister(base) != hipSuccess) {
+        (void)hipGetLastError();
+        return set_error(SHMEMX_EINVAL);
+    }
+    return SHMEMX_OK;
+}
+
 void *shmemx_get_stream(void) {
     std::lock_guard<std::recursive_mutex> lk(g_mu);
     if (ensure_init()) return nullptr;

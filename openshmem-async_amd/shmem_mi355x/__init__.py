@@ -123,6 +123,10 @@ def lib() -> ctypes.CDLL:
     L.shmem_realloc.restype = vp
     L.shmem_free.argtypes = [vp]
     L.shmem_free.restype = None
+    L.shmemx_host_register.argtypes = [vp, sz]
+    L.shmemx_host_register.restype = i
+    L.shmemx_host_unregister.argtypes = [vp]
+    L.shmemx_host_unregister.restype = i
     for t, o in REFERENCE_PAIRS:
         for prefix in ("shmem", "pshmem"):
             f = getattr(L, f"{prefix}_{t}_{o}_to_all")
@@ -311,6 +315,16 @@ def heap_ptr(address: int, pe: int) -> int:
     """shmemx_heap_ptr: PE `pe`'s copy of a symmetric-heap address, as mapped
     on this PE (0 if not mapped)."""
     return lib().shmemx_heap_ptr(address, pe) or 0
+
+
+def host_register(buf, nbytes: int) -> None:
+    """shmemx_host_register: page-lock a host range (the reference's heap
+    segment) so host operands inside it take the pinned pipeline."""
+    _check(lib().shmemx_host_register(addr(buf), nbytes), "shmemx_host_register")
+
+
+def host_unregister(buf) -> None:
+    _check(lib().shmemx_host_unregister(addr(buf)), "shmemx_host_unregister")
 
 
 _hip = None

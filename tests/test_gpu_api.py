@@ -196,6 +196,34 @@ def test_host_staging_pipeline_many_chunks(cuda, shm, oracle, t):
     assert big[3:3 + n].tobytes() == src.tobytes()
 
 
+def test_host_register_heap_segment(cuda, shm, oracle):
+    """shmemx_host_register on one page-aligned host block carved into source
+    and target (the reference's posix_memalign'd heap segment,
+    comms-inline.h:752-769): the arrays inside take the pinned pipeline, across
+    several 16 MiB chunks, and the results stay exact; unregistering an
+    unknown range is EINVAL."""
+    import mmap
+    n = (40 << 20) // 8 + 3
+    seg = mmap.mmap(-1, 2 * n * 8 + 4096)                   # page-aligned, pageable
+    base = np.frombuffer(seg, dtype=np.uint8)
+    src = base[:n * 8].view(np.float64)
+    tgt = base[n * 8 + 8:n * 8 + 8 + n * 8].view(np.float64)   # 8-byte aligned, as dlmalloc
+    src[:] = oracle.fill("double", 1, 5, n)
+    shm.host_register(base, base.nbytes)
+    try:
+        for op in ("sum", "max"):
+            tgt[:] = 0
+            shm.to_all("double", op, tgt, src, n, 0, 0, 1)
+            assert shm.last_error() == 0
+            assert tgt.tobytes() == src.tobytes()
+    finally:
+        shm.host_unregister(base)
+    with pytest.raises(shm.ShmemError):
+        shm.host_unregister(base)
+    del src, tgt, base
+    seg.close()
+
+
 def test_c_program_isx_verification(cuda, tmp_path):
     """A plain C99 program (examples/isx_verify.c) linked against the library:
     the reference's ISx verification (isx.c:615-624) with static host arrays,
