@@ -210,8 +210,16 @@ def direct_extra(world, n, src, sp, stream, barrier, max_over_ranks, steps):
             shm.reduce_on_stream("double", "sum", ht, hs, n, 0, 0, world, "direct", sp)
         for _ in range(2):
             step()
+        shm.direct_stats(reset=True)
         w, _ = time_region(step, steps, stream, barrier)
         w = max_over_ranks(w)
+        st = shm.direct_stats(reset=True)
+        calls = max(1.0, st.pop("calls"))
+        phases = {k: round(max_over_ranks(v / calls), 1) for k, v in st.items()}
+        remote = (world - 1) / world * nbytes          # bytes each PE pulls per phase
+        for k in ("fold", "gather"):
+            if phases.get(f"{k}_us"):
+                phases[f"{k}_xgmi_read_GBps"] = round(remote / (phases[f"{k}_us"] * 1e-6) / 1e9, 1)
         got = torch.empty(n, dtype=torch.float64, device="cuda")
         shm.memcpy(got, ht, nbytes)
         sample = torch.arange(0, n, max(1, n // 4096), device="cuda")
@@ -225,7 +233,8 @@ def direct_extra(world, n, src, sp, stream, barrier, max_over_ranks, steps):
         ok = shm.verify("double", ht, n, 0, 0, world) and ok
         ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
         return {"GiBps": round(world * nbytes * steps / w / GiB, 2),
-                "ms_per_call": round(w / steps * 1e3, 3), "correct": ok}
+                "ms_per_call": round(w / steps * 1e3, 3), "correct": ok,
+                "phases_per_call_max_over_ranks": phases}
     except shm.ShmemError as e:
         return str(e)
     finally:

@@ -292,6 +292,14 @@ int shmemx_reduce_plan(int type, int op, int nreduce, int PE_start,
  * NULL if `addr` is not in the heap segment or the peer is not mapped. */
 void *shmemx_heap_ptr(const void *addr, int pe);
 
+/* Host-side phase times of the DIRECT algorithm since the last reset, for
+ * tuning: out[0] = calls, then microseconds summed over them: [1] waiting for
+ * this PE's source (entry fence + stream), [2] entry barrier, [3] fold kernel
+ * (reduce-scatter from the peers' HBM), [4] barrier after it, [5] gather
+ * kernel (all-gather from the peers' HBM), [6] exit barrier(s).  Fills at most
+ * nout values and returns how many; reset != 0 zeroes the counters. */
+int shmemx_direct_stats(double *out, int nout, int reset);
+
 /* Page-lock a host range that will be handed to the entry points — the
  * reference's symmetric heap segment, posix_memalign'd once at start-up
  * (comms-inline.h:752-769) and handed to shmemi_mem_init (:794).  Host

@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <unordered_set>
 #include <vector>
@@ -121,10 +122,40 @@ bool map_members(const std::vector<node::Desc> &desc, bool local_write, int star
 
 }  // namespace
 
-void node_sync(int start, int step, int P, hipStream_t s) {
+namespace {
+
+// Host-side phase times of the DIRECT calls since the last reset
+// (shmemx_direct_stats): microseconds, summed over calls.
+enum Phase { kEntryWait, kEntryBarrier, kFold, kFoldBarrier, kGather, kExitBarrier, kNumPhases };
+double g_phase_us[kNumPhases];
+double g_calls;
+
+double now_us() {
+    return std::chrono::duration<double, std::micro>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+void node_sync(int start, int step, int P, hipStream_t s, double *stream_us, double *barrier_us,
+               double since_us) {
+    const double t0 = since_us >= 0 ? since_us : now_us();
     if (P > 1) SHMX_HIP(launch_sys_fence(s));
     SHMX_HIP(hipStreamSynchronize(s));
+    const double t1 = now_us();
     node::barrier(start, step, P);
+    if (stream_us) *stream_us += t1 - t0;
+    if (barrier_us) *barrier_us += now_us() - t1;
+}
+
+int direct_stats(double *out, int nout, bool reset) {
+    const int k = std::min(nout, 1 + (int)kNumPhases);
+    for (int i = 0; i < k; ++i) out[i] = i == 0 ? g_calls : g_phase_us[i - 1];
+    if (reset) {
+        g_calls = 0;
+        for (double &v : g_phase_us) v = 0;
+    }
+    return k;
 }
 
 char *ipc_scratch(size_t *bytes) {
@@ -191,7 +222,9 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     const bool single = n <= cmax;
     if (single && stage_src)
         SHMX_HIP(hipMemcpyAsync(g_scratch.base, src, bytes, hipMemcpyDeviceToDevice, s));
-    node_sync(start, step, P, s);   // my source (and its staging) is complete; reduce-op.c:217
+    g_calls += 1;
+    // my source (and its staging) is complete; reduce-op.c:217
+    node_sync(start, step, P, s, &g_phase_us[kEntryWait], &g_phase_us[kEntryBarrier]);
 
     // Every member reads the same descriptors, so all cut the same chunks
     // and walk them in the same direction.
@@ -227,7 +260,7 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
             // already seen every member done reading my scratch
             if (stage_src)
                 SHMX_HIP(hipMemcpyAsync(scratch_src, src + c0 * sz, cnt * sz, hipMemcpyDeviceToDevice, s));
-            node_sync(start, step, P, s);
+            node_sync(start, step, P, s, &g_phase_us[kEntryWait], &g_phase_us[kEntryBarrier]);
         }
         // a staged operand holds only the current chunk, at its region offset
         auto at = [&](char *base, const node::Loc &l, size_t elem) {
@@ -241,8 +274,10 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
             for (int i = 0; i < P; ++i)
                 if (!own_order || i != m) ins[k2++] = at(sbase[i], desc[i].src, c0);
             char *out = stage_tgt ? scratch_tgt : tgt + c0 * sz;
+            const double tf = now_us();
             fold_chain(type, op, out, ins.data(), P, cnt, s);
-            node_sync(start, step, P, s);   // reduce-op.c:250: no member reads my source any more
+            // reduce-op.c:250: no member reads my source any more
+            node_sync(start, step, P, s, &g_phase_us[kFold], &g_phase_us[kExitBarrier], tf);
             if (stage_tgt)
                 SHMX_HIP(hipMemcpyAsync(tgt + c0 * sz, scratch_tgt, cnt * sz, hipMemcpyDeviceToDevice, s));
             continue;
@@ -254,12 +289,14 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
         auto hi_of = [&](int i) { return std::min(cnt, (size_t)(i + 1) * slice); };
         const size_t lo = lo_of(m), hi = hi_of(m);
         // 1. my slice from every member's source, into my published target
+        const double tf = now_us();
         if (hi > lo) {
             for (int i = 0; i < P; ++i) ins[i] = at(sbase[i], desc[i].src, c0 + lo);
             char *out = at(tbase[m], desc[m].tgt, c0 + lo);
             SHMX_HIP(launch_fold(type, op, out, ins.data(), P, hi - lo, s));
         }
-        node_sync(start, step, P, s);   // every member's slice is final
+        // every member's slice is final
+        node_sync(start, step, P, s, &g_phase_us[kFold], &g_phase_us[kFoldBarrier], tf);
         // 2. every other member's slice (and mine, if it was staged) into my target
         std::vector<const void *> from;
         std::vector<void *> to;
@@ -271,8 +308,10 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
             to.push_back(tgt + (c0 + lo_of(i)) * sz);
             len.push_back((hi_of(i) - lo_of(i)) * sz);
         }
+        const double tg = now_us();
         SHMX_HIP(launch_gather(from.data(), to.data(), len.data(), (int)from.size(), s));
-        node_sync(start, step, P, s);   // reduce-op.c:250: no member reads my slice any more
+        // reduce-op.c:250: no member reads my slice any more
+        node_sync(start, step, P, s, &g_phase_us[kGather], &g_phase_us[kExitBarrier], tg);
     }
     if (local_write && stage_tgt) SHMX_HIP(hipStreamSynchronize(s));
     return SHMEMX_OK;

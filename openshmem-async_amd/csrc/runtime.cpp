@@ -1021,6 +1021,15 @@ void *shmemx_heap_ptr(const void *addr, int pe) {
     return b ? b + off : nullptr;
 }
 
+int shmemx_direct_stats(double *out, int nout, int reset) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    if (!out || nout < 0) {
+        set_error(SHMEMX_EINVAL);
+        return 0;
+    }
+    return direct_stats(out, nout, reset != 0);
+}
+
 int shmemx_host_register(void *base, size_t bytes) {
     std::lock_guard<std::recursive_mutex> lk(g_mu);
     clear_error();

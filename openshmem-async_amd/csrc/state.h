@@ -96,7 +96,12 @@ void direct_release();
 char *ipc_scratch(size_t *bytes);
 // Hand data between the members' GPUs: system-scope fence on every XCD
 // (launch_sys_fence), wait for stream s, then the host barrier over the set.
-void node_sync(int start, int step, int P, hipStream_t s);
+// Optionally adds the time spent waiting for the stream (from since_us, a
+// steady-clock stamp in microseconds, if >= 0) and in the barrier.
+void node_sync(int start, int step, int P, hipStream_t s, double *stream_us = nullptr,
+               double *barrier_us = nullptr, double since_us = -1);
+// DIRECT phase times since the last reset (shmemx_direct_stats).
+int direct_stats(double *out, int nout, bool reset);
 // Broadcast and [f]collect on the IPC transport (ipc_coll.cpp): members pull
 // from the root's / each other's heap or scratch over IPC mappings.  target
 // and source are device pointers (the caller stages host buffers).

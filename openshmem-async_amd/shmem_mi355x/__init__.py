@@ -123,6 +123,8 @@ def lib() -> ctypes.CDLL:
     L.shmem_realloc.restype = vp
     L.shmem_free.argtypes = [vp]
     L.shmem_free.restype = None
+    L.shmemx_direct_stats.argtypes = [ctypes.POINTER(ctypes.c_double), i, i]
+    L.shmemx_direct_stats.restype = i
     L.shmemx_host_register.argtypes = [vp, sz]
     L.shmemx_host_register.restype = i
     L.shmemx_host_unregister.argtypes = [vp]
@@ -315,6 +317,20 @@ def heap_ptr(address: int, pe: int) -> int:
     """shmemx_heap_ptr: PE `pe`'s copy of a symmetric-heap address, as mapped
     on this PE (0 if not mapped)."""
     return lib().shmemx_heap_ptr(address, pe) or 0
+
+
+DIRECT_PHASES = ("entry_wait_us", "entry_barrier_us", "fold_us", "fold_barrier_us",
+                 "gather_us", "exit_barrier_us")
+
+
+def direct_stats(reset: bool = True) -> dict:
+    """shmemx_direct_stats: DIRECT calls since the last reset and the host-side
+    microseconds summed over them per phase."""
+    buf = (ctypes.c_double * (1 + len(DIRECT_PHASES)))()
+    k = lib().shmemx_direct_stats(buf, len(buf), 1 if reset else 0)
+    out = {"calls": buf[0]}
+    out.update({name: buf[i + 1] for i, name in enumerate(DIRECT_PHASES[:max(0, k - 1)])})
+    return out
 
 
 def host_register(buf, nbytes: int) -> None:

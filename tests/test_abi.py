@@ -165,3 +165,12 @@ def test_plan_shards_cover_and_align(shm, t, P_, n):
         assert r.chunk % g == 0 and r.tail < P_ * g
     q = shm.plan(t, "sum", n, 0, 0, P_, 0, P_, "gather")
     assert q.ws_bytes == n * P_ * sz
+
+
+def test_direct_stats_without_calls(shm):
+    """shmemx_direct_stats is host-only bookkeeping: no DIRECT call yet means
+    zero calls and zero time in every phase, and it never needs a device."""
+    st = shm.direct_stats(reset=True)
+    assert st["calls"] == 0
+    assert set(st) == {"calls", *shm.DIRECT_PHASES}
+    assert all(v == 0 for v in st.values())
