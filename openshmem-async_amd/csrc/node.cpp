@@ -149,7 +149,18 @@ void barrier(int start, int step, int P) {
 void publish(Region r, void *base, size_t bytes) {
     if (!g_node.sh) return;
     RegionSlot &s = g_node.sh->pe[g_node.pe].region[r];
-    SHMX_HIP(hipIpcGetMemHandle(&s.handle, base));
+    const hipError_t e = hipIpcGetMemHandle(&s.handle, base);
+    if (e != hipSuccess) {
+        // Not fatal: the region stays usable here, and a peer that tries to
+        // map it sees bytes == 0 and fails its call collectively (DIRECT's
+        // vote) or gets NULL (shmemx_heap_ptr).  The generation still moves,
+        // so nobody keeps a mapping of what was published before.
+        (void)hipGetLastError();
+        trace(LOG_MEMORY, "hipIpcGetMemHandle(%s at %p): %s; peers cannot map it",
+              r == kHeap ? "heap" : "scratch", base, hipGetErrorString(e));
+        std::memset(&s.handle, 0, sizeof s.handle);
+        bytes = 0;
+    }
     s.bytes = bytes;
     s.gen.fetch_add(1, std::memory_order_release);
     g_node.own[r] = static_cast<char *>(base);
@@ -173,6 +184,11 @@ char *peer_base(Region r, int q) {
     Mapping &mp = g_node.peer[r][q];
     if (mp.base && mp.gen == gen) return mp.base;
     close_peer(r, q);
+    if (s.bytes == 0) {
+        snprintf(g_ipc_error, sizeof g_ipc_error, "PE %d could not export its %s", q,
+                 r == kHeap ? "heap" : "scratch");
+        return nullptr;
+    }
     void *p = nullptr;
     hipError_t e = hipIpcOpenMemHandle(&p, s.handle, hipIpcMemLazyEnablePeerAccess);
     if (e != hipSuccess) {
