@@ -190,14 +190,50 @@ def latency_extras(world, barrier, max_over_ranks):
                 shm.to_all("longlong", "sum", tgt, src, n, 0, 0, world, None, psync)
             t = max_over_ranks((time.perf_counter() - t0) / reps)
             out[f"longlong_sum_n{n}_{where}_us"] = round(t * 1e6, 1)
+    if world > 1:
+        # symmetric-heap operands: DIRECT (host barriers) and SIGNAL (device
+        # barriers), each call waited for, as a blocking call would be
+        hs, ht = malloc_pair(4096 * 8)
+        if hs and ht:
+            try:
+                for algo in ("direct", "signal"):
+                    for n in (1, 64, 4096):
+                        def call():
+                            shm.reduce_on_stream("longlong", "sum", ht, hs, n, 0, 0, world, algo)
+                            torch.cuda.synchronize()
+                        for _ in range(5):
+                            call()
+                        barrier()
+                        reps = 200
+                        t0 = time.perf_counter()
+                        for _ in range(reps):
+                            call()
+                        t = max_over_ranks((time.perf_counter() - t0) / reps)
+                        out[f"longlong_sum_n{n}_heap_{algo}_us"] = round(t * 1e6, 1)
+            except shm.ShmemError as e:
+                out["heap_latency"] = str(e)
+        if ht:
+            shm.free(ht)
+        if hs:
+            shm.free(hs)
     return out
 
 
-def direct_extra(world, n, src, sp, stream, barrier, max_over_ranks, steps):
-    """SHMEMX_ALGO_DIRECT with source and target in the symmetric heap (HBM,
-    IPC-mapped): each PE's kernels read its peers' arrays over xGMI in place
-    (reduce-scatter then all-gather, both pulls).  Checked against the same
-    ULP bound as the main line and for cross-PE consistency."""
+def malloc_pair(nbytes):
+    """Two symmetric-heap blocks (collective), zeroed."""
+    hs, ht = shm.malloc(nbytes), shm.malloc(nbytes)
+    for h in (hs, ht):
+        if h:
+            shm.memcpy(h, torch.zeros(nbytes, dtype=torch.uint8), nbytes)
+    return hs, ht
+
+
+def direct_extra(world, n, src, sp, stream, barrier, max_over_ranks, steps, algo="direct"):
+    """SHMEMX_ALGO_DIRECT (host barriers) or SHMEMX_ALGO_SIGNAL (device
+    barriers, stream-ordered) with source and target in the symmetric heap
+    (HBM, IPC-mapped): each PE's kernels read its peers' arrays over xGMI in
+    place (reduce-scatter then all-gather, both pulls).  Checked against the
+    same ULP bound as the main line and for cross-PE consistency."""
     nbytes = n * 8
     hs = ht = 0
     try:
@@ -207,15 +243,15 @@ def direct_extra(world, n, src, sp, stream, barrier, max_over_ranks, steps):
         shm.memcpy(hs, src, nbytes)
 
         def step():
-            shm.reduce_on_stream("double", "sum", ht, hs, n, 0, 0, world, "direct", sp)
+            shm.reduce_on_stream("double", "sum", ht, hs, n, 0, 0, world, algo, sp)
         for _ in range(2):
             step()
         shm.direct_stats(reset=True)
         w, _ = time_region(step, steps, stream, barrier)
         w = max_over_ranks(w)
         st = shm.direct_stats(reset=True)
-        calls = max(1.0, st.pop("calls"))
-        phases = {k: round(max_over_ranks(v / calls), 1) for k, v in st.items()}
+        calls = st.pop("calls")
+        phases = {k: round(max_over_ranks(v / calls), 1) for k, v in st.items()} if calls else {}
         remote = (world - 1) / world * nbytes          # bytes each PE pulls per phase
         for k in ("fold", "gather"):
             if phases.get(f"{k}_us"):
@@ -232,9 +268,11 @@ def direct_extra(world, n, src, sp, stream, barrier, max_over_ranks, steps):
         ok = bool(((got[sample].cpu() - ref).abs() <= tol).all())
         ok = shm.verify("double", ht, n, 0, 0, world) and ok
         ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
-        return {"GiBps": round(world * nbytes * steps / w / GiB, 2),
-                "ms_per_call": round(w / steps * 1e3, 3), "correct": ok,
-                "phases_per_call_max_over_ranks": phases}
+        out = {"GiBps": round(world * nbytes * steps / w / GiB, 2),
+               "ms_per_call": round(w / steps * 1e3, 3), "correct": ok}
+        if phases:
+            out["phases_per_call_max_over_ranks"] = phases
+        return out
     except shm.ShmemError as e:
         return str(e)
     finally:
@@ -485,6 +523,8 @@ def main():
             guarded(f"algo_{alt}_GiBps", alt_rate)
         guarded("direct_heap", lambda: direct_extra(world, n, src, sp, stream, barrier,
                                                     max_over_ranks, max(3, a.steps // 4)))
+        guarded("signal_heap", lambda: direct_extra(world, n, src, sp, stream, barrier,
+                                                    max_over_ranks, max(3, a.steps // 4), "signal"))
         guarded("configs", lambda: config_extras(world, stream, barrier, max_over_ranks))
         guarded("latency", lambda: latency_extras(world, barrier, max_over_ranks))
 

@@ -204,17 +204,26 @@ enum {
  *   ALLREDUCE  one ncclAllReduce (full set, RCCL-native pairs, as RCCL)
  *   DIRECT  one HIP kernel per PE reads slice m of every member's source
  *           straight from the peers' HBM (IPC-mapped symmetric heap, over
- *           xGMI), folds in active-set order and stores the result into
- *           every member's target; host barriers before and after (the
- *           reference's two).  Any set of <= 16 PEs, any op, PE_start bits
- *           on every PE.  Operands outside the symmetric heap are staged
- *           through an IPC scratch region.  Host-synchronous.
+ *           xGMI) and folds it in active-set order into its own target; a
+ *           second kernel pulls the other members' result slices.  Host
+ *           barriers around and between (the reference's two plus one).
+ *           Any set of <= 16 PEs, any op, PE_start bits on every PE.
+ *           Operands outside the symmetric heap are staged through an IPC
+ *           scratch region.  Host-synchronous.
+ *   SIGNAL  DIRECT's pulls with device-side barriers (per-peer counters in
+ *           each PE's heap segment, polled over xGMI): no host wait,
+ *           stream-ordered, capturable.  Source and target must both be in
+ *           the symmetric heap on every member (ENOTSUP otherwise); calls on
+ *           one PE must not overlap in time.  A peer that never arrives
+ *           times out after $SHMEMX_SIGNAL_TIMEOUT s (default 20); the next
+ *           blocking call then aborts with a FATAL line.
  * With $SHMEMX_TRANSPORT=ipc there is no RCCL communicator: AUTO means
  * DIRECT, GATHER runs as a DIRECT-style kernel in each PE's own order, and
- * RCCL / A2A / ALLREDUCE are ENOTSUP. */
+ * RCCL / A2A / ALLREDUCE are ENOTSUP; SIGNAL runs on both transports. */
 enum {
     SHMEMX_ALGO_AUTO = 0, SHMEMX_ALGO_RCCL, SHMEMX_ALGO_A2A,
-    SHMEMX_ALGO_GATHER, SHMEMX_ALGO_ALLREDUCE, SHMEMX_ALGO_DIRECT, SHMEMX_NALGOS
+    SHMEMX_ALGO_GATHER, SHMEMX_ALGO_ALLREDUCE, SHMEMX_ALGO_DIRECT, SHMEMX_ALGO_SIGNAL,
+    SHMEMX_NALGOS
 };
 
 /* Error codes returned by shmemx_* and stored for shmemx_reduce_last_error. */

@@ -85,39 +85,19 @@ bool ensure_scratch() {
     return true;
 }
 
-// Open (or reuse) the mappings of every region the members' descriptors name.
-// The first time a set meets a given combination of region generations, the
-// members vote (node::agree), so a mapping that fails on one PE fails the
-// call on all of them alike; the combinations that passed are remembered, and
-// every member decides identically whether to vote (same set, same
-// descriptors, same generations from the shared block).
 std::unordered_set<uint64_t> g_voted;
 
+// The region of each member that DIRECT reads: its source, and its target
+// when the peers gather from it.
 bool map_members(const std::vector<node::Desc> &desc, bool local_write, int start, int step,
                  int P) {
-    uint64_t key = 1469598103934665603ull;
-    auto mix = [&key](uint64_t v) { key = (key ^ v) * 1099511628211ull; };
-    mix((uint64_t)start);
-    mix((uint64_t)step);
-    mix((uint64_t)P);
-    bool ok = true;
+    std::vector<std::pair<node::Region, int>> regs;
     for (int i = 0; i < P; ++i) {
-        const int pe = start + i * step;
-        for (int k = 0; k < (local_write ? 1 : 2); ++k) {
-            const node::Region r = static_cast<node::Region>(k == 0 ? desc[i].src.region
-                                                                   : desc[i].tgt.region);
-            mix((uint64_t)r);
-            mix(node::region_gen(r, pe));
-            ok &= node::peer_base(r, pe) != nullptr;
-        }
+        regs.emplace_back(static_cast<node::Region>(desc[i].src.region), start + i * step);
+        if (!local_write)
+            regs.emplace_back(static_cast<node::Region>(desc[i].tgt.region), start + i * step);
     }
-    if (g_voted.count(key)) {   // every member mapped these before
-        if (!ok) fatal("DIRECT reduction: a peer region mapped before is gone", node::last_ipc_error());
-        return true;
-    }
-    if (!node::agree(start, step, P, ok)) return false;
-    g_voted.insert(key);
-    return true;
+    return map_regions(regs, start, step, P);
 }
 
 }  // namespace
@@ -136,6 +116,34 @@ double now_us() {
 }
 
 }  // namespace
+
+// Open (or reuse) the mappings of the given (region, PE) pairs.  The first
+// time a set meets a given combination of region generations, the members
+// vote (node::agree), so a mapping that fails on one PE fails the call on all
+// of them alike; the combinations that passed are remembered, and every
+// member decides identically whether to vote (same set, same regions, same
+// generations from the shared block).
+bool map_regions(const std::vector<std::pair<node::Region, int>> &regs, int start, int step, int P) {
+    uint64_t key = 1469598103934665603ull;
+    auto mix = [&key](uint64_t v) { key = (key ^ v) * 1099511628211ull; };
+    mix((uint64_t)start);
+    mix((uint64_t)step);
+    mix((uint64_t)P);
+    bool ok = true;
+    for (const auto &rp : regs) {
+        mix((uint64_t)rp.first);
+        mix((uint64_t)rp.second);
+        mix(node::region_gen(rp.first, rp.second));
+        ok &= node::peer_base(rp.first, rp.second) != nullptr;
+    }
+    if (g_voted.count(key)) {   // every member mapped these before
+        if (!ok) fatal("peer region mapped before is gone", node::last_ipc_error());
+        return true;
+    }
+    if (!node::agree(start, step, P, ok)) return false;
+    g_voted.insert(key);
+    return true;
+}
 
 void node_sync(int start, int step, int P, hipStream_t s, double *stream_us, double *barrier_us,
                double since_us) {

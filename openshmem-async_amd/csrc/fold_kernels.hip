@@ -541,7 +541,33 @@ __global__ __launch_bounds__(64) void sys_fence_kernel() {
     if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");   // system scope
 }
 
+__global__ __launch_bounds__(64) void signal_kernel(SignalArgs a) {
+    const int i = threadIdx.x;
+    if (i >= a.P || a.pe[i] == a.me) return;
+    unsigned long long *mine = a.mine + a.pe[i];
+    const unsigned long long want =
+        __hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1;
+    __hip_atomic_store(mine, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned long long *theirs = a.peer[i] + a.me;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(theirs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+            __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
 }  // namespace
+
+hipError_t launch_signal(const SignalArgs &a, hipStream_t stream) {
+    if (a.P < 1 || a.P > kMaxFoldInputs || !a.mine || !a.err) return hipErrorInvalidValue;
+    for (int i = 0; i < a.P; ++i)
+        if (a.pe[i] != a.me && !a.peer[i]) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(signal_kernel, dim3(1), dim3(64), 0, stream, a);
+    return hipGetLastError();
+}
 
 hipError_t launch_sys_fence(hipStream_t stream) {
     hipLaunchKernelGGL(sys_fence_kernel, dim3(kFenceBlocks), dim3(64), 0, stream);

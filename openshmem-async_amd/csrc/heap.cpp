@@ -17,6 +17,10 @@ namespace {
 // The reference's default is 32 MiB (comms-shared.h:74) for a host heap; an
 // MI355X PE has 288 GB of HBM, and the heap holds whole reduction operands.
 constexpr uint64_t kDefaultHeapBytes = uint64_t(4) << 30;
+// The top of the segment is the library's own: the SIGNAL algorithm's
+// counters (signal_area()), zeroed at creation, at the same offset on every
+// PE and mapped by the peers together with the heap.
+constexpr uint64_t kSignalBytes = uint64_t(64) << 10;
 
 struct Private {
     void *base;     // what hipMalloc returned
@@ -38,6 +42,7 @@ bool ensure_segment() {
         if (!parse_size(e, &bytes) || bytes == 0)
             fatal("shmem_malloc", "unusable SHMEM_SYMMETRIC_HEAP_SIZE");
     }
+    bytes += kSignalBytes;
     bytes = (bytes + (uint64_t(1) << 21) - 1) & ~((uint64_t(1) << 21) - 1);   // 2 MiB pages
     void *p = nullptr;
     if (hipMalloc(&p, bytes) != hipSuccess) {
@@ -48,7 +53,9 @@ bool ensure_segment() {
         return false;
     }
     g_heap.base = static_cast<char *>(p);
-    g_heap.arena.reset(bytes);
+    g_heap.arena.reset(bytes - kSignalBytes);
+    SHMX_HIP(hipMemset(g_heap.base + (bytes - kSignalBytes), 0, kSignalBytes));
+    SHMX_HIP(hipDeviceSynchronize());
     node::publish(node::kHeap, p, bytes);   // peers map it after the allocation's barrier
     trace(LOG_MEMORY, "symmetric heap segment: %llu bytes of HBM at %p", (unsigned long long)bytes, p);
     return true;
@@ -105,6 +112,13 @@ bool offset_of(const void *p, size_t bytes, uint64_t *off) {
     *off = o;
     return true;
 }
+
+unsigned long long *signal_area() {
+    if (!ensure_segment()) return nullptr;
+    return reinterpret_cast<unsigned long long *>(g_heap.base + g_heap.arena.capacity());
+}
+
+uint64_t signal_offset() { return g_heap.arena.capacity(); }
 
 void release_all() {
     for (auto &kv : g_heap.priv) (void)hipFree(kv.second.base);

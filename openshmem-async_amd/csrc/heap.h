@@ -55,6 +55,11 @@ bool free(void *p);
 size_t size_of(const void *p);                  // 0 if not a heap block
 // Offset of [p, p + bytes) inside this PE's segment; false if not inside it.
 bool offset_of(const void *p, size_t bytes, uint64_t *off);
+// The library's signal area at the top of the segment (outside the arena):
+// 64 KiB, zero at creation, at signal_offset() from the segment base on every
+// PE.  nullptr if there is no segment.
+unsigned long long *signal_area();
+uint64_t signal_offset();
 void release_all();                             // shmem_finalize
 
 }  // namespace heap

@@ -39,6 +39,28 @@ hipError_t launch_gather(const void *const *srcs, void *const *dsts, const size_
 // Enqueued before every host barrier that hands data between GPUs.
 hipError_t launch_sys_fence(hipStream_t stream);
 
+// Device-side barrier of the SIGNAL algorithm (signal.cpp): the reference's
+// linear barrier (barrier-linear.c:51-77: every member bumps a counter of
+// every other member, then waits for its own to reach PE_size - 1) as one
+// 64-lane wave, with the counters kept where only their owner writes them.
+// cnt[q] in a PE's signal area = barriers that PE has entered together with
+// PE q.  Lane i (member i != me) bumps mine[pe[i]] with a system-scope store,
+// then polls peer[i][me] (member i's counter for me, read over xGMI) until it
+// has caught up.  Counter state lives on the device, so a captured graph
+// replays correctly.  A wait longer than timeout_ticks (s_memrealtime, 100
+// MHz) sets *err and gives up, so a missing peer never hangs the GPU.
+// Enqueue launch_sys_fence first: it publishes this GPU's writes and drops
+// stale peer lines on every XCD, which a single wave cannot do.
+struct SignalArgs {
+    unsigned long long *mine;
+    const unsigned long long *peer[kMaxFoldInputs];
+    int pe[kMaxFoldInputs];
+    int P, me;
+    unsigned long long timeout_ticks;
+    unsigned int *err;   // host-mapped
+};
+hipError_t launch_signal(const SignalArgs &a, hipStream_t stream);
+
 // Position-aware 64-bit checksum of n elements of `type` at device address
 // ptr (16-byte aligned) into *out (device memory), stream-ordered.
 hipError_t launch_checksum(int type, const void *ptr, size_t n, unsigned long long *out,

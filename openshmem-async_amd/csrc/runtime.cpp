@@ -132,6 +132,7 @@ static int parse_algo(const char *s) {
     if (v == "gather") return SHMEMX_ALGO_GATHER;
     if (v == "allreduce") return SHMEMX_ALGO_ALLREDUCE;
     if (v == "direct") return SHMEMX_ALGO_DIRECT;
+    if (v == "signal") return SHMEMX_ALGO_SIGNAL;
     return SHMEMX_ALGO_AUTO;
 }
 
@@ -336,9 +337,11 @@ static int make_plan(int type, int op, int nreduce, int start, int logstride,
     if ((algo == SHMEMX_ALGO_RCCL || algo == SHMEMX_ALGO_ALLREDUCE) &&
         !(world && rccl_native(type, op)))
         return SHMEMX_ENOTSUP;
-    if (g_state.ipc_only && algo != SHMEMX_ALGO_DIRECT && algo != SHMEMX_ALGO_GATHER)
+    if (g_state.ipc_only && algo != SHMEMX_ALGO_DIRECT && algo != SHMEMX_ALGO_GATHER &&
+        algo != SHMEMX_ALGO_SIGNAL)
         return SHMEMX_ENOTSUP;   // no RCCL communicator on the IPC transport
-    if (algo == SHMEMX_ALGO_DIRECT && size > kMaxFoldInputs) return SHMEMX_ENOTSUP;
+    if ((algo == SHMEMX_ALGO_DIRECT || algo == SHMEMX_ALGO_SIGNAL) && size > kMaxFoldInputs)
+        return SHMEMX_ENOTSUP;
     p->algo = algo;
     p->member = m;
     p->nmembers = P;
@@ -364,7 +367,8 @@ static int make_plan(int type, int op, int nreduce, int start, int logstride,
         p->ws_bytes = c * P * sz;
         break;
     }
-    case SHMEMX_ALGO_DIRECT: {   // slice per member; no workspace
+    case SHMEMX_ALGO_DIRECT:
+    case SHMEMX_ALGO_SIGNAL: {   // slice per member; no workspace
         long long c = (n + P - 1) / P;
         p->chunk = (c + g - 1) / g * g;
         break;
@@ -457,6 +461,13 @@ static int reduce_device(int type, int op, void *target, const void *source,
     if (rc) return set_error(rc);
     if (nreduce == 0) return SHMEMX_OK;
     const bool collective = size > 1 || g_state.force_collective;
+    if (collective && p.algo == SHMEMX_ALGO_SIGNAL) {
+        if (log_enabled(LOG_REDUCTION))
+            trace(LOG_REDUCTION, "type %d op %d nreduce %d set (%d,%d,%d) member %d algo signal",
+                  type, op, nreduce, start, logstride, size, p.member);
+        return signal_reduce(type, op, static_cast<char *>(target), static_cast<const char *>(source),
+                             nreduce, start, logstride, p, s);
+    }
     const bool over_ipc = p.algo == SHMEMX_ALGO_DIRECT ||
                           (p.algo == SHMEMX_ALGO_GATHER && g_state.ipc_only);
     if (collective && over_ipc) {
@@ -475,7 +486,7 @@ static int reduce_device(int type, int op, void *target, const void *source,
 
     if (log_enabled(LOG_REDUCTION)) {
         static const char *const algos[SHMEMX_NALGOS] = {"auto", "rccl", "a2a", "gather",
-                                                         "allreduce", "direct"};
+                                                         "allreduce", "direct", "signal"};
         trace(LOG_REDUCTION, "type %d op %d nreduce %d set (%d,%d,%d) member %d algo %s chunk %lld",
               type, op, nreduce, start, logstride, size, p.member, algos[p.algo], p.chunk);
         // the reference's own messages, reduce-op.c:199-210
@@ -757,6 +768,7 @@ void reduce_blocking(int type, int op, void *target, const void *source,
     if (tdev && sdev) {
         reduce_device(type, op, target, source, nreduce, start, logstride, size, g_state.algo, s);
         SHMX_HIP(hipStreamSynchronize(s));
+        if (signal_timed_out()) fatal("SIGNAL reduction", "a member never reached the device barrier");
         return;
     }
     // Host-resident symmetric arrays (the reference's heap): stage over PCIe

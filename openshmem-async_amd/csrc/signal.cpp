@@ -1,0 +1,159 @@
+// SIGNAL algorithm: DIRECT's pulls (direct.cpp) with the barriers moved onto
+// the GPU, so a reduction is pure stream work — no host wait, no host
+// barrier, capturable into a hipGraph.
+//
+// The reference synchronises its reduction with two linear barriers
+// (reduce-op.c:217,250; barrier-linear.c:51-77: remote increments of pSync
+// counters, then a wait until the local counter has heard from every peer).
+// Here each barrier is two stream-ordered launches:
+//   launch_sys_fence  every XCD writes back its L2 and drops stale peer lines
+//                     (this GPU's results become visible over xGMI);
+//   launch_signal     one wave bumps this PE's per-peer counters in its own
+//                     signal area (system-scope stores) and polls the peers'
+//                     counters for it over xGMI (system-scope loads);
+// the counters live at the top of every PE's heap segment
+// (heap::signal_area), at the same offset on every PE.
+//
+// Operands must be symmetric — both in the heap, which is what OpenSHMEM
+// requires of source and target — so every member computes every peer's
+// address from its own offsets, with no descriptor exchange.  A member whose
+// operands are not in the heap returns ENOTSUP; its peers' device barriers
+// then time out ($SHMEMX_SIGNAL_TIMEOUT seconds, default 20) and the next
+// blocking call reports it.
+//
+// Two-shot (set order, PE_start bits on every member, as DIRECT):
+//   barrier                 every source is final; nobody reads my target
+//   fold                    slice m of all P sources -> my target's slice m
+//   barrier                 every slice is final
+//   gather                  the other P-1 slices from the peers' targets
+//   barrier                 nobody reads my source or target any more
+// One shot (arrays up to $SHMEMX_DIRECT_ONESHOT_KB, target != source):
+//   barrier; fold all of every source -> my target; barrier.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <vector>
+
+#include "heap.h"
+#include "internal.h"
+#include "node.h"
+#include "shmem_reduce_mi355x.h"
+#include "state.h"
+
+namespace shmx {
+
+namespace {
+
+constexpr size_t kDefaultOneShotBytes = size_t(256) << 10;
+
+size_t oneshot_bytes() {
+    static const size_t b = [] {
+        const char *e = std::getenv("SHMEMX_DIRECT_ONESHOT_KB");
+        return e ? size_t(std::atol(e)) << 10 : kDefaultOneShotBytes;
+    }();
+    return b;
+}
+
+unsigned long long timeout_ticks() {   // s_memrealtime runs at 100 MHz
+    static const unsigned long long t = [] {
+        const char *e = std::getenv("SHMEMX_SIGNAL_TIMEOUT");
+        const double s = e ? std::atof(e) : 0.0;
+        return (unsigned long long)((s > 0 ? s : 20.0) * 1e8);
+    }();
+    return t;
+}
+
+// Host-mapped error word the signal kernel sets on a timeout.
+unsigned int *error_word() {
+    static unsigned int *w = [] {
+        void *p = nullptr;
+        SHMX_HIP(hipHostMalloc(&p, sizeof(unsigned int), hipHostMallocCoherent));
+        *static_cast<volatile unsigned int *>(p) = 0;
+        return static_cast<unsigned int *>(p);
+    }();
+    return w;
+}
+
+}  // namespace
+
+bool signal_timed_out() {
+    volatile unsigned int *w = error_word();
+    const bool bad = *w != 0;
+    *w = 0;
+    return bad;
+}
+
+int signal_reduce(int type, int op, char *tgt, const char *src, int nreduce, int start,
+                  int logstride, const shmemx_plan_t &p, hipStream_t s) {
+    const int P = p.nmembers, m = p.member, step = 1 << logstride;
+    if (!node::up() || P > kMaxFoldInputs) return set_error(SHMEMX_ENOTSUP);
+    const size_t sz = (size_t)p.elem_size;
+    const size_t n = (size_t)nreduce;
+    const size_t bytes = n * sz;
+    uint64_t soff = 0, toff = 0;
+    const bool partial = tgt != src && tgt < src + bytes && src < tgt + bytes;
+    if (partial || !heap::offset_of(src, bytes, &soff) || !heap::offset_of(tgt, bytes, &toff))
+        return set_error(SHMEMX_ENOTSUP);
+    unsigned long long *mine = heap::signal_area();
+    if (!mine) return set_error(SHMEMX_ENOTSUP);
+    // The peers' heap segments: mapped (and voted on) the first time this set
+    // meets them, plain lookups afterwards.
+    std::vector<std::pair<node::Region, int>> regs;
+    for (int i = 0; i < P; ++i) regs.emplace_back(node::kHeap, start + i * step);
+    if (!map_regions(regs, start, step, P)) {
+        trace(LOG_REDUCTION, "SIGNAL: a member could not map a peer heap (%s)", node::last_ipc_error());
+        return set_error(SHMEMX_ENOTSUP);
+    }
+    std::vector<char *> hb(P);
+    SignalArgs sa{};
+    sa.mine = mine;
+    sa.P = P;
+    sa.me = g_state.pe;
+    sa.timeout_ticks = timeout_ticks();
+    sa.err = error_word();
+    const uint64_t sig = heap::signal_offset();
+    for (int i = 0; i < P; ++i) {
+        const int q = start + i * step;
+        hb[i] = node::peer_base(node::kHeap, q);
+        sa.pe[i] = q;
+        sa.peer[i] = reinterpret_cast<const unsigned long long *>(hb[i] + sig);
+    }
+    auto barrier = [&] {
+        SHMX_HIP(launch_sys_fence(s));
+        SHMX_HIP(launch_signal(sa, s));
+    };
+    const void *ins[kMaxFoldInputs];
+    barrier();   // reduce-op.c:217
+    if (tgt != src && bytes <= oneshot_bytes()) {
+        for (int i = 0; i < P; ++i) ins[i] = hb[i] + soff;
+        SHMX_HIP(launch_fold(type, op, tgt, ins, P, n, s));
+        barrier();   // reduce-op.c:250
+        return SHMEMX_OK;
+    }
+    const size_t g = sz >= 16 ? 1 : 16 / sz;
+    size_t slice = (n + P - 1) / P;
+    slice = (slice + g - 1) / g * g;
+    auto lo_of = [&](int i) { return std::min(n, (size_t)i * slice); };
+    auto hi_of = [&](int i) { return std::min(n, (size_t)(i + 1) * slice); };
+    if (hi_of(m) > lo_of(m)) {
+        for (int i = 0; i < P; ++i) ins[i] = hb[i] + soff + lo_of(m) * sz;
+        SHMX_HIP(launch_fold(type, op, tgt + lo_of(m) * sz, ins, P, hi_of(m) - lo_of(m), s));
+    }
+    barrier();   // every member's slice is final
+    const void *from[kMaxFoldInputs];
+    void *to[kMaxFoldInputs];
+    size_t len[kMaxFoldInputs];
+    int k = 0;
+    for (int i = 0; i < P; ++i) {
+        if (i == m || hi_of(i) <= lo_of(i)) continue;
+        from[k] = hb[i] + toff + lo_of(i) * sz;
+        to[k] = tgt + lo_of(i) * sz;
+        len[k++] = (hi_of(i) - lo_of(i)) * sz;
+    }
+    SHMX_HIP(launch_gather(from, to, len, k, s));
+    barrier();   // reduce-op.c:250
+    return SHMEMX_OK;
+}
+
+}  // namespace shmx

@@ -6,10 +6,12 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include "node.h"
 #include "shmem_reduce_mi355x.h"
 
 #include <chrono>
 #include <mutex>
+#include <utility>
 #include <vector>
 
 namespace shmx {
@@ -100,6 +102,16 @@ char *ipc_scratch(size_t *bytes);
 // steady-clock stamp in microseconds, if >= 0) and in the barrier.
 void node_sync(int start, int step, int P, hipStream_t s, double *stream_us = nullptr,
                double *barrier_us = nullptr, double since_us = -1);
+// Map the peers' regions a collective reads (node::peer_base), voting across
+// the set the first time a combination is met; false on every member alike
+// if any member failed (direct.cpp).
+bool map_regions(const std::vector<std::pair<node::Region, int>> &regs, int start, int step, int P);
+// SIGNAL algorithm (signal.cpp): DIRECT's pulls with device-side barriers,
+// stream-ordered and graph-capturable; symmetric-heap operands only.
+int signal_reduce(int type, int op, char *tgt, const char *src, int nreduce, int start,
+                  int logstride, const shmemx_plan_t &p, hipStream_t s);
+// After the stream has drained: did a SIGNAL barrier time out?  (Clears it.)
+bool signal_timed_out();
 // DIRECT phase times since the last reset (shmemx_direct_stats).
 int direct_stats(double *out, int nout, bool reset);
 // Broadcast and [f]collect on the IPC transport (ipc_coll.cpp): members pull

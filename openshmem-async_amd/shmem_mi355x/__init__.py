@@ -24,7 +24,8 @@ LIB_PATH = os.path.join(os.path.dirname(_HERE), "libshmem_reduce_mi355x.so")
 TYPES = {"short": 0, "int": 1, "long": 2, "longlong": 3, "float": 4,
          "double": 5, "longdouble": 6, "complexd": 7, "complexf": 8}
 OPS = {"sum": 0, "prod": 1, "and": 2, "or": 3, "xor": 4, "min": 5, "max": 6}
-ALGOS = {"auto": 0, "rccl": 1, "a2a": 2, "gather": 3, "allreduce": 4, "direct": 5}
+ALGOS = {"auto": 0, "rccl": 1, "a2a": 2, "gather": 3, "allreduce": 4, "direct": 5,
+         "signal": 6}
 ERRORS = {0: "OK", 1: "EINVAL", 2: "ENOTMEMBER", 3: "ENOTSUP", 4: "ENOINIT",
           5: "ENOMEM", 6: "EDEVICE"}
 

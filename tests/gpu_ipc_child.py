@@ -52,8 +52,8 @@ def active_sets():
 def expected(t, op, srcs, st, algo):
     start, log, size = st
     ref = oracle.reduce_sim(t, op, srcs, start, log, size)
-    # DIRECT: PE_start's fold order on every member; GATHER: each PE's own
-    return ref[start] if algo in ("auto", "direct") else ref[pe]
+    # DIRECT / SIGNAL: PE_start's fold order on every member; GATHER: each PE's own
+    return ref[start] if algo in ("auto", "direct", "signal") else ref[pe]
 
 
 def read(ptr, t, n):
@@ -254,6 +254,73 @@ elif scenario == "chunk":
         run_collect(64, [100003, 30001, 0][:npes] + [7] * max(0, npes - 3), (0, 0, npes), mode, seed)
         seed += 1
         run_collect(32, [150001] * npes, (0, 0, npes), mode, seed)
+elif scenario == "signal":
+    # SIGNAL: device-side barriers, stream-ordered, heap operands only.  Every
+    # reference pair on every active set (one-shot and two-shot sizes), in
+    # place, interleaved sets, and a captured graph replayed with new inputs.
+    for (t, op) in shm.REFERENCE_PAIRS:
+        for st in active_sets():
+            for n in (1013, 70001 if t != "longdouble" else 20001):
+                seed += 1
+                run_case(t, op, n, st, "signal", "heap", seed)
+    for t, op in (("double", "sum"), ("long", "xor"), ("float", "min")):
+        for n in (4103, 300007):
+            seed += 1
+            run_case(t, op, n, (0, 0, npes), "signal", "inplace", seed)
+    for n in (0, 1, 2, 63, 65, 1 << 20):
+        seed += 1
+        run_case("double", "sum", n, (0, 0, npes), "signal", "heap", seed)
+    # a torch (non-heap) operand is refused up front, before any barrier
+    if member(0, 0, npes):
+        d = torch.zeros(64, dtype=torch.float64, device="cuda")
+        try:
+            shm.reduce_on_stream("double", "sum", d, HEAP_SRC, 64, 0, 0, npes, "signal")
+            fails.append("signal with a torch target: no error")
+        except shm.ShmemError as e:
+            if e.code != 3:
+                fails.append(f"signal with a torch target: error {e.code}, want ENOTSUP")
+    # graph capture: the barriers' counters live on the device, so replays
+    # stay in step across PEs; each replay reduces fresh inputs
+    n = 50000
+    stream = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    shm.reduce_on_stream("double", "sum", HEAP_TGT, HEAP_SRC, n, 0, 0, npes, "signal",
+                         stream.cuda_stream)          # warm: maps and votes
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=stream):
+        shm.reduce_on_stream("double", "sum", HEAP_TGT, HEAP_SRC, n, 0, 0, npes, "signal",
+                             stream.cuda_stream)
+    for rep_i in range(5):
+        seed += 1
+        srcs = oracle.sources("double", 1, npes, n, base_seed=seed)
+        shm.memcpy(HEAP_SRC, np.ascontiguousarray(srcs[pe]), n * 8)
+        torch.cuda.synchronize()
+        graph.replay()
+        torch.cuda.synchronize()
+        ncases += 1
+        want = oracle.reduce_sim("double", "sum", srcs, 0, 0, npes)[0]
+        if not same_bits(read(HEAP_TGT, "double", n), want):
+            fails.append(f"graph replay {rep_i}: wrong result")
+    del graph
+elif scenario == "signal_timeout":
+    # one SIGNAL call together (maps and votes), then PE 0 calls again alone:
+    # its device barrier must give up after $SHMEMX_SIGNAL_TIMEOUT seconds and
+    # the blocking call abort with a FATAL line, not hang the GPU
+    import time
+    shm.set_algo("signal")
+    shm.to_all("double", "sum", HEAP_TGT, HEAP_SRC, 64, 0, 0, npes)
+    torch.cuda.synchronize()
+    if pe == 0:
+        t0 = time.time()
+        print("calling alone", flush=True)
+        shm.to_all("double", "sum", HEAP_TGT, HEAP_SRC, 64, 0, 0, npes)
+        fails.append(f"returned after {time.time() - t0:.1f} s")
+    else:
+        time.sleep(8)            # keep the heap mapped while PE 0 waits
+    with open(out_path, "w") as f:
+        json.dump({"pe": pe, "fails": fails, "ncases": 1}, f)
+    os._exit(0)
 else:
     raise SystemExit(f"unknown scenario {scenario}")
 

@@ -19,7 +19,7 @@ import pytest
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def run_pes(tmp_path, npes, scenario, extra_env=None, timeout=900):
+def start_pes(tmp_path, npes, scenario, extra_env=None):
     boot = str(tmp_path / "uid")
     procs = []
     for pe in range(npes):
@@ -34,24 +34,35 @@ def run_pes(tmp_path, npes, scenario, extra_env=None, timeout=900):
         procs.append((subprocess.Popen([sys.executable, os.path.join(HERE, "gpu_ipc_child.py"), out,
                                         scenario], env=env, stdout=log, stderr=subprocess.STDOUT,
                                        start_new_session=True), out, log))
-    reports = []
+    return procs
+
+
+def wait_pes(procs, timeout):
+    """Exit codes and log texts of every PE (killing stragglers)."""
     try:
         rcs = [p.wait(timeout=timeout) for p, _, _ in procs]
-        if any(rcs):
-            tails = []
-            for (p, _, log), rc in zip(procs, rcs):
-                log.close()
-                tails.append(f"--- PE {procs.index((p, _, log))} exit {rc}:\n" + open(log.name).read()[-1500:])
-            raise AssertionError("\n".join(tails))
-        for p, out, log in procs:
-            log.close()
-            with open(out) as f:
-                reports.append(json.load(f))
     finally:
         for p, _, _ in procs:
             if p.poll() is None:
                 os.killpg(p.pid, signal.SIGKILL)
                 p.wait()
+    logs = []
+    for _, _, log in procs:
+        log.close()
+        logs.append(open(log.name).read())
+    return rcs, logs
+
+
+def run_pes(tmp_path, npes, scenario, extra_env=None, timeout=900):
+    procs = start_pes(tmp_path, npes, scenario, extra_env)
+    rcs, logs = wait_pes(procs, timeout)
+    if any(rcs):
+        raise AssertionError("\n".join(f"--- PE {pe} exit {rc}:\n" + log[-1500:]
+                                       for pe, (rc, log) in enumerate(zip(rcs, logs))))
+    reports = []
+    for _, out, _ in procs:
+        with open(out) as f:
+            reports.append(json.load(f))
     return reports
 
 
@@ -107,3 +118,28 @@ def test_isx_c_program_four_pes(tmp_path):
     for pe, (p, out) in enumerate(zip(procs, outs)):
         assert p.returncode == 0, f"PE {pe}: {out[-2000:]}"
         assert f"PE {pe} of {npes}: ISx verification passed" in out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("npes", [2, 3, 4])
+def test_ipc_signal_device_barriers(tmp_path, npes):
+    """SIGNAL: DIRECT's pulls with device-side barriers (counters in the
+    heap segments, polled across processes), stream-ordered: every reference
+    pair on every active set, one-shot and two-shot, in place, and a
+    captured hipGraph replayed with fresh inputs."""
+    reports = run_pes(tmp_path, npes, "signal")
+    for r in reports:
+        assert r["ncases"] > 0
+        assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
+
+
+@pytest.mark.gpu
+def test_ipc_signal_missing_peer_times_out(tmp_path):
+    """A peer that never reaches a SIGNAL barrier: the waiting PE's device
+    barrier gives up after $SHMEMX_SIGNAL_TIMEOUT and the blocking call aborts
+    with a FATAL line; the GPU is not left spinning."""
+    procs = start_pes(tmp_path, 2, "signal_timeout", {"SHMEMX_SIGNAL_TIMEOUT": "2"})
+    rcs, logs = wait_pes(procs, 120)
+    assert rcs[1] == 0, logs[1][-1500:]
+    assert rcs[0] != 0, logs[0][-1500:]
+    assert "never reached the device barrier" in logs[0], logs[0][-1500:]
