@@ -9,6 +9,7 @@ received shards in the order the HIP kernel uses:
   A2A    shard i of every source -> member i; fold in active-set order;
          shard all-gather              -> must equal the reference PE_start
                                           result on every member, bit for bit
+         (DIRECT and SIGNAL pull exactly these slices over xGMI instead)
   GATHER every source -> every member; fold me first, then ascending
                                        -> must equal the reference PE me
                                           result, bit for bit
@@ -46,6 +47,13 @@ CASES = [
     ("double", "sum", 0, 0, None, "a2a"),      # nreduce = 0
     ("int", "min", 1, 300, "strided", "auto"),
     ("double", "sum", 0, 300, "offset", "auto"),
+    # DIRECT / SIGNAL pull the same slices A2A exchanges (slice m of every
+    # source -> member m, fold in set order, slices gathered back)
+    ("double", "sum", 0, 4103, None, "direct"),
+    ("long", "xor", 1, 1001, "strided", "signal"),
+    ("float", "max", 1, 3, None, "signal"),      # fewer elements than PEs
+    ("int", "prod", 1, 0, None, "direct"),
+    ("longdouble", "sum", 0, 257, "offset", "signal"),
 ]
 
 
@@ -92,6 +100,14 @@ def _exchange(dist, me, sends, recvs):
     return got
 
 
+def _bits(a, t):
+    """Value bytes (long double: the 10 bytes of the x87 value, not the
+    slot's padding, which the oracle leaves unspecified as C does)."""
+    if t == "longdouble":
+        return a.view(np.uint8).reshape(len(a), -1)[:, :10].tobytes()
+    return a.tobytes()
+
+
 def _run_case(dist, shm, oracle, rank, world, case):
     t, op, kind, n, setkind, algo = case
     s = _set_for(setkind, world)
@@ -108,7 +124,7 @@ def _run_case(dist, shm, oracle, rank, world, case):
     out = np.zeros(n, dtype=dt)
     if P == 1:
         out[:] = src
-    elif p.algo == "a2a":
+    elif p.algo in ("a2a", "direct", "signal"):
         c = p.chunk
         cnt = [max(0, min(c, n - i * c)) for i in range(P)]
         lo = m * c
@@ -125,7 +141,7 @@ def _run_case(dist, shm, oracle, rank, world, case):
         for i in range(P):
             if i != m and cnt[i]:
                 out[i * c:i * c + cnt[i]] = got[members[i]].view(dt)
-        assert out.tobytes() == want[members[0]].tobytes(), case
+        assert _bits(out, t) == _bits(want[members[0]], t), case
     elif p.algo == "gather":
         sends = {members[i]: src for i in range(P) if i != m}
         recvs = {members[i]: n * dt.itemsize for i in range(P) if i != m}
