@@ -145,7 +145,9 @@ int pshmem_n_pes(void);
 /* Part 2b: the collectives next to the reductions and the symmetric heap   */
 /* (SURVEY.md §8f).  Reference prototypes: shmem.h:595-651 (barrier),       */
 /* :1654-1684 (broadcast, [f]collect), :821-941 (symmetric heap).  The heap */
-/* is HBM: shmem_malloc returns device memory, collectively.                */
+/* is HBM: shmem_malloc returns device memory, collectively.  With          */
+/* $SHMEMX_HEAP_MEMORY=host it is page-locked host memory instead, as the   */
+/* reference's heap is, so host code can dereference symmetric objects.    */
 
 #ifndef SHMEM_BCAST_SYNC_SIZE
 #define SHMEM_BCAST_SYNC_SIZE   64L

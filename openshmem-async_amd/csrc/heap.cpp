@@ -2,7 +2,9 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <cstring>
 #include <map>
+#include <string>
 
 #include "heap.h"
 #include "node.h"
@@ -27,6 +29,27 @@ struct Private {
     size_t bytes;   // what the caller asked for
 };
 
+// $SHMEMX_HEAP_MEMORY=host: the segment (and any private block) is
+// page-locked host memory instead of HBM, as the reference's heap is
+// (comms-inline.h:752-769).  Host code can then write and read symmetric
+// objects directly, as reference programs do; reductions on them take the
+// pinned host pipeline.  Peers cannot map host segments, so shmemx_heap_ptr
+// returns NULL for them (as the reference's shmem_ptr always does) and
+// DIRECT/SIGNAL are not used on them.
+bool host_kind() {
+    static const bool h = [] {
+        const char *e = std::getenv("SHMEMX_HEAP_MEMORY");
+        return e && std::string(e) == "host";
+    }();
+    return h;
+}
+
+hipError_t seg_alloc(void **p, size_t bytes) {
+    return host_kind() ? hipHostMalloc(p, bytes, hipHostMallocDefault) : hipMalloc(p, bytes);
+}
+
+hipError_t seg_free(void *p) { return host_kind() ? hipHostFree(p) : hipFree(p); }
+
 struct Heap {
     char *base = nullptr;     // the segment (nullptr until the first allocation)
     bool failed = false;      // the segment could not be allocated
@@ -45,7 +68,7 @@ bool ensure_segment() {
     bytes += kSignalBytes;
     bytes = (bytes + (uint64_t(1) << 21) - 1) & ~((uint64_t(1) << 21) - 1);   // 2 MiB pages
     void *p = nullptr;
-    if (hipMalloc(&p, bytes) != hipSuccess) {
+    if (seg_alloc(&p, bytes) != hipSuccess) {
         (void)hipGetLastError();
         g_heap.failed = true;
         trace(LOG_MEMORY, "symmetric heap segment of %llu bytes not available",
@@ -54,10 +77,15 @@ bool ensure_segment() {
     }
     g_heap.base = static_cast<char *>(p);
     g_heap.arena.reset(bytes - kSignalBytes);
-    SHMX_HIP(hipMemset(g_heap.base + (bytes - kSignalBytes), 0, kSignalBytes));
-    SHMX_HIP(hipDeviceSynchronize());
-    node::publish(node::kHeap, p, bytes);   // peers map it after the allocation's barrier
-    trace(LOG_MEMORY, "symmetric heap segment: %llu bytes of HBM at %p", (unsigned long long)bytes, p);
+    if (host_kind()) {
+        std::memset(g_heap.base + (bytes - kSignalBytes), 0, kSignalBytes);
+    } else {
+        SHMX_HIP(hipMemset(g_heap.base + (bytes - kSignalBytes), 0, kSignalBytes));
+        SHMX_HIP(hipDeviceSynchronize());
+        node::publish(node::kHeap, p, bytes);   // peers map it after the allocation's barrier
+    }
+    trace(LOG_MEMORY, "symmetric heap segment: %llu bytes of %s at %p", (unsigned long long)bytes,
+          host_kind() ? "page-locked host memory" : "HBM", p);
     return true;
 }
 
@@ -78,7 +106,7 @@ void *alloc(size_t alignment, size_t bytes) {
     // since the segment's state is the same on every PE.
     const size_t pad = alignment > 256 ? alignment : 0;
     void *base = nullptr;
-    if (hipMalloc(&base, bytes + pad) != hipSuccess) {
+    if (seg_alloc(&base, bytes + pad) != hipSuccess) {
         (void)hipGetLastError();
         return nullptr;
     }
@@ -94,7 +122,7 @@ bool free(void *p) {
     auto it = g_heap.priv.find(p);
     if (it == g_heap.priv.end()) return false;
     SHMX_HIP(hipDeviceSynchronize());
-    SHMX_HIP(hipFree(it->second.base));
+    SHMX_HIP(seg_free(it->second.base));
     g_heap.priv.erase(it);
     return true;
 }
@@ -114,17 +142,17 @@ bool offset_of(const void *p, size_t bytes, uint64_t *off) {
 }
 
 unsigned long long *signal_area() {
-    if (!ensure_segment()) return nullptr;
+    if (host_kind() || !ensure_segment()) return nullptr;
     return reinterpret_cast<unsigned long long *>(g_heap.base + g_heap.arena.capacity());
 }
 
 uint64_t signal_offset() { return g_heap.arena.capacity(); }
 
 void release_all() {
-    for (auto &kv : g_heap.priv) (void)hipFree(kv.second.base);
+    for (auto &kv : g_heap.priv) (void)seg_free(kv.second.base);
     if (g_heap.base) {
         node::unpublish(node::kHeap);
-        (void)hipFree(g_heap.base);
+        (void)seg_free(g_heap.base);
     }
     g_heap.priv.clear();
     g_heap.base = nullptr;

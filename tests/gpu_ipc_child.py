@@ -82,6 +82,16 @@ def run_case(t, op, n, st, algo, mode, seed):
         shm.to_all(t, op, tgt, src, n, *st)
         shm.set_algo("auto")
         got = tgt
+    elif mode == "hostheap":
+        # $SHMEMX_HEAP_MEMORY=host: symmetric objects the host writes directly
+        src = host_view(HEAP_SRC, mine.dtype, n)
+        tgt = host_view(HEAP_TGT, mine.dtype, n)
+        src[:] = mine
+        tgt[:] = np.zeros_like(mine)
+        shm.set_algo(algo)
+        shm.to_all(t, op, HEAP_TGT, HEAP_SRC, n, *st)
+        shm.set_algo("auto")
+        got = tgt.copy()
     elif mode == "device":
         s, d = to_dev(torch, mine), to_dev(torch, np.zeros_like(mine))
         torch.cuda.synchronize()
@@ -112,6 +122,14 @@ def run_case(t, op, n, st, algo, mode, seed):
         fails.append(f"{tag}: {len(bad)} elements differ, first at {bad[:4].tolist()}")
     if shm.last_error():
         fails.append(f"{tag}: last_error {shm.last_error()}")
+
+
+def host_view(ptr, dtype, n):
+    """A numpy array over host memory at `ptr` (the host-kind heap)."""
+    import ctypes
+    nbytes = max(1, n) * np.dtype(dtype).itemsize
+    buf = (ctypes.c_char * nbytes).from_address(ptr)
+    return np.frombuffer(buf, dtype=dtype, count=n)
 
 
 def place(arr, mode, heap_ptr):
@@ -181,13 +199,16 @@ def run_collect(bits, counts, st, mode, seed):
         fails.append(f"{kind}{bits} counts={counts} set={st} mode={mode} err={shm.last_error()}")
 
 
-CAP = 1 << 23   # bytes per heap operand
+CAP = 1 << 23 if os.environ.get("SHMEMX_HEAP_MEMORY") != "host" else 48 << 20   # bytes per heap operand
 HEAP_SRC = shm.malloc(CAP + 64)
 HEAP_TGT = shm.malloc(CAP)
 assert HEAP_SRC and HEAP_TGT, "shmem_malloc failed"
+HOST_HEAP = os.environ.get("SHMEMX_HEAP_MEMORY") == "host"
 for q in range(npes):
-    if not shm.heap_ptr(HEAP_SRC, q):
-        fails.append(f"heap_ptr(SRC, {q}) is NULL")
+    # a host-kind heap is not peer-addressable: NULL, as the reference's shmem_ptr
+    want_null = HOST_HEAP and q != pe
+    if bool(shm.heap_ptr(HEAP_SRC, q)) == want_null:
+        fails.append(f"heap_ptr(SRC, {q}) = {shm.heap_ptr(HEAP_SRC, q)}")
 
 seed = 0x1000
 if scenario == "full":
@@ -303,6 +324,23 @@ elif scenario == "signal":
         if not same_bits(read(HEAP_TGT, "double", n), want):
             fails.append(f"graph replay {rep_i}: wrong result")
     del graph
+elif scenario == "hostheap":
+    # $SHMEMX_HEAP_MEMORY=host: shmem_malloc returns page-locked host memory,
+    # as the reference's heap is; the host writes the symmetric objects and
+    # the blocking calls stage them through the pinned pipeline
+    assert HOST_HEAP
+    for (t, op) in shm.REFERENCE_PAIRS:
+        for st in active_sets():
+            seed += 1
+            run_case(t, op, 1013, st, "auto", "hostheap", seed)
+    for n in (1, 65, (40 << 20) // 8 + 3):
+        seed += 1
+        run_case("double", "sum", n, (0, 0, npes), "auto", "hostheap", seed)
+    for st in active_sets():
+        seed += 1
+        run_bcast(64, 1031, 0, st, "heap", seed)
+        seed += 1
+        run_collect(32, [(37 * (q + 1)) % 101 for q in range(npes)], st, "heap", seed)
 elif scenario == "signal_timeout":
     # one SIGNAL call together (maps and votes), then PE 0 calls again alone:
     # its device barrier must give up after $SHMEMX_SIGNAL_TIMEOUT seconds and

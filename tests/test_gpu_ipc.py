@@ -143,3 +143,17 @@ def test_ipc_signal_missing_peer_times_out(tmp_path):
     assert rcs[1] == 0, logs[1][-1500:]
     assert rcs[0] != 0, logs[0][-1500:]
     assert "never reached the device barrier" in logs[0], logs[0][-1500:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("npes", [1, 3])
+def test_ipc_host_kind_heap(tmp_path, npes):
+    """$SHMEMX_HEAP_MEMORY=host: shmem_malloc returns page-locked host memory,
+    as the reference's symmetric heap is (comms-inline.h:752-769), so host code
+    writes symmetric objects directly; every reference pair on every active
+    set, 40 MiB arrays across staging chunks, broadcast and collect, against
+    the oracle; peers' heap_ptr is NULL."""
+    reports = run_pes(tmp_path, npes, "hostheap", {"SHMEMX_HEAP_MEMORY": "host"})
+    for r in reports:
+        assert r["ncases"] > 0
+        assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
