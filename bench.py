@@ -190,28 +190,35 @@ def latency_extras(world, barrier, max_over_ranks):
                 shm.to_all("longlong", "sum", tgt, src, n, 0, 0, world, None, psync)
             t = max_over_ranks((time.perf_counter() - t0) / reps)
             out[f"longlong_sum_n{n}_{where}_us"] = round(t * 1e6, 1)
-    if world > 1:
-        # symmetric-heap operands: DIRECT (host barriers) and SIGNAL (device
-        # barriers), each call waited for, as a blocking call would be
-        hs, ht = malloc_pair(4096 * 8)
-        if hs and ht:
-            try:
-                for algo in ("direct", "signal"):
-                    for n in (1, 64, 4096):
-                        def call():
-                            shm.reduce_on_stream("longlong", "sum", ht, hs, n, 0, 0, world, algo)
-                            torch.cuda.synchronize()
-                        for _ in range(5):
-                            call()
-                        barrier()
-                        reps = 200
-                        t0 = time.perf_counter()
-                        for _ in range(reps):
-                            call()
-                        t = max_over_ranks((time.perf_counter() - t0) / reps)
-                        out[f"longlong_sum_n{n}_heap_{algo}_us"] = round(t * 1e6, 1)
-            except shm.ShmemError as e:
-                out["heap_latency"] = str(e)
+    return out
+
+
+def heap_latency_extras(world, barrier, max_over_ranks):
+    """Small-message latency with symmetric-heap operands (N > 1): DIRECT
+    (host barriers) and SIGNAL (device barriers), each call waited for, as a
+    blocking call would be; microseconds per call (max over ranks)."""
+    out = {}
+    hs, ht = malloc_pair(4096 * 8)
+    try:
+        if not (hs and ht):
+            return "shmem_malloc failed"
+        for algo in ("direct", "signal"):
+            for n in (1, 64, 4096):
+                def call():
+                    shm.reduce_on_stream("longlong", "sum", ht, hs, n, 0, 0, world, algo)
+                    torch.cuda.synchronize()
+                for _ in range(5):
+                    call()
+                barrier()
+                reps = 200
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    call()
+                t = max_over_ranks((time.perf_counter() - t0) / reps)
+                out[f"longlong_sum_n{n}_heap_{algo}_us"] = round(t * 1e6, 1)
+    except shm.ShmemError as e:
+        out["error"] = str(e)
+    finally:
         if ht:
             shm.free(ht)
         if hs:
@@ -459,15 +466,28 @@ def main():
         "roofline": roofline, "cpu_baseline": cpu, "correct": ok, "extras": extras,
     }
     emitted = threading.Lock()
+    exit_code = 0 if ok else 1
 
     def emit(note=None):
         """Print the one JSON line (rank 0), at most once."""
         if not emitted.acquire(blocking=False):
             return
+        shm.set_fatal_note(None)       # the line is printed here, not by the handler
         if note:
             line["extras"] = dict(extras, note=note)
         if rank == 0:
             print(json.dumps(line), flush=True)
+
+    def arm_fatal_note(running):
+        """If this process dies on a fatal signal while `running` (a FATAL
+        abort in an RCCL/HIP call, a GPU fault, the launcher's SIGTERM after
+        another rank died), rank 0 still prints the measured line, with the
+        extras finished so far."""
+        text = ""
+        if rank == 0:
+            text = json.dumps(dict(line, extras=dict(
+                extras, note=f"extras stopped by a fatal signal during {running}"))) + "\n"
+        shm.set_fatal_note(text, exit_code)
 
     # The headline is measured and checked by now.  The extras below exercise
     # other algorithms and API forms; a hang among them must not cost the
@@ -481,6 +501,7 @@ def main():
     timer.start()
 
     def guarded(name, fn):
+        arm_fatal_note(name)
         try:
             extras[name] = fn()
         except Exception as e:   # noqa: BLE001 — an extra never costs the headline
@@ -521,12 +542,14 @@ def main():
                 except shm.ShmemError as e:
                     return str(e)
             guarded(f"algo_{alt}_GiBps", alt_rate)
+        guarded("configs", lambda: config_extras(world, stream, barrier, max_over_ranks))
+        guarded("latency", lambda: latency_extras(world, barrier, max_over_ranks))
+        # last: the kernels that load from the peers' HBM through IPC mappings
         guarded("direct_heap", lambda: direct_extra(world, n, src, sp, stream, barrier,
                                                     max_over_ranks, max(3, a.steps // 4)))
         guarded("signal_heap", lambda: direct_extra(world, n, src, sp, stream, barrier,
                                                     max_over_ranks, max(3, a.steps // 4), "signal"))
-        guarded("configs", lambda: config_extras(world, stream, barrier, max_over_ranks))
-        guarded("latency", lambda: latency_extras(world, barrier, max_over_ranks))
+        guarded("heap_latency", lambda: heap_latency_extras(world, barrier, max_over_ranks))
 
     timer.cancel()
     emit()

@@ -342,6 +342,15 @@ int shmemx_verify(int type, const void *target, int nreduce, int PE_start,
 int shmemx_reduce_last_error(void);
 const char *shmemx_reduce_error_string(int err);
 
+/* Last words.  FATAL conditions abort the process, as the reference's
+ * SHMEM_LOG_FATAL exits it (trace.c:424-427); so do GPU memory faults (HSA)
+ * and a launcher's SIGTERM when another PE died.  A caller holding a result
+ * it must not lose registers it here: on SIGABRT, SIGSEGV, SIGBUS, SIGFPE,
+ * SIGILL or SIGTERM the text is written to stdout and the process leaves with
+ * _exit(exit_code).  Calling again replaces the text; NULL uninstalls and
+ * restores the previous handlers.  SHMEMX_OK or SHMEMX_ENOMEM. */
+int shmemx_set_fatal_note(const char *text, int exit_code);
+
 /* Typed stream-ordered forms of the 44 entry points. */
 #define SHMEMX_DECL_REDUCE_STREAM(Name, Op, T)                                 \
     void shmemx_##Name##_##Op##_to_all_on_stream(                            \

@@ -130,6 +130,8 @@ def lib() -> ctypes.CDLL:
     L.shmemx_host_register.restype = i
     L.shmemx_host_unregister.argtypes = [vp]
     L.shmemx_host_unregister.restype = i
+    L.shmemx_set_fatal_note.argtypes = [ctypes.c_char_p, i]
+    L.shmemx_set_fatal_note.restype = i
     for t, o in REFERENCE_PAIRS:
         for prefix in ("shmem", "pshmem"):
             f = getattr(L, f"{prefix}_{t}_{o}_to_all")
@@ -342,6 +344,14 @@ def host_register(buf, nbytes: int) -> None:
 
 def host_unregister(buf) -> None:
     _check(lib().shmemx_host_unregister(addr(buf)), "shmemx_host_unregister")
+
+
+def set_fatal_note(text: str | None, exit_code: int = 1) -> None:
+    """shmemx_set_fatal_note: text written to stdout (then _exit(exit_code))
+    if the process dies on SIGABRT/SIGSEGV/SIGBUS/SIGFPE/SIGILL/SIGTERM; None
+    uninstalls."""
+    raw = None if text is None else text.encode()
+    _check(lib().shmemx_set_fatal_note(raw, exit_code), "shmemx_set_fatal_note")
 
 
 _hip = None
