@@ -289,6 +289,41 @@ def direct_extra(world, n, src, sp, stream, barrier, max_over_ranks, steps, algo
             shm.free(hs)
 
 
+def crossover_extra(world, sp, stream, barrier, max_over_ranks):
+    """double sum over the full set, per algorithm and size, with source and
+    target in the symmetric heap (so DIRECT and SIGNAL can run too): GiB/s of
+    the whole job (N * n * 8 B / max-over-ranks time).  The data `auto`'s
+    per-size choice between RCCL and the IPC pulls is to be set from."""
+    sizes = [1 << 12, 1 << 16, 1 << 20, 1 << 24]
+    nbytes = sizes[-1] * 8
+    hs, ht = malloc_pair(nbytes)
+    out = {}
+    try:
+        if not (hs and ht):
+            return "shmem_malloc failed"
+        for algo in ("rccl", "allreduce", "a2a", "direct", "signal"):
+            row = {}
+            for n in sizes:
+                def step(n=n, algo=algo):
+                    shm.reduce_on_stream("double", "sum", ht, hs, n, 0, 0, world, algo, sp)
+                try:
+                    for _ in range(3):
+                        step()
+                    k = 20 if n <= 1 << 20 else 10
+                    w, _ = time_region(step, k, stream, barrier)
+                    w = max_over_ranks(w)
+                    row[str(n)] = round(world * n * 8 * k / w / GiB, 2)
+                except shm.ShmemError as e:
+                    row[str(n)] = str(e)
+            out[algo] = row
+    finally:
+        if ht:
+            shm.free(ht)
+        if hs:
+            shm.free(hs)
+    return out
+
+
 def time_region(fn, steps, stream, barrier):
     """Run fn() `steps` times on `stream`; returns (wall_s, event_s)."""
     barrier()
@@ -550,6 +585,8 @@ def main():
         guarded("signal_heap", lambda: direct_extra(world, n, src, sp, stream, barrier,
                                                     max_over_ranks, max(3, a.steps // 4), "signal"))
         guarded("heap_latency", lambda: heap_latency_extras(world, barrier, max_over_ranks))
+        guarded("algo_crossover_GiBps", lambda: crossover_extra(world, sp, stream, barrier,
+                                                                max_over_ranks))
 
     timer.cancel()
     emit()
