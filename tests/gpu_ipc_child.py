@@ -341,6 +341,52 @@ elif scenario == "hostheap":
         run_bcast(64, 1031, 0, st, "heap", seed)
         seed += 1
         run_collect(32, [(37 * (q + 1)) % 101 for q in range(npes)], st, "heap", seed)
+elif scenario == "configs":
+    # BASELINE.json configs at full size through the blocking drop-in entry
+    # points, every PE a process: long and/or/xor over 64 Mi elements
+    # (configs[3]) and double sum over 32 Mi (configs[2]).  Every PE
+    # regenerates all P sources on the GPU and folds them with torch in the
+    # reference's PE_start order; the result must match bit for bit, and the
+    # checksums of all PEs' targets must agree (shmemx_verify).
+    big = 64 * 1024 * 1024 * 8
+    BIG_SRC, BIG_TGT = shm.malloc(big), shm.malloc(big)
+    assert BIG_SRC and BIG_TGT, "shmem_malloc of the config operands failed"
+
+    def gen(t, q, n, salt):
+        g = torch.Generator(device="cuda")
+        g.manual_seed(0xC0F1C + 97 * q + salt)
+        if t == "long":
+            return torch.randint(-2**63, 2**63 - 1, (n,), dtype=torch.int64, device="cuda", generator=g)
+        return torch.rand(n, dtype=torch.float64, device="cuda", generator=g) + 1.0
+
+    cases = [("long", op, 64 * 1024 * 1024) for op in ("and", "or", "xor")]
+    cases += [("double", "sum", 32 * 1024 * 1024)]
+    for salt, (t, op, n) in enumerate(cases):
+        ncases += 1
+        print(f"config {t} {op} n={n}", flush=True)
+        shm.memcpy(BIG_SRC, gen(t, pe, n, salt), n * 8)
+        shm.memcpy(BIG_TGT, torch.zeros(n, dtype=torch.int64, device="cuda"), n * 8)
+        torch.cuda.synchronize()
+        shm.to_all(t, op, BIG_TGT, BIG_SRC, n, 0, 0, npes)
+        if shm.last_error():
+            fails.append(f"config {t} {op}: last_error {shm.last_error()}")
+            continue
+        got = torch.empty(n, dtype=torch.int64 if t == "long" else torch.float64, device="cuda")
+        shm.memcpy(got, BIG_TGT, n * 8)
+        f = {"and": torch.bitwise_and, "or": torch.bitwise_or, "xor": torch.bitwise_xor,
+             "sum": torch.add}[op]
+        want = gen(t, 0, n, salt)
+        for q in range(1, npes):
+            want = f(want, gen(t, q, n, salt))
+        torch.cuda.synchronize()
+        if not torch.equal(got.view(torch.int64), want.view(torch.int64)):
+            bad = int((got.view(torch.int64) != want.view(torch.int64)).sum())
+            fails.append(f"config {t} {op} n={n}: {bad} elements differ")
+        if not shm.verify(t, BIG_TGT, n, 0, 0, npes):
+            fails.append(f"config {t} {op} n={n}: targets differ across PEs")
+        del got, want
+    shm.free(BIG_TGT)
+    shm.free(BIG_SRC)
 elif scenario == "signal_timeout":
     # one SIGNAL call together (maps and votes), then PE 0 calls again alone:
     # its device barrier must give up after $SHMEMX_SIGNAL_TIMEOUT seconds and

@@ -81,6 +81,18 @@ def test_ipc_transport_all_pairs_sets_placements(tmp_path, npes, shots):
 
 
 @pytest.mark.gpu
+def test_ipc_baseline_configs_full_size(tmp_path):
+    """BASELINE.json configs[3] (long and/or/xor, 64 Mi, 4 PEs) and configs[2]'s
+    double sum over 32 Mi, as 4 PE processes through the blocking drop-in
+    entry points: bit-exact against torch's fold of all regenerated sources in
+    PE_start order, and identical on every PE."""
+    reports = run_pes(tmp_path, 4, "configs", timeout=600)
+    for r in reports:
+        assert r["ncases"] == 4
+        assert not r["fails"], f"PE {r['pe']}: {r['fails']}"
+
+
+@pytest.mark.gpu
 def test_ipc_direct_staged_in_chunks(tmp_path):
     # a 1 MiB scratch: every staged operand crosses several chunks per call
     reports = run_pes(tmp_path, 3, "chunk", {"SHMEMX_DIRECT_SCRATCH_MB": "1"})
