@@ -312,6 +312,14 @@ static ncclRedOp_t rccl_op(int op) {
     }
 }
 
+// Up to this many bytes, AUTO takes one RCCL all-reduce for the RCCL-native
+// pairs on the full set ($SHMEMX_ALLREDUCE_MAX_KB, default 4 MiB); above it,
+// the reduce-scatter + all-gather form.
+static long long allreduce_max_bytes() {
+    static const long long b = (long long)env_int("SHMEMX_ALLREDUCE_MAX_KB", nullptr, 4096) << 10;
+    return b;
+}
+
 static int make_plan(int type, int op, int nreduce, int start, int logstride,
                      int size, int pe, int npes, int algo, shmemx_plan_t *p) {
     std::memset(p, 0, sizeof *p);
@@ -332,7 +340,11 @@ static int make_plan(int type, int op, int nreduce, int start, int logstride,
     const bool world = start == 0 && (logstride == 0 || size == 1) && size == npes;
     if (algo == SHMEMX_ALGO_AUTO) {
         if (g_state.ipc_only) algo = SHMEMX_ALGO_DIRECT;
-        else algo = (world && rccl_native(type, op)) ? SHMEMX_ALGO_RCCL : SHMEMX_ALGO_A2A;
+        else if (!(world && rccl_native(type, op))) algo = SHMEMX_ALGO_A2A;
+        // Small arrays are latency-bound: one RCCL all-reduce (one launch,
+        // and RCCL's own small-message all-reduce algorithms) instead of
+        // reduce-scatter + all-gather (+ a tail all-reduce).
+        else algo = n * sz <= allreduce_max_bytes() ? SHMEMX_ALGO_ALLREDUCE : SHMEMX_ALGO_RCCL;
     }
     if ((algo == SHMEMX_ALGO_RCCL || algo == SHMEMX_ALGO_ALLREDUCE) &&
         !(world && rccl_native(type, op)))

@@ -107,10 +107,13 @@ def test_header_compiles_as_cpp(tmp_path):
 # ------------------------------------------------------------------- plans
 def test_plan_algorithm_selection(shm):
     P = shm.plan
-    # full set, RCCL-native pairs -> RCCL
+    # full set, RCCL-native pairs -> RCCL reduce-scatter + all-gather; up to
+    # 4 MiB ($SHMEMX_ALLREDUCE_MAX_KB) one RCCL all-reduce
     assert P("double", "sum", 1 << 25, 0, 0, 8, 3, 8).algo == "rccl"
-    assert P("long", "max", 1000, 0, 0, 4, 0, 4).algo == "rccl"
-    assert P("int", "prod", 1000, 0, 0, 2, 1, 2).algo == "rccl"
+    assert P("double", "sum", (4 << 20) // 8 + 1, 0, 0, 8, 3, 8).algo == "rccl"
+    assert P("double", "sum", (4 << 20) // 8, 0, 0, 8, 3, 8).algo == "allreduce"
+    assert P("long", "max", 1000, 0, 0, 4, 0, 4).algo == "allreduce"
+    assert P("int", "prod", 1000, 0, 0, 2, 1, 2).algo == "allreduce"
     # bitwise (no RCCL op), float min/max (NaN semantics), short (no RCCL type),
     # complex -> A2A
     for t, o in [("long", "xor"), ("int", "and"), ("double", "min"), ("float", "max"),

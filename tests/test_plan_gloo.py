@@ -37,6 +37,9 @@ CASES = [
     ("double", "sum", 0, 4103, None, "gather"),
     ("double", "sum", 0, 4103, None, "rccl"),
     ("int", "sum", 1, 4103, None, "rccl"),
+    ("double", "sum", 0, 4103, None, "auto"),    # small: one all-reduce
+    ("long", "max", 1, 1001, None, "allreduce"),
+    ("float", "prod", 0, 0, None, "allreduce"),
     ("long", "xor", 1, 777, None, "auto"),
     ("long", "and", 1, 65, None, "a2a"),
     ("short", "max", 1, 130, None, "auto"),
@@ -150,6 +153,17 @@ def _run_case(dist, shm, oracle, rank, world, case):
             if n else np.zeros((P, 0), dt)
         out = oracle.reduce_sim(t, op, full, 0, 0, P)[m]
         assert out.tobytes() == want[rank].tobytes(), case
+    elif p.algo == "allreduce":
+        # one all-reduce: every member gets the whole reduction, in RCCL's
+        # order (here: descending member order, unlike the reference's)
+        assert p.chunk == n and p.main == n and p.tail == 0
+        sends = {members[i]: src for i in range(P) if i != m}
+        recvs = {members[i]: n * dt.itemsize for i in range(P) if i != m}
+        got = _exchange(dist, rank, sends, recvs) if n else {}
+        full = np.stack([src if i == m else got[members[i]].view(dt) for i in range(P)][::-1]) \
+            if n else np.zeros((P, 0), dt)
+        out = oracle.reduce_sim(t, op, full, 0, 0, P)[0]
+        _check_rccl(out, want[rank], srcs[members], dt, case)
     else:  # rccl: reduce-scatter main part, all-gather, all-reduce tail
         c, main = p.chunk, p.main
         assert main + p.tail == n
@@ -172,13 +186,18 @@ def _run_case(dist, shm, oracle, rank, world, case):
             tails = np.stack([src[main:] if i == m else got[members[i]].view(dt)
                               for i in range(P)])
             out[main:] = oracle.reduce_sim(t, op, tails, 0, 0, P)[0]
-        if dt.kind in "iu":
-            assert out.tobytes() == want[rank].tobytes(), case
-        else:
-            # any summation order: |d| <= 2 (P-1) u sum|x| (BASELINE/SURVEY §8d)
-            u = np.finfo(dt).eps / 2
-            bound = 2 * (P - 1) * u * np.abs(srcs[members]).sum(axis=0)
-            assert (np.abs(out - want[rank]) <= bound).all(), case
+        _check_rccl(out, want[rank], srcs[members], dt, case)
+
+
+def _check_rccl(out, want, member_srcs, dt, case):
+    if dt.kind in "iu":
+        assert out.tobytes() == want.tobytes(), case
+    else:
+        # any summation order: |d| <= 2 (P-1) u sum|x| (BASELINE/SURVEY §8d)
+        P = len(member_srcs)
+        u = np.finfo(dt).eps / 2
+        bound = 2 * (P - 1) * u * np.abs(member_srcs).sum(axis=0)
+        assert (np.abs(out - want) <= bound).all(), case
 
 
 def _worker(rank, world, port, q):
