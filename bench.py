@@ -494,7 +494,9 @@ def main():
         "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": workload, "nreduce": n, "type": "double", "op": "sum",
-                   "PE_size": world, "algo": algo_used,
+                   "PE_size": world,
+                   "algo": algo_used if world == 1 else
+                   shm.plan("double", "sum", n, 0, 0, world, rank, world, algo_used).algo,
                    "parallelism": f"one PE per GPU x{world}",
                    "transport": os.environ.get("SHMEMX_TRANSPORT", "rccl"),
                    "arrays": "symmetric heap (shmem_malloc, HBM)" if use_heap else "hipMalloc (torch)"},
