@@ -17,6 +17,7 @@ void reduce_blocking(int type, int op, void *target, const void *source,
 int reduce_on_stream(int type, int op, void *target, const void *source,
                      int nreduce, int start, int logstride, int size, int algo,
                      void *stream);
+void debug_checks(const char *name, const void *target, const void *source);
 }  // namespace shmx
 
 #define SHMX_ENTRY(Name, Op, T, TYPE, OPC)                                     \
@@ -26,6 +27,7 @@ int reduce_on_stream(int type, int op, void *target, const void *source,
     {                                                                        \
         (void)pWrk;                                                          \
         (void)pSync;                                                         \
+        shmx::debug_checks("shmem_" #Name "_" #Op "_to_all", target, source); \
         shmx::reduce_blocking(TYPE, OPC, target, source, nreduce, PE_start,  \
                               logPE_stride, PE_size);                        \
     }                                                                        \

@@ -1,10 +1,12 @@
 // The symmetric heap on HBM (heap.h): one segment per PE, exported over IPC.
 #include <hip/hip_runtime.h>
+#include <link.h>
 
 #include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
+#include <vector>
 
 #include "heap.h"
 #include "node.h"
@@ -139,6 +141,47 @@ bool offset_of(const void *p, size_t bytes, uint64_t *off) {
     if (bytes > g_heap.arena.capacity() - o) return false;
     *off = o;
     return true;
+}
+
+namespace {
+
+struct Range {
+    uintptr_t lo, hi;
+};
+
+// Writable PT_LOAD segments of the main program (.data and .bss): the first
+// object dl_iterate_phdr reports.
+int collect_main_data(struct dl_phdr_info *info, size_t, void *arg) {
+    auto *out = static_cast<std::vector<Range> *>(arg);
+    for (int i = 0; i < info->dlpi_phnum; ++i) {
+        const ElfW(Phdr) &ph = info->dlpi_phdr[i];
+        if (ph.p_type == PT_LOAD && (ph.p_flags & PF_W))
+            out->push_back({info->dlpi_addr + ph.p_vaddr, info->dlpi_addr + ph.p_vaddr + ph.p_memsz});
+    }
+    return 1;   // the main program only
+}
+
+const std::vector<Range> &main_data() {
+    static const std::vector<Range> r = [] {
+        std::vector<Range> v;
+        dl_iterate_phdr(collect_main_data, &v);
+        return v;
+    }();
+    return r;
+}
+
+}  // namespace
+
+bool is_symmetric(const void *p) {
+    if (in_segment(p)) return true;
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    for (const auto &kv : g_heap.priv) {
+        const uintptr_t b = reinterpret_cast<uintptr_t>(kv.first);
+        if (a >= b && a < b + kv.second.bytes) return true;
+    }
+    for (const Range &r : main_data())
+        if (a >= r.lo && a < r.hi) return true;
+    return false;
 }
 
 unsigned long long *signal_area() {

@@ -55,6 +55,11 @@ bool free(void *p);
 size_t size_of(const void *p);                  // 0 if not a heap block
 // Offset of [p, p + bytes) inside this PE's segment; false if not inside it.
 bool offset_of(const void *p, size_t bytes, uint64_t *off);
+// The reference's symmetric-address test (shmemi_symmetric_addr_lookup,
+// comms-inline.h:519-545): p lies in the heap segment or a private heap
+// block, or in the executable's writable data/bss — the global and static
+// variables the reference makes symmetric (globalvar/globalvar.c:99-369).
+bool is_symmetric(const void *p);
 // The library's signal area at the top of the segment (outside the arena):
 // 64 KiB, zero at creation, at signal_offset() from the segment base on every
 // PE.  nullptr if there is no segment.

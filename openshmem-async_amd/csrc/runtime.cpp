@@ -934,6 +934,21 @@ void reduce_blocking(int type, int op, void *target, const void *source,
     SHMX_HIP(hipStreamSynchronize(g_state.d2h));
 }
 
+// $SHMEMX_DEBUG=1: the checks the reference's wrappers make when configured
+// with --enable-debug (reduce-op.c:379-381, utils.h:64-116): target and
+// source must be symmetric (heap, or the program's globals), else FATAL.
+void debug_checks(const char *name, const void *target, const void *source) {
+    static const bool on = env_int("SHMEMX_DEBUG", nullptr, 0) != 0;
+    if (!on) return;
+    std::lock_guard<std::recursive_mutex> lk(g_mu);   // the heap's block table
+    const void *args[2] = {target, source};
+    for (int i = 0; i < 2; ++i) {
+        if (heap::is_symmetric(args[i])) continue;
+        trace(LOG_FATAL, "%s(), argument #%d @ %p is not symmetric", name, i + 1, args[i]);
+        std::abort();
+    }
+}
+
 int reduce_on_stream(int type, int op, void *target, const void *source,
                      int nreduce, int start, int logstride, int size, int algo,
                      void *stream) {

@@ -241,6 +241,38 @@ def test_c_program_isx_verification(cuda, tmp_path):
     assert "ISx verification passed" in out.stdout
 
 
+def test_debug_symmetry_check(cuda, tmp_path):
+    """$SHMEMX_DEBUG=1 makes the wrappers' --enable-debug checks live
+    (reduce-op.c:379-381, utils.h:98-116): the C program's static arrays (the
+    reference's symmetric globals) and shmem_malloc blocks pass; a torch
+    tensor as target or source is FATAL with the reference's message."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    libdir = os.path.join(repo, "openshmem-async_amd")
+    exe = tmp_path / "isx_verify"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(repo, "include"),
+                    os.path.join(repo, "examples", "isx_verify.c"), "-L", libdir,
+                    "-lshmem_reduce_mi355x", f"-Wl,-rpath,{libdir}", "-o", str(exe)], check=True)
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env["SHMEMX_DEBUG"] = "1"
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120, env=env)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "ISx verification passed" in out.stdout
+    for args, pos in (("t, a", 1), ("b + 8, t", 2)):
+        code = (f"import sys, torch; sys.path.insert(0, {libdir!r}); import shmem_mi355x as s; "
+                "s.init(); a = s.malloc(8 * 64); b = s.malloc(8 * 64); "
+                "s.to_all('double', 'sum', b, a, 64, 0, 0, 1); print('heap ok', flush=True); "
+                "t = torch.zeros(64, dtype=torch.float64, device='cuda'); "
+                f"s.to_all('double', 'sum', {args}, 63, 0, 0, 1)")
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                           timeout=120)
+        assert "heap ok" in r.stdout, r.stderr[-2000:]
+        assert r.returncode != 0
+        assert f"FATAL: shmem_double_sum_to_all(), argument #{pos} @ " in r.stderr, r.stderr[-2000:]
+        assert "is not symmetric" in r.stderr
+
+
 @pytest.mark.parametrize("n", [1, 7, 4096, 32768])
 def test_host_small_messages_bounce_path(cuda, shm, oracle, n):
     """Host arrays up to 256 KiB take the page-locked bounce path; mixed
