@@ -482,6 +482,9 @@ def main():
                     "alg_bytes_per_launch": int(xgmi_bytes),
                     "avg_launch_us": round(t_call * 1e6, 2),
                     "busbw_GBps": round(achieved, 1),
+                    "peak_basis": "bytes each GPU sends (= receives), RS + AG, over its N-1 "
+                                  "direct links at 153 GB/s per link per direction (the task's "
+                                  "figure; if 153 GB/s is the two-way link rate, frac doubles)",
                     "algbw_GiBps": round(nbytes / t_call / GiB, 2)}
 
     cpu = None
