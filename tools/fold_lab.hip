@@ -118,6 +118,40 @@ __global__ __launch_bounds__(B) void v_persist(f64x2 *acc, const f64x2 *in, size
     }
 }
 
+// V4: persistent and software-pipelined: chunk k+1's loads are issued before
+// chunk k's stores, so every wave writes one chunk while reading the next
+// (the in-place fold otherwise reads and writes the same lines back to back).
+// The lab arrays are a whole number of chunks per block (32 Mi doubles).
+template <int B, int U, int NT>
+__global__ __launch_bounds__(B) void v_pipe(f64x2 *acc, const f64x2 *in, size_t nvec) {
+    const size_t step = (size_t)gridDim.x * B * U;
+    size_t base = (size_t)blockIdx.x * B * U;
+    if (base + (size_t)B * U > nvec) return;
+    f64x2 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) a[u] = ld<NT>(acc + base + threadIdx.x + u * B);
+#pragma unroll
+    for (int u = 0; u < U; ++u) b[u] = ld<NT>(in + base + threadIdx.x + u * B);
+    for (;;) {
+        const bool more = base + step + (size_t)B * U <= nvec;
+        const size_t nb = more ? base + step : base;     // unconditional loads: counted waits
+        f64x2 a2[U], b2[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) a2[u] = ld<NT>(acc + nb + threadIdx.x + u * B);
+#pragma unroll
+        for (int u = 0; u < U; ++u) b2[u] = ld<NT>(in + nb + threadIdx.x + u * B);
+#pragma unroll
+        for (int u = 0; u < U; ++u) st<NT>(acc + base + threadIdx.x + u * B, a[u] + b[u]);
+        if (!more) break;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            a[u] = a2[u];
+            b[u] = b2[u];
+        }
+        base = nb;
+    }
+}
+
 struct Variant {
     const char *name;
     void (*launch)(f64x2 *, const f64x2 *, size_t, hipStream_t);
@@ -138,6 +172,11 @@ void L_xcd(f64x2 *a, const f64x2 *b, size_t nv, hipStream_t s) {
 template <int B, int U, int NT, int G>
 void L_persist(f64x2 *a, const f64x2 *b, size_t nv, hipStream_t s) {
     hipLaunchKernelGGL((v_persist<B, U, NT>), dim3(G), dim3(B), 0, s, a, b, nv);
+}
+
+template <int B, int U, int NT, int G>
+void L_pipe(f64x2 *a, const f64x2 *b, size_t nv, hipStream_t s) {
+    hipLaunchKernelGGL((v_pipe<B, U, NT>), dim3(G), dim3(B), 0, s, a, b, nv);
 }
 
 // Mode "offsets": does the distance between acc and in matter (channel /
@@ -262,6 +301,15 @@ int main(int argc, char **argv) {
         {"persist_b1024_u2_nt3_g512", L_persist<1024, 2, 3, 512>},
         {"strided_b256_u4_nt1", L_strided<256, 4, 1>},
         {"strided_b256_u4_nt2", L_strided<256, 4, 2>},
+        {"pipe_b256_u4_nt3_g1024", L_pipe<256, 4, 3, 1024>},
+        {"pipe_b256_u4_nt3_g2048", L_pipe<256, 4, 3, 2048>},
+        {"pipe_b256_u4_nt3_g4096", L_pipe<256, 4, 3, 4096>},
+        {"pipe_b256_u2_nt3_g2048", L_pipe<256, 2, 3, 2048>},
+        {"pipe_b256_u2_nt3_g4096", L_pipe<256, 2, 3, 4096>},
+        {"pipe_b512_u2_nt3_g2048", L_pipe<512, 2, 3, 2048>},
+        {"pipe_b256_u4_nt1_g2048", L_pipe<256, 4, 1, 2048>},
+        {"pipe_b256_u2_nt3_g8192", L_pipe<256, 2, 3, 8192>},
+        {"strided_b256_u4_nt3_again", L_strided<256, 4, 3>},
     };
     const int K = cold ? 1 : 20, R = 7;
     std::vector<std::vector<float>> t(vs.size());
