@@ -28,6 +28,8 @@ def _ensure_built():
         subprocess.run(["make", "-j8", "-C", os.path.join(REPO, "openshmem-async_amd")], check=True)
     if not os.path.exists(os.path.join(REPO, "oracle", "liboracle_reduce.so")):
         subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
+    if not os.path.exists(os.path.join(REPO, "tests", "native", "libfake_rccl.so")):
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "tests", "native")], check=True)
 
 
 _ensure_built()

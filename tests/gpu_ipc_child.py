@@ -28,6 +28,11 @@ from gpu_util import same_bits, to_dev  # noqa: E402
 
 out_path, scenario = sys.argv[1], sys.argv[2]
 pe, npes = int(os.environ["SHMEM_PE"]), int(os.environ["SHMEM_NPES"])
+if os.environ.get("FAKE_RCCL"):
+    # the RCCL test double (tests/native/fake_rccl.cpp), global before the
+    # library loads, so its nccl* calls bind there and PEs may share the GPU
+    import ctypes
+    ctypes.CDLL(os.environ["FAKE_RCCL"], mode=ctypes.RTLD_GLOBAL)
 torch.cuda.set_device(0)
 shm.init()
 assert shm.my_pe() == pe and shm.n_pes() == npes
@@ -52,8 +57,10 @@ def active_sets():
 def expected(t, op, srcs, st, algo):
     start, log, size = st
     ref = oracle.reduce_sim(t, op, srcs, start, log, size)
-    # DIRECT / SIGNAL: PE_start's fold order on every member; GATHER: each PE's own
-    return ref[start] if algo in ("auto", "direct", "signal") else ref[pe]
+    # DIRECT / SIGNAL / A2A: PE_start's fold order on every member; GATHER: each
+    # PE's own.  RCCL / ALLREDUCE under the RCCL test double: it reduces in rank
+    # order, which for the full set is PE_start's order too.
+    return ref[start] if algo != "gather" else ref[pe]
 
 
 def read(ptr, t, n):
@@ -341,6 +348,61 @@ elif scenario == "hostheap":
         run_bcast(64, 1031, 0, st, "heap", seed)
         seed += 1
         run_collect(32, [(37 * (q + 1)) % 101 for q in range(npes)], st, "heap", seed)
+elif scenario == "rccl":
+    # The default RCCL transport, with the RCCL test double standing in for
+    # librccl ($FAKE_RCCL): the library's own RCCL call sequences — reduce-
+    # scatter + all-gather with the all-reduce tail, one all-reduce, A2A and
+    # GATHER over grouped send/recv, broadcast / [f]collect / barrier /
+    # verify over RCCL — across real processes and device pointers.
+    def usable(t, op, n, st, algo):
+        try:
+            shm.plan(t, op, n, *st, st[0], npes, algo)
+            return True
+        except shm.ShmemError:
+            return False
+
+    for (t, op) in shm.REFERENCE_PAIRS:
+        for st in active_sets():
+            for algo in ("auto", "rccl", "allreduce", "a2a", "gather"):
+                if not usable(t, op, 1013, st, algo):
+                    continue
+                seed += 1
+                run_case(t, op, 1013, st, algo, "device", seed)
+    for t, op in (("double", "sum"), ("int", "max"), ("long", "xor"), ("float", "prod")):
+        for algo in ("auto", "rccl", "allreduce", "a2a", "gather"):
+            if not usable(t, op, 4103, (0, 0, npes), algo):
+                continue
+            for mode in ("heap", "inplace", "overlap", "host"):
+                seed += 1
+                run_case(t, op, 4103, (0, 0, npes), algo, mode, seed)
+    for n in (0, 1, 2, 63, 65, 1 << 20, (4 << 20) // 8 + 13, (6 << 20) + 5):
+        seed += 1
+        run_case("double", "sum", n, (0, 0, npes), "auto", "device", seed)   # all-reduce, then RS+AG+tail
+    seed += 1
+    run_case("long", "sum", (6 << 20) + 5, (0, 0, npes), "rccl", "device", seed)
+    for st in active_sets():
+        size = st[2]
+        for mode in ("heap", "device", "host"):
+            for bits in (32, 64):
+                seed += 1
+                run_bcast(bits, 1031, seed % size, st, mode, seed)
+                seed += 1
+                run_collect(bits, [517] * npes, st, mode, seed)
+                seed += 1
+                run_collect(bits, [(37 * (q + 1)) % 101 for q in range(npes)], st, mode, seed)
+    for st in active_sets():
+        if member(*st):
+            shm.barrier(*st)
+            ncases += 1
+            n = 4099
+            v = torch.arange(n, dtype=torch.float64, device="cuda")
+            if not shm.verify("double", v, n, *st):
+                fails.append(f"verify of identical arrays on {st}")
+            w = v.clone()
+            w[pe % n] += 1
+            if st[2] > 1 and shm.verify("double", w, n, *st):
+                fails.append(f"verify of differing arrays on {st} said equal")
+        shm.barrier_all()
 elif scenario == "configs":
     # BASELINE.json configs at full size through the blocking drop-in entry
     # points, every PE a process: long and/or/xor over 64 Mi elements

@@ -81,6 +81,26 @@ def test_ipc_transport_all_pairs_sets_placements(tmp_path, npes, shots):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("npes", [2, 3, 4])
+def test_rccl_transport_with_rccl_double(tmp_path, npes):
+    """The default RCCL transport across PE processes on the one GPU, with
+    the RCCL test double (tests/native/fake_rccl.cpp) in place of librccl:
+    every reference pair on every active set through AUTO, RCCL (reduce-
+    scatter + all-gather + all-reduce tail), ALLREDUCE, A2A and GATHER, heap /
+    device / host / in-place / overlapping operands, sizes across the
+    all-reduce threshold, and broadcast, [f]collect, barrier and verify over
+    RCCL — all against the oracle, bit for bit (the double reduces in rank
+    order)."""
+    fake = os.path.join(HERE, "native", "libfake_rccl.so")
+    assert os.path.exists(fake), "tests/native/libfake_rccl.so not built (make -C tests/native)"
+    reports = run_pes(tmp_path, npes, "rccl", {"SHMEMX_TRANSPORT": "rccl", "FAKE_RCCL": fake},
+                      timeout=600)
+    for r in reports:
+        assert r["ncases"] > 0
+        assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
+
+
+@pytest.mark.gpu
 def test_ipc_baseline_configs_full_size(tmp_path):
     """BASELINE.json configs[3] (long and/or/xor, 64 Mi, 4 PEs) and configs[2]'s
     double sum over 32 Mi, as 4 PE processes through the blocking drop-in
