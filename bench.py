@@ -352,8 +352,16 @@ def main():
     # SHMEMX_SHARE_GPU=1: every rank on device 0 (a rehearsal of the N > 1
     # path on a one-GPU box, IPC transport only; never a reported number)
     share = os.environ.get("SHMEMX_SHARE_GPU") == "1"
-    if share and os.environ.get("SHMEMX_TRANSPORT") != "ipc":
-        sys.exit("SHMEMX_SHARE_GPU=1 needs SHMEMX_TRANSPORT=ipc (RCCL refuses two ranks on one GPU)")
+    # $FAKE_RCCL: the RCCL test double (tests/native/fake_rccl.cpp) in place
+    # of librccl, so the RCCL transport can be rehearsed with every rank on
+    # one GPU; its numbers are a host-memory shim's, never reported
+    fake_rccl = os.environ.get("FAKE_RCCL")
+    if fake_rccl:
+        import ctypes
+        ctypes.CDLL(fake_rccl, mode=ctypes.RTLD_GLOBAL)
+    if share and os.environ.get("SHMEMX_TRANSPORT") != "ipc" and not fake_rccl:
+        sys.exit("SHMEMX_SHARE_GPU=1 needs SHMEMX_TRANSPORT=ipc or $FAKE_RCCL "
+                 "(RCCL refuses two ranks on one GPU)")
     local = 0 if share else local
     torch.cuda.set_device(local)
     dist = None
@@ -414,7 +422,12 @@ def main():
         alg_bytes = 3 * nbytes                 # read acc, read in, write acc
         algo_used = "fold"
     else:
-        over = "IPC transport, all ranks on one GPU (rehearsal)" if share else "RCCL over xGMI"
+        if fake_rccl:
+            over = "RCCL TEST DOUBLE through host memory, all ranks on one GPU (rehearsal)"
+        elif share:
+            over = "IPC transport, all ranks on one GPU (rehearsal)"
+        else:
+            over = "RCCL over xGMI"
         workload = f"shmem_double_sum_to_all on {world} PEs (one per GPU), {over}"
         algo_used = a.algo
         src_a = arr(src, 0)
