@@ -212,8 +212,34 @@ struct Pending {
 int g_depth = 0;
 std::vector<Pending> g_group;
 
+bool ranges_overlap(const void *a, size_t na, const void *b, size_t nb) {
+    const char *x = static_cast<const char *>(a), *y = static_cast<const char *>(b);
+    return na && nb && x < y + nb && y < x + na;
+}
+
+// Buffer rules real RCCL does not check but relies on (anything else is a
+// race there, even where this double would happen to get it right): a
+// collective is in place only in RCCL's exact layout, and a group's receive
+// buffers overlap neither each other nor any of its send buffers.
+void check_layout(const char *what, const void *send, size_t send_bytes, const void *recv,
+                  size_t recv_bytes, const void *inplace_send) {
+    if (send == inplace_send) return;
+    if (ranges_overlap(send, send_bytes, recv, recv_bytes)) {
+        std::fprintf(stderr, "fake_rccl: %s: send and receive buffers overlap outside RCCL's in-place layout\n",
+                     what);
+        std::abort();
+    }
+}
+
 void flush_group() {
     if (g_group.empty()) return;
+    for (size_t i = 0; i < g_group.size(); ++i) {
+        if (g_group[i].send) continue;
+        for (size_t j = 0; j < g_group.size(); ++j)
+            if (j != i && ranges_overlap(g_group[i].buf, g_group[i].bytes, g_group[j].buf, g_group[j].bytes))
+                die(g_group[j].send ? "a group receives into one of its send buffers"
+                                    : "two receives of a group overlap");
+    }
     for (const Pending &p : g_group) wait_stream(p.stream);
     ncclComm *c = g_group.front().comm;
     std::vector<std::vector<char>> host(g_group.size());
@@ -316,8 +342,9 @@ ncclResult_t ncclRecv(void *buf, size_t count, ncclDataType_t t, int peer, ncclC
 ncclResult_t ncclAllReduce(const void *send, void *recv, size_t count, ncclDataType_t t, ncclRedOp_t op,
                            ncclComm_t c, hipStream_t s) {
     if (g_depth) die("collective inside a group (not used by the library)");
-    wait_stream(s);
     const size_t b = count * dt_size(t);
+    check_layout("ncclAllReduce", send, b, recv, b, recv);
+    wait_stream(s);
     std::vector<std::vector<char>> out(c->n, to_host(send, b));
     auto in = exchange(c, out, b);
     in[c->rank] = out[c->rank];
@@ -330,8 +357,11 @@ ncclResult_t ncclAllReduce(const void *send, void *recv, size_t count, ncclDataT
 ncclResult_t ncclReduceScatter(const void *send, void *recv, size_t count, ncclDataType_t t,
                                ncclRedOp_t op, ncclComm_t c, hipStream_t s) {
     if (g_depth) die("collective inside a group (not used by the library)");
-    wait_stream(s);
     const size_t b = count * dt_size(t);
+    // in place: recvbuff == sendbuff + rank * recvcount
+    check_layout("ncclReduceScatter", send, b * c->n, recv, b,
+                 static_cast<const char *>(recv) - (size_t)c->rank * b);
+    wait_stream(s);
     const std::vector<char> all = to_host(send, b * c->n);
     std::vector<std::vector<char>> out(c->n);
     for (int p = 0; p < c->n; ++p) out[p].assign(all.begin() + p * b, all.begin() + (p + 1) * b);
@@ -346,8 +376,11 @@ ncclResult_t ncclReduceScatter(const void *send, void *recv, size_t count, ncclD
 ncclResult_t ncclAllGather(const void *send, void *recv, size_t count, ncclDataType_t t, ncclComm_t c,
                            hipStream_t s) {
     if (g_depth) die("collective inside a group (not used by the library)");
-    wait_stream(s);
     const size_t b = count * dt_size(t);
+    // in place: sendbuff == recvbuff + rank * sendcount
+    check_layout("ncclAllGather", send, b, recv, b * c->n,
+                 static_cast<const char *>(recv) + (size_t)c->rank * b);
+    wait_stream(s);
     std::vector<std::vector<char>> out(c->n, to_host(send, b));
     auto in = exchange(c, out, b);
     in[c->rank] = out[c->rank];
@@ -362,8 +395,9 @@ ncclResult_t ncclBroadcast(const void *send, void *recv, size_t count, ncclDataT
                            ncclComm_t c, hipStream_t s) {
     if (g_depth) die("collective inside a group (not used by the library)");
     if (root < 0 || root >= c->n) return ncclInvalidArgument;
-    wait_stream(s);
     const size_t b = count * dt_size(t);
+    if (c->rank == root) check_layout("ncclBroadcast", send, b, recv, b, recv);
+    wait_stream(s);
     std::vector<P2p> ops;
     std::vector<char> data;
     if (c->rank == root) {
