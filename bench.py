@@ -340,11 +340,22 @@ def time_region(fn, steps, stream, barrier):
     return t1 - t0, start.elapsed_time(stop) * 1e-3
 
 
+def stage(rank, what):
+    """Progress on stderr (the JSON line stays alone on stdout): where a run
+    that never prints its line stopped."""
+    print(f"[bench rank {rank} {time.strftime('%H:%M:%S')}] {what}", file=sys.stderr, flush=True)
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # a run stuck anywhere (RCCL bootstrap, a collective) leaves every
+    # thread's Python stack on stderr after 10 minutes
+    import faulthandler
+    faulthandler.dump_traceback_later(600, exit=False)
+    stage(rank, f"start: {world} rank(s), steps {a.steps}, warm-up {a.warmup}")
     if a.gpus != world:
         if world == 1 and a.gpus > 1:
             sys.exit("bench.py --gpus N>1 must be launched with torch.distributed.run")
@@ -437,10 +448,13 @@ def main():
             shm.reduce_on_stream("double", "sum", tgt_a, src_a, n, 0, 0, world, algo_used, sp)
         alg_bytes = None
 
+    stage(rank, f"operands ready ({workload}); warm-up")
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
+    stage(rank, "timed region")
     wall, ev = time_region(step, a.steps, stream, barrier)
+    stage(rank, "timed region done; checking")
     wall = max_over_ranks(wall)
     ev = max_over_ranks(ev)
     ms_per_step = wall / a.steps * 1e3
@@ -555,6 +569,7 @@ def main():
 
     def guarded(name, fn):
         arm_fatal_note(name)
+        stage(rank, f"extra {name}")
         try:
             extras[name] = fn()
         except Exception as e:   # noqa: BLE001 — an extra never costs the headline
@@ -607,7 +622,9 @@ def main():
                                                                 max_over_ranks))
 
     timer.cancel()
+    faulthandler.cancel_dump_traceback_later()
     emit()
+    stage(rank, "line printed")
     for blk in heap_blocks:
         if blk:
             shm.free(blk)
