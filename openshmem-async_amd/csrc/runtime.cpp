@@ -43,11 +43,6 @@ namespace shmx {
 
 State g_state;
 
-// Host-resident arrays move over PCIe in chunks of this size (pipelined);
-// up to kSmallHostBytes they bounce through page-locked buffers instead.
-constexpr size_t kStageChunkBytes = size_t(16) << 20;
-constexpr size_t kSmallHostBytes = size_t(256) << 10;
-constexpr size_t kRingSlots = 4;     // page-locked bounce slots per direction
 std::recursive_mutex g_mu;
 static thread_local int t_last_error = SHMEMX_OK;
 
@@ -320,7 +315,7 @@ static long long allreduce_max_bytes() {
     return b;
 }
 
-static int make_plan(int type, int op, int nreduce, int start, int logstride,
+int make_plan(int type, int op, int nreduce, int start, int logstride,
                      int size, int pe, int npes, int algo, shmemx_plan_t *p) {
     std::memset(p, 0, sizeof *p);
     p->member = -1;
@@ -434,7 +429,7 @@ static void ws_release(hipStream_t s) {
     g_state.ws_stream = s;
 }
 
-static bool overlap(const void *a, const void *b, size_t bytes) {
+bool overlap(const void *a, const void *b, size_t bytes) {
     const char *x = static_cast<const char *>(a), *y = static_cast<const char *>(b);
     return x != y && x < y + bytes && y < x + bytes;
 }
@@ -464,7 +459,7 @@ static int reduce_exchange(int type, int op, char *tgt, const char *src, int nre
                            bool &uses_ws);
 
 // The engine: device-resident target/source, stream-ordered.
-static int reduce_device(int type, int op, void *target, const void *source,
+int reduce_device(int type, int op, void *target, const void *source,
                          int nreduce, int start, int logstride, int size,
                          int algo, hipStream_t s) {
     shmemx_plan_t p;
@@ -646,293 +641,6 @@ bool host_pinned(const void *ptr) {
 // ------------------------------------------------------------- internal API
 // (used by entry.cpp; C++ linkage, not exported in the header)
 namespace shmx {
-
-// ------------------------------------------- page-locked ring, copy pool
-// Pageable host arrays (dlmalloc'd heaps, numpy) cannot be DMA'd
-// asynchronously; they go through kRingSlots page-locked slots per direction,
-// filled and emptied by a small pool of CPU threads, so the CPU copies of
-// one chunk overlap the PCIe transfers and device work of its neighbours.
-static bool ring_reserve(size_t slot_bytes) {
-    if (g_state.ring && g_state.ring_slot >= slot_bytes) return true;
-    if (g_state.ring) {
-        SHMX_HIP(hipDeviceSynchronize());
-        SHMX_HIP(hipHostFree(g_state.ring));
-        g_state.ring = nullptr;
-    }
-    if (hipHostMalloc(&g_state.ring, 2 * kRingSlots * slot_bytes, hipHostMallocDefault) != hipSuccess) {
-        (void)hipGetLastError();
-        g_state.ring = nullptr;
-        g_state.ring_slot = 0;
-        return false;
-    }
-    g_state.ring_slot = slot_bytes;
-    return true;
-}
-static char *ring_in(size_t slot) { return static_cast<char *>(g_state.ring) + slot * g_state.ring_slot; }
-static char *ring_out(size_t slot) {
-    return static_cast<char *>(g_state.ring) + (kRingSlots + slot) * g_state.ring_slot;
-}
-
-namespace {
-class CopyPool {
-  public:
-    CopyPool() {
-        unsigned hw = std::thread::hardware_concurrency();
-        nthreads_ = hw >= 16 ? 8 : (hw >= 4 ? hw / 2 : 1);
-        if (const char *e = std::getenv("SHMEMX_COPY_THREADS"))
-            nthreads_ = std::max(1, std::min(64, std::atoi(e)));
-        for (unsigned i = 1; i < nthreads_; ++i) workers_.emplace_back([this, i] { run(i); });
-    }
-    ~CopyPool() {
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            stop_ = true;
-        }
-        cv_.notify_all();
-        for (auto &t : workers_) t.join();
-    }
-    // memcpy split over the pool; returns when every piece is done
-    void copy(void *dst, const void *src, size_t bytes) {
-        if (bytes < (size_t(4) << 20) || nthreads_ == 1) {
-            std::memcpy(dst, src, bytes);
-            return;
-        }
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            dst_ = static_cast<char *>(dst);
-            src_ = static_cast<const char *>(src);
-            bytes_ = bytes;
-            pending_ = nthreads_ - 1;
-            ++gen_;
-        }
-        cv_.notify_all();
-        piece(0);
-        std::unique_lock<std::mutex> lk(mu_);
-        done_.wait(lk, [this] { return pending_ == 0; });
-    }
-
-  private:
-    void piece(unsigned i) {
-        const size_t per = (bytes_ / nthreads_ + 63) & ~size_t(63);
-        const size_t lo = std::min(bytes_, per * i), hi = std::min(bytes_, per * (i + 1));
-        if (hi > lo) std::memcpy(dst_ + lo, src_ + lo, hi - lo);
-    }
-    void run(unsigned i) {
-        unsigned long long seen = 0;
-        for (;;) {
-            {
-                std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-                if (stop_) return;
-                seen = gen_;
-            }
-            piece(i);
-            {
-                std::lock_guard<std::mutex> lk(mu_);
-                if (--pending_ == 0) done_.notify_one();
-            }
-        }
-    }
-    unsigned nthreads_ = 1;
-    std::vector<std::thread> workers_;
-    std::mutex mu_;
-    std::condition_variable cv_, done_;
-    bool stop_ = false;
-    unsigned long long gen_ = 0;
-    unsigned pending_ = 0;
-    char *dst_ = nullptr;
-    const char *src_ = nullptr;
-    size_t bytes_ = 0;
-};
-}  // namespace
-
-static void parallel_copy(void *dst, const void *src, size_t bytes) {
-    static CopyPool pool;
-    pool.copy(dst, src, bytes);
-}
-
-// The blocking entry point body: host- or device-resident arrays.
-void reduce_blocking(int type, int op, void *target, const void *source,
-                     int nreduce, int start, int logstride, int size) {
-    std::lock_guard<std::recursive_mutex> lk(g_mu);
-    t_last_error = SHMEMX_OK;
-    if (ensure_init()) {
-        trace(LOG_FATAL, "reduction called before shmem_init with npes > 1");
-        return;
-    }
-    if (!op_on_device(type, op)) {
-        set_error(op_valid(type, op) ? SHMEMX_ENOTSUP : SHMEMX_EINVAL);
-        return;
-    }
-    if (nreduce <= 0 || !target || !source) {
-        if (nreduce < 0 || ((!target || !source) && nreduce > 0)) set_error(SHMEMX_EINVAL);
-        else {  // n == 0: nothing moves, but validate membership like a call would
-            shmemx_plan_t p;
-            int rc = make_plan(type, op, 0, start, logstride, size, g_state.pe, g_state.npes,
-                               g_state.algo, &p);
-            if (rc) set_error(rc);
-        }
-        return;
-    }
-    const size_t bytes = type_size(type) * (size_t)nreduce;
-    const bool tdev = device_accessible(target), sdev = device_accessible(source);
-    hipStream_t s = g_state.stream;
-    if (tdev && sdev) {
-        reduce_device(type, op, target, source, nreduce, start, logstride, size, g_state.algo, s);
-        SHMX_HIP(hipStreamSynchronize(s));
-        if (signal_timed_out()) fatal("SIGNAL reduction", "a member never reached the device barrier");
-        return;
-    }
-    // Host-resident symmetric arrays (the reference's heap): stage over PCIe
-    // in chunks, H2D on one copy stream, the reduction on the library stream,
-    // D2H on a second copy stream, so the two PCIe directions and the device
-    // work overlap.  Every PE cuts the same chunks, so the collective
-    // sequence matches across PEs.
-    {
-        shmemx_plan_t p;
-        const int rc = make_plan(type, op, nreduce, start, logstride, size, g_state.pe,
-                                 g_state.npes, g_state.algo, &p);
-        if (rc) {
-            set_error(rc);
-            return;
-        }
-    }
-    if (bytes > g_state.stage_bytes) {
-        SHMX_HIP(hipDeviceSynchronize());
-        if (g_state.stage_src) SHMX_HIP(hipFree(g_state.stage_src));
-        if (g_state.stage_tgt) SHMX_HIP(hipFree(g_state.stage_tgt));
-        g_state.stage_src = g_state.stage_tgt = nullptr;
-        g_state.stage_bytes = 0;
-        if (hipMalloc(&g_state.stage_src, bytes) != hipSuccess ||
-            hipMalloc(&g_state.stage_tgt, bytes) != hipSuccess) {
-            (void)hipGetLastError();
-            set_error(SHMEMX_ENOMEM);
-            return;
-        }
-        g_state.stage_bytes = bytes;
-    }
-    if (bytes <= kSmallHostBytes) {
-        // Small messages (the ISx nreduce = 1 case, isx.c:617): latency, not
-        // bandwidth.  Bounce through page-locked host buffers so both copies
-        // are plain DMA on the library stream, and wait once.
-        if (bytes > g_state.bounce_bytes) {
-            if (g_state.bounce) SHMX_HIP(hipHostFree(g_state.bounce));
-            g_state.bounce = nullptr;
-            g_state.bounce_bytes = 0;
-            if (hipHostMalloc(&g_state.bounce, 2 * kSmallHostBytes, hipHostMallocDefault) != hipSuccess) {
-                (void)hipGetLastError();
-                set_error(SHMEMX_ENOMEM);
-                return;
-            }
-            g_state.bounce_bytes = kSmallHostBytes;
-        }
-        char *bin = static_cast<char *>(g_state.bounce);
-        char *bout = bin + kSmallHostBytes;
-        const void *dsrc = source;
-        if (!sdev) {
-            std::memcpy(bin, source, bytes);
-            SHMX_HIP(hipMemcpyAsync(g_state.stage_src, bin, bytes, hipMemcpyHostToDevice, s));
-            dsrc = g_state.stage_src;
-        }
-        void *dtgt = tdev ? target : g_state.stage_tgt;
-        const int rc = reduce_device(type, op, dtgt, dsrc, nreduce, start, logstride, size,
-                                     g_state.algo, s);
-        if (!rc && !tdev) SHMX_HIP(hipMemcpyAsync(bout, dtgt, bytes, hipMemcpyDeviceToHost, s));
-        SHMX_HIP(hipStreamSynchronize(s));
-        if (!rc && !tdev) std::memcpy(target, bout, bytes);
-        return;
-    }
-    if (!g_state.h2d) {
-        SHMX_HIP(hipStreamCreateWithFlags(&g_state.h2d, hipStreamNonBlocking));
-        SHMX_HIP(hipStreamCreateWithFlags(&g_state.d2h, hipStreamNonBlocking));
-    }
-    const size_t sz = type_size(type);
-    const size_t g = sz >= 16 ? 1 : 16 / sz;
-    static const size_t stage_chunk = [] {
-        const char *e = std::getenv("SHMEMX_STAGE_CHUNK_MB");
-        const int mb = e ? std::atoi(e) : 0;
-        return mb > 0 ? size_t(mb) << 20 : kStageChunkBytes;
-    }();
-    size_t chunk = ((stage_chunk / sz) / g) * g;
-    if (chunk == 0) chunk = g;
-    // a host target that partially overlaps the host source would be
-    // overwritten under a later chunk's H2D: no pipelining then
-    const bool host_overlap = !tdev && !sdev && overlap(target, source, bytes);
-    if (host_overlap) chunk = (size_t)nreduce;
-    const size_t nchunks = ((size_t)nreduce + chunk - 1) / chunk;
-    // How each end reaches the device: directly (device memory), by DMA
-    // (page-locked host memory), or through the page-locked bounce ring
-    // (pageable memory: CPU copy by the worker pool, then DMA).
-    const bool in_bounce = !sdev && !host_pinned(source) && !host_overlap;
-    const bool out_bounce = !tdev && !host_pinned(target) && !host_overlap;
-    const size_t chunk_bytes = chunk * sz;
-    if ((in_bounce || out_bounce) && !ring_reserve(chunk_bytes)) {
-        set_error(SHMEMX_ENOMEM);
-        return;
-    }
-    while (g_state.events.size() < 2 * nchunks + 2 * kRingSlots) {
-        hipEvent_t e;
-        SHMX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        g_state.events.push_back(e);
-    }
-    hipEvent_t *ev_chunk = g_state.events.data();             // 2 per chunk
-    hipEvent_t *ev_in_slot = ev_chunk + 2 * nchunks;          // ring slot free again
-    hipEvent_t *ev_out_slot = ev_in_slot + kRingSlots;        // ring slot filled
-    char *hsrc = static_cast<char *>(const_cast<void *>(source));
-    char *htgt = static_cast<char *>(target);
-    char *ssrc = static_cast<char *>(g_state.stage_src);
-    char *stgt = static_cast<char *>(g_state.stage_tgt);
-    size_t drained = 0;  // chunks copied out of the ring so far (out_bounce)
-    auto drain_one = [&]() {
-        const size_t j = drained++;
-        const size_t slot = j % kRingSlots;
-        const size_t cnt = std::min(chunk, (size_t)nreduce - j * chunk);
-        SHMX_HIP(hipEventSynchronize(ev_out_slot[slot]));
-        parallel_copy(htgt + j * chunk_bytes, ring_out(slot), cnt * sz);
-    };
-    int rc = SHMEMX_OK;
-    for (size_t k = 0; k < nchunks && !rc; ++k) {
-        const size_t off = k * chunk_bytes;
-        const size_t cnt = std::min(chunk, (size_t)nreduce - k * chunk);
-        const size_t b = cnt * sz;
-        const size_t slot = k % kRingSlots;
-        const void *dsrc = hsrc + off;
-        if (!sdev) {
-            const char *from = hsrc + off;
-            if (in_bounce) {
-                if (k >= kRingSlots) SHMX_HIP(hipEventSynchronize(ev_in_slot[slot]));
-                parallel_copy(ring_in(slot), hsrc + off, b);
-                from = ring_in(slot);
-            }
-            SHMX_HIP(hipMemcpyAsync(ssrc + off, from, b, hipMemcpyHostToDevice, g_state.h2d));
-            SHMX_HIP(hipEventRecord(ev_chunk[2 * k], g_state.h2d));
-            if (in_bounce) SHMX_HIP(hipEventRecord(ev_in_slot[slot], g_state.h2d));
-            SHMX_HIP(hipStreamWaitEvent(s, ev_chunk[2 * k], 0));
-            dsrc = ssrc + off;
-        }
-        void *dtgt = tdev ? static_cast<void *>(htgt + off) : static_cast<void *>(stgt + off);
-        rc = reduce_device(type, op, dtgt, dsrc, (int)cnt, start, logstride, size, g_state.algo, s);
-        if (!rc && !tdev) {
-            SHMX_HIP(hipEventRecord(ev_chunk[2 * k + 1], s));
-            SHMX_HIP(hipStreamWaitEvent(g_state.d2h, ev_chunk[2 * k + 1], 0));
-            if (out_bounce) {
-                // the slot's previous chunk must be copied out before reuse
-                while (drained + kRingSlots <= k) drain_one();
-                SHMX_HIP(hipMemcpyAsync(ring_out(slot), dtgt, b, hipMemcpyDeviceToHost, g_state.d2h));
-                SHMX_HIP(hipEventRecord(ev_out_slot[slot], g_state.d2h));
-                // keep the CPU busy on the oldest finished chunk, one behind
-                if (k >= 1 && drained < k) drain_one();
-            } else {
-                SHMX_HIP(hipMemcpyAsync(htgt + off, dtgt, b, hipMemcpyDeviceToHost, g_state.d2h));
-            }
-        }
-    }
-    if (out_bounce && !rc)
-        while (drained < nchunks) drain_one();
-    SHMX_HIP(hipStreamSynchronize(g_state.h2d));
-    SHMX_HIP(hipStreamSynchronize(s));
-    SHMX_HIP(hipStreamSynchronize(g_state.d2h));
-}
 
 // $SHMEMX_DEBUG=1: the checks the reference's wrappers make when configured
 // with --enable-debug (reduce-op.c:379-381, utils.h:64-116): target and

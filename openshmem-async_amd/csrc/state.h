@@ -82,6 +82,14 @@ void trace(int level, const char *fmt, ...);
     } while (0)
 
 int ensure_init();                  // single-PE auto-init; ENOINIT if npes > 1
+// The plan of one call (shmemx_reduce_plan) and the device-resident engine
+// (runtime.cpp); the host staging of the blocking entry points (staging.cpp)
+// runs the engine chunk by chunk.
+int make_plan(int type, int op, int nreduce, int start, int logstride, int size, int pe, int npes,
+              int algo, shmemx_plan_t *p);
+int reduce_device(int type, int op, void *target, const void *source, int nreduce, int start,
+                  int logstride, int size, int algo, hipStream_t s);
+bool overlap(const void *a, const void *b, size_t bytes);   // distinct, overlapping ranges
 bool is_member(int pe, int start, int logstride, int size, int *index);
 bool device_accessible(const void *ptr);
 bool host_pinned(const void *ptr);
