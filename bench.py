@@ -87,12 +87,19 @@ def cpu_baseline(n: int, reps: int):
     times, _ = oracle.reduce_fork("double", "sum", 2, 0, 0, 2, n, kind=0, reps=reps, pin_base=0)
     wall = time.perf_counter() - t0
     med = statistics.median(times)
+    model = "unknown CPU"
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next(ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
     return {"value": round(n * 8 / med / GiB, 4), "unit": "GiB/s", "cores": 2,
             "kind": "port",
             "sample": f"oracle restatement of reduce-op.c (gcc -O2), shmem_double_sum_to_all "
-                      f"nreduce={n} on 2 PEs = 2 processes pinned to 2 cores, shm loopback; "
+                      f"nreduce={n} on 2 PEs = 2 processes pinned to cores 0 and 1, shm loopback; "
                       f"PE 0 per-call time, median of {reps} warm calls "
-                      f"({med * 1e3:.1f} ms/call, {wall:.1f} s wall)"}
+                      f"({med * 1e3:.1f} ms/call, {wall:.1f} s wall); host: {model}, "
+                      f"{os.cpu_count()} logical CPUs"}
 
 
 def host_e2e(n: int):
