@@ -403,6 +403,36 @@ elif scenario == "rccl":
             if st[2] > 1 and shm.verify("double", w, n, *st):
                 fails.append(f"verify of differing arrays on {st} said equal")
         shm.barrier_all()
+elif scenario == "soak":
+    # Random calls, the same sequence on every PE (one seeded generator):
+    # type/op pair, size (edges favoured), active set, algorithm and operand
+    # placement, on whichever transport the environment selects.
+    import random
+    rng = random.Random(int(os.environ.get("SOAK_SEED", "7")))
+    iters = int(os.environ.get("SOAK_ITERS", "60"))
+    rccl = os.environ.get("SHMEMX_TRANSPORT") != "ipc"
+    algos = ("auto", "rccl", "allreduce", "a2a", "gather", "direct", "signal") if rccl else \
+        ("auto", "direct", "gather", "signal")
+    sets = active_sets()
+    edges = (0, 1, 2, 3, 7, 15, 16, 17, 63, 64, 65, 127, 1023, 4096, 4097, 32768 + 1)
+    for it in range(iters):
+        t, op = rng.choice(shm.REFERENCE_PAIRS)
+        n = rng.choice(edges) if rng.random() < 0.5 else rng.randrange(1, 300000)
+        if t == "longdouble":
+            n = min(n, 40000)
+        st = rng.choice(sets)
+        algo = rng.choice(algos)
+        mode = rng.choice(("heap", "device", "inplace", "overlap", "host"))
+        if algo == "signal":
+            mode = rng.choice(("heap", "inplace"))     # symmetric operands only
+        if (n + 3) * 16 > CAP:
+            n = CAP // 16 - 3
+        try:
+            shm.plan(t, op, n, *st, st[0], npes, algo)
+        except shm.ShmemError:
+            continue                               # not a valid (set, algo) pair here
+        seed += 1
+        run_case(t, op, n, st, algo, mode, seed)
 elif scenario == "configs":
     # BASELINE.json configs at full size through the blocking drop-in entry
     # points, every PE a process: long and/or/xor over 64 Mi elements

@@ -101,6 +101,24 @@ def test_rccl_transport_with_rccl_double(tmp_path, npes):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("transport,npes", [("ipc", 3), ("rccl", 4)])
+def test_soak_random_calls(tmp_path, transport, npes):
+    """Random collective calls, the same seeded sequence on every PE: any
+    reference pair, size (edges favoured), active set, algorithm the transport
+    offers and operand placement, each against the oracle.  The RCCL
+    transport runs on the RCCL test double.  $SOAK_ITERS / $SOAK_SEED make
+    longer or different runs."""
+    env = {"SHMEMX_TRANSPORT": transport, "SOAK_ITERS": os.environ.get("SOAK_ITERS", "60"),
+           "SOAK_SEED": os.environ.get("SOAK_SEED", "7")}
+    if transport == "rccl":
+        env["FAKE_RCCL"] = os.path.join(HERE, "native", "libfake_rccl.so")
+    reports = run_pes(tmp_path, npes, "soak", env, timeout=900)
+    for r in reports:
+        assert r["ncases"] > 0
+        assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
+
+
+@pytest.mark.gpu
 def test_ipc_baseline_configs_full_size(tmp_path):
     """BASELINE.json configs[3] (long and/or/xor, 64 Mi, 4 PEs) and configs[2]'s
     double sum over 32 Mi, as 4 PE processes through the blocking drop-in
