@@ -416,6 +416,20 @@ elif scenario == "soak":
     sets = active_sets()
     edges = (0, 1, 2, 3, 7, 15, 16, 17, 63, 64, 65, 127, 1023, 4096, 4097, 32768 + 1)
     for it in range(iters):
+        if rng.random() < 0.2:
+            # a neighbouring collective instead: broadcast, fcollect or collect
+            st = rng.choice(sets)
+            mode = rng.choice(("heap", "device", "host"))
+            bits = rng.choice((32, 64))
+            kind = rng.choice(("bcast", "fcollect", "collect"))
+            seed += 1
+            if kind == "bcast":
+                run_bcast(bits, rng.choice((0, 1, 5, 1031, 70001)), rng.randrange(st[2]), st, mode, seed)
+            elif kind == "fcollect":
+                run_collect(bits, [rng.choice((0, 1, 17, 517, 20000))] * npes, st, mode, seed)
+            else:
+                run_collect(bits, [rng.randrange(0, 20000) for _ in range(npes)], st, mode, seed)
+            continue
         t, op = rng.choice(shm.REFERENCE_PAIRS)
         n = rng.choice(edges) if rng.random() < 0.5 else rng.randrange(1, 300000)
         if t == "longdouble":
