@@ -132,6 +132,22 @@ static void parallel_copy(void *dst, const void *src, size_t bytes) {
     pool.copy(dst, src, bytes);
 }
 
+// The small-message bounce buffers: fine-grained (coherent) page-locked
+// memory, so a kernel that reads or writes them in place sees the host's
+// bytes and the host sees its stores after the stream wait, with no cached
+// copy in any XCD's L2 across calls.
+static bool small_bounce_reserve() {
+    if (g_state.bounce) return true;
+    if (hipHostMalloc(&g_state.bounce, 2 * kSmallHostBytes, hipHostMallocCoherent) != hipSuccess) {
+        (void)hipGetLastError();
+        g_state.bounce = nullptr;
+        g_state.bounce_bytes = 0;
+        return false;
+    }
+    g_state.bounce_bytes = kSmallHostBytes;
+    return true;
+}
+
 // The blocking entry point body: host- or device-resident arrays.
 void reduce_blocking(int type, int op, void *target, const void *source,
                      int nreduce, int start, int logstride, int size) {
@@ -169,14 +185,31 @@ void reduce_blocking(int type, int op, void *target, const void *source,
     // D2H on a second copy stream, so the two PCIe directions and the device
     // work overlap.  Every PE cuts the same chunks, so the collective
     // sequence matches across PEs.
+    shmemx_plan_t plan;
     {
-        shmemx_plan_t p;
         const int rc = make_plan(type, op, nreduce, start, logstride, size, g_state.pe,
-                                 g_state.npes, g_state.algo, &p);
+                                 g_state.npes, g_state.algo, &plan);
         if (rc) {
             set_error(rc);
             return;
         }
+    }
+    if (bytes <= kSmallHostBytes && !small_bounce_reserve()) {
+        set_error(SHMEMX_ENOMEM);
+        return;
+    }
+    if (bytes <= kSmallHostBytes && plan.nmembers == 1 && !g_state.force_collective) {
+        // A one-member set is a copy (reduce-op.c:213-216).  The copy kernel
+        // reads and writes the page-locked bounce buffers in place over PCIe
+        // (zero-copy): one launch and one wait, no DMA commands.
+        char *bin = static_cast<char *>(g_state.bounce);
+        char *bout = bin + kSmallHostBytes;
+        if (!sdev) std::memcpy(bin, source, bytes);
+        const int rc = reduce_device(type, op, tdev ? target : bout, sdev ? source : bin, nreduce,
+                                     start, logstride, size, g_state.algo, s);
+        SHMX_HIP(hipStreamSynchronize(s));
+        if (!rc && !tdev) std::memcpy(target, bout, bytes);
+        return;
     }
     if (bytes > g_state.stage_bytes) {
         SHMX_HIP(hipDeviceSynchronize());
@@ -194,31 +227,26 @@ void reduce_blocking(int type, int op, void *target, const void *source,
     }
     if (bytes <= kSmallHostBytes) {
         // Small messages (the ISx nreduce = 1 case, isx.c:617): latency, not
-        // bandwidth.  Bounce through page-locked host buffers so both copies
-        // are plain DMA on the library stream, and wait once.
-        if (bytes > g_state.bounce_bytes) {
-            if (g_state.bounce) SHMX_HIP(hipHostFree(g_state.bounce));
-            g_state.bounce = nullptr;
-            g_state.bounce_bytes = 0;
-            if (hipHostMalloc(&g_state.bounce, 2 * kSmallHostBytes, hipHostMallocDefault) != hipSuccess) {
-                (void)hipGetLastError();
-                set_error(SHMEMX_ENOMEM);
-                return;
-            }
-            g_state.bounce_bytes = kSmallHostBytes;
-        }
+        // bandwidth.  Bounce through the page-locked buffers; copy kernels on
+        // the library stream move them to and from the device (no DMA
+        // command: 25 vs 33 us per call at 32 KiB, profiles/r01_host_latency.txt),
+        // and the host waits once.
         char *bin = static_cast<char *>(g_state.bounce);
         char *bout = bin + kSmallHostBytes;
         const void *dsrc = source;
         if (!sdev) {
             std::memcpy(bin, source, bytes);
-            SHMX_HIP(hipMemcpyAsync(g_state.stage_src, bin, bytes, hipMemcpyHostToDevice, s));
+            const void *in[1] = {bin};
+            fold_chain(type, op, g_state.stage_src, in, 1, (size_t)nreduce, s);
             dsrc = g_state.stage_src;
         }
         void *dtgt = tdev ? target : g_state.stage_tgt;
         const int rc = reduce_device(type, op, dtgt, dsrc, nreduce, start, logstride, size,
                                      g_state.algo, s);
-        if (!rc && !tdev) SHMX_HIP(hipMemcpyAsync(bout, dtgt, bytes, hipMemcpyDeviceToHost, s));
+        if (!rc && !tdev) {
+            const void *in[1] = {dtgt};
+            fold_chain(type, op, bout, in, 1, (size_t)nreduce, s);
+        }
         SHMX_HIP(hipStreamSynchronize(s));
         if (!rc && !tdev) std::memcpy(target, bout, bytes);
         return;
