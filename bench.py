@@ -641,8 +641,13 @@ def main():
     # Leave without the interpreter's and the runtimes' exit-time teardown
     # (RCCL communicator, HIP): the line is out, and nothing the driver
     # reads depends on it (the node block's /dev/shm name went at init).
+    # Under rocprofv3 (it sets ROCPROF* variables) leave normally instead: its
+    # tool writes the traces and counters at exit.
     sys.stdout.flush()
     sys.stderr.flush()
+    if any(k.startswith("ROCPROF") for k in os.environ):
+        shm.finalize()
+        sys.exit(0 if ok else 1)
     os._exit(0 if ok else 1)
 
 
