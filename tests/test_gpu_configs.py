@@ -63,3 +63,34 @@ def test_config5_float_sum_size_sweep(cuda, shm):
         want = want + s
     torch.cuda.synchronize()
     assert torch.equal(out, want)
+
+
+def test_beyond_2gib_and_max_nreduce(cuda, shm):
+    """The reference computes the byte count as an int (reduce-op.c:180), so
+    it breaks above 2 GiB; here offsets are 64-bit everywhere.  nreduce =
+    INT_MAX shorts (4 GiB per array, odd length: scalar tail at the far end)
+    through the blocking drop-in call at PE_size = 1 (a copy), and a
+    2.5 GiB long xor fold checked by the involution (a ^ b) ^ b == a."""
+    import torch
+    g = torch.Generator(device="cuda")
+    g.manual_seed(31)
+    n = 2**31 - 1
+    src = torch.randint(-2**15, 2**15, (n,), dtype=torch.int16, device="cuda", generator=g)
+    tgt = torch.zeros_like(src)
+    shm.to_all("short", "max", tgt, src, n, 0, 0, 1)
+    assert shm.last_error() == 0
+    torch.cuda.synchronize()
+    assert torch.equal(tgt, src)
+    assert torch.equal(tgt[-3:], src[-3:])
+    del src, tgt
+    torch.cuda.empty_cache()
+    n = 320 * 1024 * 1024 + 3
+    a = torch.randint(-2**63, 2**63 - 1, (n,), dtype=torch.int64, device="cuda", generator=g)
+    b = torch.randint(-2**63, 2**63 - 1, (n,), dtype=torch.int64, device="cuda", generator=g)
+    acc = a.clone()
+    shm.fold("long", "xor", acc, b, n)
+    torch.cuda.synchronize()
+    assert torch.equal(acc, torch.bitwise_xor(a, b))
+    shm.fold("long", "xor", acc, b, n)
+    torch.cuda.synchronize()
+    assert torch.equal(acc, a)
