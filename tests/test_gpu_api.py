@@ -288,6 +288,18 @@ def test_host_small_messages_bounce_path(cuda, shm, oracle, n):
     tgt[:] = 0
     shm.to_all("int", "min", tgt, d, n, 0, 0, 1)                 # device -> host
     assert tgt.tobytes() == src.tobytes()
+    # in place and partially overlapping host arrays (the one-member set is a
+    # copy of the source as it was on entry, reduce-op.c:187-216)
+    buf = np.concatenate([src, np.zeros(5, src.dtype)])
+    shm.to_all("int", "sum", buf, buf, n, 0, 0, 1)
+    assert shm.last_error() == 0 and buf[:n].tobytes() == src.tobytes()
+    shm.to_all("int", "sum", buf[3:], buf, n, 0, 0, 1)
+    assert shm.last_error() == 0 and buf[3:n + 3].tobytes() == src.tobytes()
+    # fresh data through the same bounce buffers on every call
+    for k in range(3):
+        fresh = oracle.fill("int", 10 + k, n, n)
+        shm.to_all("int", "or", tgt, fresh, n, 0, 0, 1)
+        assert tgt.tobytes() == fresh.tobytes()
 
 
 def test_trace_facility(cuda, tmp_path):
