@@ -52,6 +52,32 @@ __global__ __launch_bounds__(B) void v_strided(f64x2 *acc, const f64x2 *in, size
     }
 }
 
+// V6: per-array cache policy. P bit0: acc loads nt, bit1: stores nt,
+// bit2: in loads nt (v_strided's NT = 1 is P = 5, NT = 3 is P = 7).
+template <int B, int U, int P>
+__global__ __launch_bounds__(B) void v_mixed(f64x2 *acc, const f64x2 *in, size_t nvec) {
+    constexpr int LA = (P & 1) ? 1 : 0, LI = (P & 4) ? 1 : 0, S = (P & 2) ? 2 : 0;
+    const size_t base = (size_t)blockIdx.x * B * U;
+    if (base + (size_t)B * U <= nvec) {
+        f64x2 a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) a[u] = ld<LA>(acc + base + threadIdx.x + u * B);
+#pragma unroll
+        for (int u = 0; u < U; ++u) b[u] = ld<LI>(in + base + threadIdx.x + u * B);
+#pragma unroll
+        for (int u = 0; u < U; ++u) st<S>(acc + base + threadIdx.x + u * B, a[u] + b[u]);
+    } else {
+        for (int u = 0; u < U; ++u) {
+            size_t v = base + threadIdx.x + u * B;
+            if (v < nvec) st<S>(acc + v, ld<LA>(acc + v) + ld<LI>(in + v));
+        }
+    }
+}
+template <int B, int U, int P>
+static void L_mixed(f64x2 *a, const f64x2 *b, size_t nv, hipStream_t s) {
+    hipLaunchKernelGGL((v_mixed<B, U, P>), dim3((nv + B * U - 1) / (B * U)), dim3(B), 0, s, a, b, nv);
+}
+
 // V1: interleaved issue order (acc[u], in[u], acc[u+1], ...)
 template <int B, int U, int NT>
 __global__ __launch_bounds__(B) void v_interleave(f64x2 *acc, const f64x2 *in, size_t nvec) {
@@ -271,7 +297,7 @@ static int pairs_mode(size_t n) {
 
 int main(int argc, char **argv) {
     const size_t n = argc > 1 ? strtoull(argv[1], 0, 10) : (32ull << 20);
-    const int cold = argc > 2 ? atoi(argv[2]) : 0;
+    int cold = argc > 2 ? atoi(argv[2]) : 0;
     if (cold == 2) return offsets_mode(n);
     if (cold == 3) return pairs_mode(n);
     const size_t nvec = n / 2;
@@ -284,6 +310,16 @@ int main(int argc, char **argv) {
     CK(hipMemset(in, 0, n * 8));
     hipStream_t s;
     CK(hipStreamCreate(&s));
+    std::vector<Variant> mixed = {
+        {"mixed_p7_ldA_ldI_st_nt", L_mixed<256, 4, 7>},
+        {"mixed_p6_ldI_st_nt", L_mixed<256, 4, 6>},
+        {"mixed_p3_ldA_st_nt", L_mixed<256, 4, 3>},
+        {"mixed_p5_ldA_ldI_nt", L_mixed<256, 4, 5>},
+        {"mixed_p4_ldI_nt", L_mixed<256, 4, 4>},
+        {"mixed_p1_ldA_nt", L_mixed<256, 4, 1>},
+        {"mixed_p2_st_nt", L_mixed<256, 4, 2>},
+        {"mixed_p7_again", L_mixed<256, 4, 7>},
+    };
     std::vector<Variant> vs = {
         {"strided_b256_u4_nt3", L_strided<256, 4, 3>},
         {"strided_b256_u2_nt3", L_strided<256, 2, 3>},
@@ -311,6 +347,10 @@ int main(int argc, char **argv) {
         {"pipe_b256_u2_nt3_g8192", L_pipe<256, 2, 3, 8192>},
         {"strided_b256_u4_nt3_again", L_strided<256, 4, 3>},
     };
+    if (cold >= 4) {  // modes 4 (warm) and 5 (cold): the per-array policies
+        vs = mixed;
+        cold -= 4;
+    }
     const int K = cold ? 1 : 20, R = 7;
     std::vector<std::vector<float>> t(vs.size());
     hipEvent_t e0, e1;
