@@ -307,7 +307,11 @@ void *shmemx_heap_ptr(const void *addr, int pe);
  * tuning: out[0] = calls, then microseconds summed over them: [1] waiting for
  * this PE's source (entry fence + stream), [2] entry barrier, [3] fold kernel
  * (reduce-scatter from the peers' HBM), [4] barrier after it, [5] gather
- * kernel (all-gather from the peers' HBM), [6] exit barrier(s).  Fills at most
+ * kernel (all-gather from the peers' HBM), [6] exit barrier(s); then the
+ * system-fence coverage counters (every XCD must run the fence that hands
+ * data to the peers): [7] fences checked on the host, [8] of them run again
+ * because a block did not reach some XCD, [9] fences checked by the SIGNAL
+ * device barrier, [10] of them incomplete (the call fails).  Fills at most
  * nout values and returns how many; reset != 0 zeroes the counters. */
 int shmemx_direct_stats(double *out, int nout, int reset);
 

@@ -122,8 +122,8 @@ int barrier_impl(int start, int logstride, int size) {
     // (system-scope fence on every XCD) visible to the peers, whose stores
     // through shmemx_heap_ptr this GPU will then not see through stale lines
     const bool coll = collective(si);
-    if (coll && si.P > 1) SHMX_HIP(launch_sys_fence(s));
-    SHMX_HIP(hipStreamSynchronize(s));
+    if (coll && si.P > 1) fence_and_wait(s);
+    else SHMX_HIP(hipStreamSynchronize(s));
     trace(LOG_BARRIER, "set (%d,%d,%d) member %d", start, logstride, size, si.m);
     if (!coll) return SHMEMX_OK;
     if (!g_state.comm) {   // IPC transport

@@ -36,6 +36,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
+#include <cstring>
 #include <unordered_set>
 #include <vector>
 
@@ -145,11 +146,76 @@ bool map_regions(const std::vector<std::pair<node::Region, int>> &regs, int star
     return true;
 }
 
+// ------------------------------------------------- fence coverage (XCDs)
+// Every system fence records which XCD each of its blocks ran on
+// (launch_sys_fence); a fence that did not reach every XCD of the device is
+// run again (host-synchronous paths) or fails the SIGNAL call loudly.
+namespace {
+
+struct FenceState {
+    unsigned int *host_seen = nullptr;         // host-coherent, kFenceBlocks words
+    unsigned int *dev_seen = nullptr;          // device, kFenceBlocks words
+    unsigned long long *dev_stats = nullptr;   // device: [checks, incomplete]
+    int nxcc = 0;
+    double host_checks = 0, host_refills = 0;
+} g_fence;
+
+void ensure_fence() {
+    if (g_fence.host_seen) return;
+    int dev = 0, nxcc = 0;
+    SHMX_HIP(hipGetDevice(&dev));
+    if (hipDeviceGetAttribute(&nxcc, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess || nxcc < 1) {
+        (void)hipGetLastError();
+        nxcc = 8;   // MI355X: 8 XCDs
+    }
+    g_fence.nxcc = nxcc > 16 ? 16 : nxcc;
+    void *h = nullptr, *d = nullptr, *st = nullptr;
+    SHMX_HIP(hipHostMalloc(&h, kFenceBlocks * sizeof(unsigned int), hipHostMallocCoherent));
+    std::memset(h, 0, kFenceBlocks * sizeof(unsigned int));
+    SHMX_HIP(hipMalloc(&d, kFenceBlocks * sizeof(unsigned int)));
+    SHMX_HIP(hipMemset(d, 0, kFenceBlocks * sizeof(unsigned int)));
+    SHMX_HIP(hipMalloc(&st, 2 * sizeof(unsigned long long)));
+    SHMX_HIP(hipMemset(st, 0, 2 * sizeof(unsigned long long)));
+    SHMX_HIP(hipDeviceSynchronize());
+    g_fence.host_seen = static_cast<unsigned int *>(h);
+    g_fence.dev_seen = static_cast<unsigned int *>(d);
+    g_fence.dev_stats = static_cast<unsigned long long *>(st);
+    trace(LOG_INIT, "system fences: %d blocks over %d XCDs", kFenceBlocks, g_fence.nxcc);
+}
+
+}  // namespace
+
+void fence_and_wait(hipStream_t s) {
+    ensure_fence();
+    volatile unsigned int *seen = g_fence.host_seen;
+    for (int attempt = 0;; ++attempt) {
+        SHMX_HIP(launch_sys_fence(s, g_fence.host_seen));
+        SHMX_HIP(hipStreamSynchronize(s));
+        unsigned int mask = 0;
+        for (int b = 0; b < kFenceBlocks; ++b) {
+            const unsigned int v = seen[b];
+            if (v & kFenceSeen) mask |= 1u << (v & 15u);
+            seen[b] = 0;
+        }
+        g_fence.host_checks += 1;
+        if (__builtin_popcount(mask) >= g_fence.nxcc) return;
+        g_fence.host_refills += 1;
+        trace(LOG_INFO, "system fence reached XCD mask 0x%x (%d of %d XCDs): fencing again", mask,
+              __builtin_popcount(mask), g_fence.nxcc);
+        if (attempt >= 15) fatal("system fence", "an XCD never ran a fence block (16 attempts)");
+    }
+}
+
+FenceRecords fence_records() {
+    ensure_fence();
+    return FenceRecords{g_fence.dev_seen, g_fence.nxcc, g_fence.dev_stats};
+}
+
 void node_sync(int start, int step, int P, hipStream_t s, double *stream_us, double *barrier_us,
                double since_us) {
     const double t0 = since_us >= 0 ? since_us : now_us();
-    if (P > 1) SHMX_HIP(launch_sys_fence(s));
-    SHMX_HIP(hipStreamSynchronize(s));
+    if (P > 1) fence_and_wait(s);
+    else SHMX_HIP(hipStreamSynchronize(s));
     const double t1 = now_us();
     node::barrier(start, step, P);
     if (stream_us) *stream_us += t1 - t0;
@@ -157,11 +223,26 @@ void node_sync(int start, int step, int P, hipStream_t s, double *stream_us, dou
 }
 
 int direct_stats(double *out, int nout, bool reset) {
-    const int k = std::min(nout, 1 + (int)kNumPhases);
-    for (int i = 0; i < k; ++i) out[i] = i == 0 ? g_calls : g_phase_us[i - 1];
+    // [calls, 6 phase times, host fences, host refills, device fence
+    // checks, device fences that missed an XCD]
+    double all[1 + kNumPhases + 4] = {g_calls};
+    for (int i = 0; i < kNumPhases; ++i) all[1 + i] = g_phase_us[i];
+    unsigned long long dev[2] = {0, 0};
+    if (g_fence.dev_stats) {
+        SHMX_HIP(hipDeviceSynchronize());
+        SHMX_HIP(hipMemcpy(dev, g_fence.dev_stats, sizeof dev, hipMemcpyDeviceToHost));
+    }
+    all[1 + kNumPhases] = g_fence.host_checks;
+    all[2 + kNumPhases] = g_fence.host_refills;
+    all[3 + kNumPhases] = (double)dev[0];
+    all[4 + kNumPhases] = (double)dev[1];
+    const int k = std::min(nout, (int)(sizeof all / sizeof all[0]));
+    for (int i = 0; i < k; ++i) out[i] = all[i];
     if (reset) {
         g_calls = 0;
         for (double &v : g_phase_us) v = 0;
+        g_fence.host_checks = g_fence.host_refills = 0;
+        if (g_fence.dev_stats) SHMX_HIP(hipMemset(g_fence.dev_stats, 0, sizeof dev));
     }
     return k;
 }
@@ -173,6 +254,12 @@ char *ipc_scratch(size_t *bytes) {
 }
 
 void direct_release() {
+    if (g_fence.host_seen) {
+        (void)hipHostFree(g_fence.host_seen);
+        (void)hipFree(g_fence.dev_seen);
+        (void)hipFree(g_fence.dev_stats);
+        g_fence = FenceState{};
+    }
     if (!g_scratch.base) return;
     node::unpublish(node::kScratch);
     (void)hipFree(g_scratch.base);

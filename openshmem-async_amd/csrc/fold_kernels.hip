@@ -532,16 +532,49 @@ __global__ __launch_bounds__(kBlock) void gather_kernel(GatherArgs a) {
     }
 }
 
-// Workgroups are dispatched round-robin over the 8 XCDs, so 64 one-wave
-// blocks put 8 on every XCD; the fence of any one of them covers that XCD's
-// L2 (the per-XCD L2s are not coherent with each other or with the peers).
-constexpr int kFenceBlocks = 64;
+// The per-XCD L2s are not coherent with each other or with the peers, so a
+// system-scope fence must run on EVERY XCD.  Dispatch spreads workgroups
+// round-robin over the XCDs in practice, so 64 one-wave blocks put 8 on each
+// — but the block -> XCD map is not architecturally defined, so each block
+// also records the XCD it ran on (HW_REG_XCC_ID) in seen[blockIdx.x]: the host
+// (fence_and_wait) or the next signal_kernel checks that every XCD of the
+// device reported, and refills or fails loudly if one did not.
+// s_getreg_b32 hwreg(HW_REG_XCC_ID, 0, 4): id 20, offset 0, size 4
+constexpr int kXccIdReg = 20 | (0 << 6) | ((4 - 1) << 11);
 
-__global__ __launch_bounds__(64) void sys_fence_kernel() {
-    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");   // system scope
+__global__ __launch_bounds__(64) void sys_fence_kernel(unsigned int *seen) {
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");   // system scope
+        const unsigned int xcc = (unsigned int)__builtin_amdgcn_s_getreg(kXccIdReg) & 15u;
+        __hip_atomic_store(seen + blockIdx.x, kFenceSeen | xcc, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+__device__ __forceinline__ void check_fence(const SignalArgs &a) {
+    // lane b reads block b's record of the fence just before this kernel
+    const int lane = threadIdx.x;
+    unsigned int rec = 0;
+    if (a.seen && lane < kFenceBlocks) {
+        rec = __hip_atomic_load(a.seen + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(a.seen + lane, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (!a.seen) return;
+    int covered = 0;
+#pragma unroll
+    for (unsigned int x = 0; x < 16; ++x)
+        covered += __ballot(rec == (kFenceSeen | x)) != 0 ? 1 : 0;
+    if (lane == 0) {
+        atomicAdd(a.fence_stats, 1ull);
+        if (covered < a.nxcc) {
+            atomicAdd(a.fence_stats + 1, 1ull);
+            __hip_atomic_store(a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
 
 __global__ __launch_bounds__(64) void signal_kernel(SignalArgs a) {
+    check_fence(a);
     const int i = threadIdx.x;
     if (i >= a.P || a.pe[i] == a.me) return;
     unsigned long long *mine = a.mine + a.pe[i];
@@ -569,8 +602,9 @@ hipError_t launch_signal(const SignalArgs &a, hipStream_t stream) {
     return hipGetLastError();
 }
 
-hipError_t launch_sys_fence(hipStream_t stream) {
-    hipLaunchKernelGGL(sys_fence_kernel, dim3(kFenceBlocks), dim3(64), 0, stream);
+hipError_t launch_sys_fence(hipStream_t stream, unsigned int *seen) {
+    if (!seen) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(sys_fence_kernel, dim3(kFenceBlocks), dim3(64), 0, stream, seen);
     return hipGetLastError();
 }
 

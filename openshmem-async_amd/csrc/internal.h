@@ -37,7 +37,13 @@ hipError_t launch_gather(const void *const *srcs, void *const *dsts, const size_
 // this GPU's writes become visible to peers reading its HBM over xGMI, and
 // no line of a peer's memory cached here survives into the next kernel.
 // Enqueued before every host barrier that hands data between GPUs.
-hipError_t launch_sys_fence(hipStream_t stream);
+// Each of the kFenceBlocks blocks stores kFenceSeen | (its XCC id) into
+// seen[block] (system scope), so the reader can prove every XCD fenced:
+// fence_and_wait (host, seen host-coherent) or the next signal_kernel (seen
+// in device memory; it also clears the records).
+constexpr int kFenceBlocks = 64;
+constexpr unsigned int kFenceSeen = 0x100u;
+hipError_t launch_sys_fence(hipStream_t stream, unsigned int *seen);
 
 // Device-side barrier of the SIGNAL algorithm (signal.cpp): the reference's
 // linear barrier (barrier-linear.c:51-77: every member bumps a counter of
@@ -57,7 +63,13 @@ struct SignalArgs {
     int pe[kMaxFoldInputs];
     int P, me;
     unsigned long long timeout_ticks;
-    unsigned int *err;   // host-mapped
+    unsigned int *err;   // host-mapped: 1 = a peer timed out, 2 = a fence missed an XCD
+    // the preceding launch_sys_fence's records (device memory, kFenceBlocks
+    // words): fewer than nxcc distinct XCDs sets *err = 2.  fence_stats[0] +=
+    // 1 per check, fence_stats[1] += 1 per incomplete fence (device memory).
+    unsigned int *seen;
+    int nxcc;
+    unsigned long long *fence_stats;
 };
 hipError_t launch_signal(const SignalArgs &a, hipStream_t stream);
 

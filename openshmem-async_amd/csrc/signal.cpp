@@ -7,8 +7,10 @@
 // counters, then a wait until the local counter has heard from every peer).
 // Here each barrier is two stream-ordered launches:
 //   launch_sys_fence  every XCD writes back its L2 and drops stale peer lines
-//                     (this GPU's results become visible over xGMI);
-//   launch_signal     one wave bumps this PE's per-peer counters in its own
+//                     (this GPU's results become visible over xGMI); each
+//                     block records its XCD;
+//   launch_signal     one wave checks that the fence reached every XCD (else
+//                     the call fails loudly: error word 2), then bumps this PE's per-peer counters in its own
 //                     signal area (system-scope stores) and polls the peers'
 //                     counters for it over xGMI (system-scope loads);
 // the counters live at the top of every PE's heap segment
@@ -77,11 +79,11 @@ unsigned int *error_word() {
 
 }  // namespace
 
-bool signal_timed_out() {
+unsigned int signal_error() {
     volatile unsigned int *w = error_word();
-    const bool bad = *w != 0;
+    const unsigned int e = *w;
     *w = 0;
-    return bad;
+    return e;
 }
 
 int signal_reduce(int type, int op, char *tgt, const char *src, int nreduce, int start,
@@ -112,6 +114,10 @@ int signal_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     sa.me = g_state.pe;
     sa.timeout_ticks = timeout_ticks();
     sa.err = error_word();
+    const FenceRecords fr = fence_records();
+    sa.seen = fr.seen;
+    sa.nxcc = fr.nxcc;
+    sa.fence_stats = fr.stats;
     const uint64_t sig = heap::signal_offset();
     for (int i = 0; i < P; ++i) {
         const int q = start + i * step;
@@ -120,7 +126,7 @@ int signal_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
         sa.peer[i] = reinterpret_cast<const unsigned long long *>(hb[i] + sig);
     }
     auto barrier = [&] {
-        SHMX_HIP(launch_sys_fence(s));
+        SHMX_HIP(launch_sys_fence(s, sa.seen));
         SHMX_HIP(launch_signal(sa, s));
     };
     const void *ins[kMaxFoldInputs];

@@ -177,7 +177,11 @@ void reduce_blocking(int type, int op, void *target, const void *source,
     if (tdev && sdev) {
         reduce_device(type, op, target, source, nreduce, start, logstride, size, g_state.algo, s);
         SHMX_HIP(hipStreamSynchronize(s));
-        if (signal_timed_out()) fatal("SIGNAL reduction", "a member never reached the device barrier");
+        switch (signal_error()) {
+        case 0: break;
+        case 2: fatal("SIGNAL reduction", "a system fence before a device barrier missed an XCD");
+        default: fatal("SIGNAL reduction", "a member never reached the device barrier");
+        }
         return;
     }
     // Host-resident symmetric arrays (the reference's heap): stage over PCIe

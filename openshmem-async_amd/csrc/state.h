@@ -104,8 +104,19 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
 void direct_release();
 // This PE's IPC scratch region (allocated and published on first use).
 char *ipc_scratch(size_t *bytes);
-// Hand data between the members' GPUs: system-scope fence on every XCD
-// (launch_sys_fence), wait for stream s, then the host barrier over the set.
+// System-scope fence on every XCD (launch_sys_fence), then wait for stream s;
+// a fence whose blocks did not reach every XCD of the device is run again
+// (logged under SHMEM_LOG_LEVELS=info; counted in shmemx_direct_stats).
+void fence_and_wait(hipStream_t s);
+// The device-side fence records and counters the SIGNAL barrier checks.
+struct FenceRecords {
+    unsigned int *seen;
+    int nxcc;
+    unsigned long long *stats;
+};
+FenceRecords fence_records();
+// Hand data between the members' GPUs: fence_and_wait, then the host barrier
+// over the set.
 // Optionally adds the time spent waiting for the stream (from since_us, a
 // steady-clock stamp in microseconds, if >= 0) and in the barrier.
 void node_sync(int start, int step, int P, hipStream_t s, double *stream_us = nullptr,
@@ -118,8 +129,9 @@ bool map_regions(const std::vector<std::pair<node::Region, int>> &regs, int star
 // stream-ordered and graph-capturable; symmetric-heap operands only.
 int signal_reduce(int type, int op, char *tgt, const char *src, int nreduce, int start,
                   int logstride, const shmemx_plan_t &p, hipStream_t s);
-// After the stream has drained: did a SIGNAL barrier time out?  (Clears it.)
-bool signal_timed_out();
+// After the stream has drained: 0, or 1 if a SIGNAL barrier timed out, 2 if
+// a fence before one missed an XCD.  (Clears it.)
+unsigned int signal_error();
 // DIRECT phase times since the last reset (shmemx_direct_stats).
 int direct_stats(double *out, int nout, bool reset);
 // Broadcast and [f]collect on the IPC transport (ipc_coll.cpp): members pull

@@ -326,13 +326,19 @@ DIRECT_PHASES = ("entry_wait_us", "entry_barrier_us", "fold_us", "fold_barrier_u
                  "gather_us", "exit_barrier_us")
 
 
+FENCE_STATS = ("fences_host", "fence_refills_host", "fences_device", "fences_device_incomplete")
+
+
 def direct_stats(reset: bool = True) -> dict:
-    """shmemx_direct_stats: DIRECT calls since the last reset and the host-side
-    microseconds summed over them per phase."""
-    buf = (ctypes.c_double * (1 + len(DIRECT_PHASES)))()
+    """shmemx_direct_stats: DIRECT calls since the last reset, the host-side
+    microseconds summed over them per phase, and the system-fence coverage
+    counters (fences checked on the host / refilled because a fence missed an
+    XCD; fences checked by the SIGNAL barrier / found incomplete)."""
+    names = DIRECT_PHASES + FENCE_STATS
+    buf = (ctypes.c_double * (1 + len(names)))()
     k = lib().shmemx_direct_stats(buf, len(buf), 1 if reset else 0)
     out = {"calls": buf[0]}
-    out.update({name: buf[i + 1] for i, name in enumerate(DIRECT_PHASES[:max(0, k - 1)])})
+    out.update({name: buf[i + 1] for i, name in enumerate(names[:max(0, k - 1)])})
     return out
 
 

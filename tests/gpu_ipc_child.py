@@ -51,6 +51,8 @@ def active_sets():
         s += [(1, 0, npes - 1), (0, 1, (npes + 1) // 2)]
     if npes >= 4:
         s += [(1, 1, npes // 2)]
+    if npes >= 8:
+        s += [(0, 2, npes // 4), (2, 0, npes - 3)]   # stride 4; an offset run
     return s
 
 
@@ -493,6 +495,65 @@ elif scenario == "configs":
         del got, want
     shm.free(BIG_TGT)
     shm.free(BIG_SRC)
+elif scenario == "configs8":
+    # BASELINE.json's 8-PE workloads as 8 PE processes on the one GPU, through
+    # the blocking drop-in entry points (the reference's peer loop at PE_size
+    # 8, reduce-op.c:219-248): configs[2], double sum over 32 Mi elements, on
+    # DIRECT (auto on this transport), SIGNAL and own-order GATHER; configs[4],
+    # the float sum sweep 4 Ki .. 256 Mi (x4 steps; $CONFIGS8_MAX caps it).
+    # Every PE regenerates all P sources on the GPU and folds them with torch
+    # in the reference's order (PE_start first; GATHER: its own source
+    # first), one IEEE add at a time, so the result must match bit for bit;
+    # shmemx_verify checks the targets agree across the set.
+    maxn = int(os.environ.get("CONFIGS8_MAX", str(256 * 1024 * 1024)))
+    big = max(32 * 1024 * 1024 * 8, maxn * 4)
+    BIG_SRC, BIG_TGT = shm.malloc(big), shm.malloc(big)
+    assert BIG_SRC and BIG_TGT, "shmem_malloc of the config operands failed"
+
+    def gen(t, q, n, salt):
+        g = torch.Generator(device="cuda")
+        g.manual_seed(0x8E8 + 131 * q + salt)
+        dt = torch.float64 if t == "double" else torch.float32
+        return torch.rand(n, dtype=dt, device="cuda", generator=g) + 1.0
+
+    cases = [("double", 32 * 1024 * 1024, algo) for algo in ("auto", "signal", "gather")]
+    n = 4096
+    while n <= maxn:
+        cases.append(("float", n, "auto"))
+        n *= 4
+    cases += [("float", 16 * 1024 * 1024 + 5, "signal"), ("float", 4096 + 3, "gather")]
+    for salt, (t, n, algo) in enumerate(cases):
+        ncases += 1
+        print(f"configs8 {t} sum n={n} algo={algo}", flush=True)
+        dt = torch.float64 if t == "double" else torch.float32
+        sz = 8 if t == "double" else 4
+        shm.memcpy(BIG_SRC, gen(t, pe, n, salt), n * sz)
+        shm.memcpy(BIG_TGT, torch.zeros(n, dtype=dt, device="cuda"), n * sz)
+        torch.cuda.synchronize()
+        shm.set_algo(algo)
+        shm.to_all(t, "sum", BIG_TGT, BIG_SRC, n, 0, 0, npes)
+        shm.set_algo("auto")
+        if shm.last_error():
+            fails.append(f"configs8 {t} n={n} {algo}: last_error {shm.last_error()}")
+            continue
+        got = torch.empty(n, dtype=dt, device="cuda")
+        shm.memcpy(got, BIG_TGT, n * sz)
+        order = list(range(npes))
+        if algo == "gather":
+            order = [pe] + [q for q in order if q != pe]
+        want = gen(t, order[0], n, salt)
+        for q in order[1:]:
+            want = want + gen(t, q, n, salt)
+        torch.cuda.synchronize()
+        iv = torch.int64 if t == "double" else torch.int32
+        if not torch.equal(got.view(iv), want.view(iv)):
+            bad = int((got.view(iv) != want.view(iv)).sum())
+            fails.append(f"configs8 {t} n={n} {algo}: {bad} elements differ")
+        if algo != "gather" and not shm.verify(t, BIG_TGT, n, 0, 0, npes):
+            fails.append(f"configs8 {t} n={n} {algo}: targets differ across PEs")
+        del got, want
+    shm.free(BIG_TGT)
+    shm.free(BIG_SRC)
 elif scenario == "signal_timeout":
     # one SIGNAL call together (maps and votes), then PE 0 calls again alone:
     # its device barrier must give up after $SHMEMX_SIGNAL_TIMEOUT seconds and
@@ -514,8 +575,14 @@ elif scenario == "signal_timeout":
 else:
     raise SystemExit(f"unknown scenario {scenario}")
 
+# every system fence that handed data between PEs reached every XCD: none
+# had to be run again (host paths) or failed its check (SIGNAL barrier)
+stats = shm.direct_stats(reset=False)
+fences = {k: stats[k] for k in shm.FENCE_STATS}
+if fences["fence_refills_host"] or fences["fences_device_incomplete"]:
+    fails.append(f"system fences missed an XCD: {fences}")
 shm.free(HEAP_TGT)
 shm.free(HEAP_SRC)
 shm.finalize()
 with open(out_path, "w") as f:
-    json.dump({"pe": pe, "fails": fails, "ncases": ncases}, f)
+    json.dump({"pe": pe, "fails": fails, "ncases": ncases, "fences": fences}, f)

@@ -172,8 +172,9 @@ def test_plan_shards_cover_and_align(shm, t, P_, n):
 
 def test_direct_stats_without_calls(shm):
     """shmemx_direct_stats is host-only bookkeeping: no DIRECT call yet means
-    zero calls and zero time in every phase, and it never needs a device."""
+    zero calls, zero time in every phase and no fences checked, and it never
+    needs a device."""
     st = shm.direct_stats(reset=True)
     assert st["calls"] == 0
-    assert set(st) == {"calls", *shm.DIRECT_PHASES}
+    assert set(st) == {"calls", *shm.DIRECT_PHASES, *shm.FENCE_STATS}
     assert all(v == 0 for v in st.values())

@@ -66,8 +66,17 @@ def run_pes(tmp_path, npes, scenario, extra_env=None, timeout=900):
     return reports
 
 
+def fences_checked(reports, device=False):
+    """Every PE ran system fences and each reached every XCD the first time
+    (the child fails a PE whose fence needed a refill or failed its check)."""
+    key = "fences_device" if device else "fences_host"
+    for r in reports:
+        assert r["fences"][key] > 0, f"PE {r['pe']}: no {key}: {r['fences']}"
+        assert r["fences"]["fence_refills_host"] == 0 and r["fences"]["fences_device_incomplete"] == 0
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("npes", [2, 4])
+@pytest.mark.parametrize("npes", [2, 4, 8])
 @pytest.mark.parametrize("shots", ["auto", "two"])
 def test_ipc_transport_all_pairs_sets_placements(tmp_path, npes, shots):
     # "auto": arrays up to 256 KiB take DIRECT's one-shot path; "two": every
@@ -78,10 +87,26 @@ def test_ipc_transport_all_pairs_sets_placements(tmp_path, npes, shots):
     for r in reports:
         assert r["ncases"] > 0
         assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
+    fences_checked(reports)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("npes", [2, 3, 4])
+def test_ipc_eight_pe_baseline_configs(tmp_path):
+    """BASELINE.json configs[2] (double sum, 32 Mi, 8 PEs) on DIRECT, SIGNAL
+    and own-order GATHER, and configs[4] (float sum sweep 4 Ki .. 256 Mi, 8
+    PEs), as 8 PE processes sharing the GPU through the blocking drop-in entry
+    points: bit-exact against torch's fold of the regenerated sources in the
+    reference's order, identical across PEs, every fence on every XCD."""
+    reports = run_pes(tmp_path, 8, "configs8", timeout=900)
+    for r in reports:
+        assert r["ncases"] == 14
+        assert not r["fails"], f"PE {r['pe']}: {r['fails']}"
+    fences_checked(reports)
+    fences_checked(reports, device=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("npes", [2, 3, 4, 8])
 def test_rccl_transport_with_rccl_double(tmp_path, npes):
     """The default RCCL transport across PE processes on the one GPU, with
     the RCCL test double (tests/native/fake_rccl.cpp) in place of librccl:
@@ -101,7 +126,7 @@ def test_rccl_transport_with_rccl_double(tmp_path, npes):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("transport,npes", [("ipc", 3), ("rccl", 4)])
+@pytest.mark.parametrize("transport,npes", [("ipc", 3), ("rccl", 4), ("ipc", 8), ("rccl", 8)])
 def test_soak_random_calls(tmp_path, transport, npes):
     """Random collective calls, the same seeded sequence on every PE: any
     reference pair, size (edges favoured), active set, algorithm the transport
@@ -171,7 +196,7 @@ def test_isx_c_program_four_pes(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("npes", [2, 3, 4])
+@pytest.mark.parametrize("npes", [2, 3, 4, 8])
 def test_ipc_signal_device_barriers(tmp_path, npes):
     """SIGNAL: DIRECT's pulls with device-side barriers (counters in the
     heap segments, polled across processes), stream-ordered: every reference
@@ -181,6 +206,7 @@ def test_ipc_signal_device_barriers(tmp_path, npes):
     for r in reports:
         assert r["ncases"] > 0
         assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
+    fences_checked(reports, device=True)
 
 
 @pytest.mark.gpu
