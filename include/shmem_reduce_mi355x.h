@@ -275,6 +275,13 @@ int shmemx_fold_n_on_stream(int type, int op, void *out,
                             const void *const *ins, int nins, size_t nelems,
                             void *stream);
 
+/* DIRECT's all-gather step as one launch: nseg (<= 16) byte ranges
+ * srcs[i] -> dsts[i] copied concurrently (blockIdx.y = segment), so reads
+ * from every peer's HBM are in flight at once.  Device (or IPC-mapped peer)
+ * pointers, stream-ordered; ranges must not overlap. */
+int shmemx_gather_on_stream(const void *const *srcs, void *const *dsts,
+                            const size_t *bytes, int nseg, void *stream);
+
 /* Fold-kernel launch shape (defaults from $SHMEMX_FOLD_MAX_BLOCKS,
  * $SHMEMX_FOLD_NT, $SHMEMX_FOLD_UNROLL): grid cap (0 = no cap), non-temporal
  * mode (-1 = by size, the default: both non-temporal once the arrays exceed
@@ -350,9 +357,11 @@ const char *shmemx_reduce_error_string(int err);
  * SHMEM_LOG_FATAL exits it (trace.c:424-427); so do GPU memory faults (HSA)
  * and a launcher's SIGTERM when another PE died.  A caller holding a result
  * it must not lose registers it here: on SIGABRT, SIGSEGV, SIGBUS, SIGFPE,
- * SIGILL or SIGTERM the text is written to stdout and the process leaves with
- * _exit(exit_code).  Calling again replaces the text; NULL uninstalls and
- * restores the previous handlers.  SHMEMX_OK or SHMEMX_ENOMEM. */
+ * SIGILL or SIGTERM the text is written to stdout and the process leaves
+ * with _exit: exit_code for SIGTERM, 128 + the signal number for the others
+ * (a crash stays visible in the exit status).  Calling again replaces the
+ * text; NULL uninstalls and restores the previous handlers.  SHMEMX_OK or
+ * SHMEMX_ENOMEM. */
 int shmemx_set_fatal_note(const char *text, int exit_code);
 
 /* Typed stream-ordered forms of the 44 entry points. */

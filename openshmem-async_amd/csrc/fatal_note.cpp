@@ -7,8 +7,12 @@
 // lose (bench.py's headline line, measured and verified before its optional
 // extras run) registers that text here: on SIGABRT/SIGSEGV/SIGBUS/SIGFPE/
 // SIGILL/SIGTERM the handler writes it to stdout with write(2) and leaves with
-// _exit(exit_code) — both async-signal-safe, from whichever thread took the
-// signal.  Registering NULL restores the previous dispositions.
+// _exit — both async-signal-safe, from whichever thread took the signal.  The
+// exit status still says what happened: 128 + the signal number for a crash
+// of this process (SIGABRT: a FATAL line or a GPU fault; SIGSEGV, SIGBUS,
+// SIGFPE, SIGILL), the registered exit_code only for SIGTERM (the launcher
+// stopping a healthy rank because another one died).  Registering NULL
+// restores the previous dispositions.
 //
 // A note is one immutable block published by a single atomic pointer store,
 // so a handler running on another thread sees either the old note or the new
@@ -40,7 +44,7 @@ std::atomic<int> g_fired{0};
 
 void on_fatal(int sig) {
     const Note *n = g_note.load(std::memory_order_acquire);
-    const int code = n ? n->exit_code : 128 + sig;
+    const int code = (n && sig == SIGTERM) ? n->exit_code : 128 + sig;
     if (g_fired.exchange(1)) _exit(code);     // a second signal while writing
     const char *p = n ? n->text : nullptr;
     size_t left = n ? n->len : 0;

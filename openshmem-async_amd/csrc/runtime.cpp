@@ -855,6 +855,18 @@ int shmemx_fold_n_on_stream(int type, int op, void *out, const void *const *ins,
     return SHMEMX_OK;
 }
 
+int shmemx_gather_on_stream(const void *const *srcs, void *const *dsts, const size_t *bytes,
+                            int nseg, void *stream) {
+    t_last_error = SHMEMX_OK;
+    if (nseg < 0 || nseg > kMaxFoldInputs || (nseg > 0 && (!srcs || !dsts || !bytes)))
+        return set_error(SHMEMX_EINVAL);
+    for (int i = 0; i < nseg; ++i)
+        if (bytes[i] && overlap(srcs[i], dsts[i], bytes[i])) return set_error(SHMEMX_EINVAL);
+    if (launch_gather(srcs, dsts, bytes, nseg, static_cast<hipStream_t>(stream)) != hipSuccess)
+        return set_error(SHMEMX_EINVAL);
+    return SHMEMX_OK;
+}
+
 int shmemx_reduce_plan(int type, int op, int nreduce, int PE_start,
                        int logPE_stride, int PE_size, int pe, int npes,
                        int algo, shmemx_plan_t *plan) {

@@ -80,6 +80,9 @@ def lib() -> ctypes.CDLL:
     L.shmemx_fold_on_stream.restype = i
     L.shmemx_fold_n_on_stream.argtypes = [i, i, vp, ctypes.POINTER(vp), i, sz, vp]
     L.shmemx_fold_n_on_stream.restype = i
+    L.shmemx_gather_on_stream.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                          ctypes.POINTER(sz), i, vp]
+    L.shmemx_gather_on_stream.restype = i
     L.shmemx_reduce_plan.argtypes = [i, i, i, i, i, i, i, i, i, ctypes.POINTER(Plan)]
     L.shmemx_reduce_plan.restype = i
     L.shmemx_get_uniqueid.argtypes = [vp]
@@ -252,6 +255,16 @@ def fold_n(type_name: str, op: str, out, ins, nelems: int, stream: int = 0) -> N
     _check(rc, f"shmemx_fold_n_on_stream({type_name},{op})")
 
 
+def gather(srcs, dsts, nbytes, stream: int = 0) -> None:
+    """shmemx_gather_on_stream: copy byte ranges srcs[i] -> dsts[i] in one
+    launch (DIRECT's all-gather kernel)."""
+    k = len(srcs)
+    a = (ctypes.c_void_p * k)(*[addr(x) for x in srcs])
+    b = (ctypes.c_void_p * k)(*[addr(x) for x in dsts])
+    c = (ctypes.c_size_t * k)(*nbytes)
+    _check(lib().shmemx_gather_on_stream(a, b, c, k, stream or None), "shmemx_gather_on_stream")
+
+
 @dataclass
 class PlanInfo:
     algo: str
@@ -353,9 +366,9 @@ def host_unregister(buf) -> None:
 
 
 def set_fatal_note(text: str | None, exit_code: int = 1) -> None:
-    """shmemx_set_fatal_note: text written to stdout (then _exit(exit_code))
-    if the process dies on SIGABRT/SIGSEGV/SIGBUS/SIGFPE/SIGILL/SIGTERM; None
-    uninstalls."""
+    """shmemx_set_fatal_note: text written to stdout if the process dies on
+    SIGABRT/SIGSEGV/SIGBUS/SIGFPE/SIGILL/SIGTERM, then _exit(exit_code) for
+    SIGTERM and _exit(128 + signal) for the others; None uninstalls."""
     raw = None if text is None else text.encode()
     _check(lib().shmemx_set_fatal_note(raw, exit_code), "shmemx_set_fatal_note")
 

@@ -30,13 +30,18 @@ def run_child(sig, text="line {\"value\": 1}\n", code=7, uninstall=False):
 
 @pytest.mark.parametrize("sig", ["SIGABRT", "SIGSEGV", "SIGTERM", "SIGBUS"])
 def test_note_written_on_fatal_signal(sig):
+    """The note is printed on every fatal signal; a crash of this process
+    still exits 128 + signal (a GPU fault during bench extras must not read
+    as success), only the launcher's SIGTERM takes the registered code."""
+    import signal
     r = run_child(sig)
-    assert r.returncode == 7, r.stderr
+    want = 7 if sig == "SIGTERM" else 128 + int(getattr(signal, sig))
+    assert r.returncode == want, r.stderr
     assert r.stdout == 'before\nline {"value": 1}\n'
 
 
 def test_empty_note_only_sets_exit_code():
-    r = run_child("SIGABRT", text="", code=0)
+    r = run_child("SIGTERM", text="", code=0)
     assert r.returncode == 0, r.stderr
     assert r.stdout == "before\n"
 

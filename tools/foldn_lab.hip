@@ -8,11 +8,14 @@
 //               input k is folded
 //   st<P,U>     nins fixed at compile time: every input's loads issued first
 //   pred<U>     up to 8 inputs, loads under uniform (scalar) predicates, so
-//               they all issue up front for any nins <= 8
+//               they all issue up front for any nins <= 8 (round 2: 3.2-5.6
+//               TB/s, dropped from the list)
+//   rdonly<U>   rt's loads only (reads ceiling for P streams; rdonly's
+//               GB/s counts the P input streams plus the never-written output)
 // Timed with HIP events, interleaved rounds, warm (back to back) and cold
 // (a 1 GiB scratch rewritten before every launch).
 //   Build: hipcc --offload-arch=gfx950 -O3 tools/foldn_lab.hip -o tools/foldn_lab
-//   Run:   tools/foldn_lab <n per input> <cold 0|1>
+//   Run:   tools/foldn_lab <n per input> <cold 0|1> [skew bytes, -1 = separate]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -114,6 +117,26 @@ __global__ __launch_bounds__(B) void pred(f64x2 *out, Ins in, int P) {
     for (int u = 0; u < U; ++u) st(out + v0 + u * B, x[0][u]);
 }
 
+// read-only ceiling: the P inputs are loaded and folded, the result stored
+// only where it can never be true (keeps the loads alive)
+template <int U>
+__global__ __launch_bounds__(B) void rdonly(f64x2 *out, Ins in, int P) {
+    const size_t v0 = (size_t)blockIdx.x * B * U + threadIdx.x;
+    f64x2 acc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u] = ld(in.p[0] + v0 + u * B);
+    for (int k = 1; k < P; ++k) {
+        f64x2 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = ld(in.p[k] + v0 + u * B);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u] += x[u];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (acc[u].x == -1.0) st(out + v0 + u * B, acc[u]);
+}
+
 __global__ void flush(f64x2 *p, size_t n, double v) {
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
         p[i] = f64x2{v, v};
@@ -137,19 +160,26 @@ void add_static(std::vector<Var> &v) {
 int main(int argc, char **argv) {
     const size_t n = argc > 1 ? strtoull(argv[1], nullptr, 0) : (size_t(4) << 20);
     const int cold = argc > 2 ? atoi(argv[2]) : 0;
+    // skew < 0: every input its own hipMalloc; else all inputs in one block at
+    // k * (n * 8 + skew) bytes (the A2A workspace layout when skew = 0)
+    const long skew = argc > 3 ? atol(argv[3]) : -1;
     const size_t nvec = n / 2;
     std::vector<f64x2 *> bufs(MAXP + 1);
-    for (auto &b : bufs) {
-        CK(hipMalloc(&b, n * 8));
-        hipLaunchKernelGGL(flush, dim3(4096), dim3(256), 0, 0, b, nvec, 1.0);
+    if (skew < 0) {
+        for (auto &b : bufs) CK(hipMalloc(&b, n * 8));
+    } else {
+        char *blk = nullptr;
+        CK(hipMalloc(&blk, (MAXP + 1) * (n * 8 + (size_t)skew)));
+        for (int k = 0; k <= MAXP; ++k) bufs[k] = reinterpret_cast<f64x2 *>(blk + k * (n * 8 + (size_t)skew));
     }
+    for (auto &b : bufs) hipLaunchKernelGGL(flush, dim3(4096), dim3(256), 0, 0, b, nvec, 1.0);
     f64x2 *scratch = nullptr;
     const size_t sn = (size_t(1) << 30) / 16;
     CK(hipMalloc(&scratch, sn * 16));
     CK(hipDeviceSynchronize());
     std::vector<Var> vars = {{"rt_u4", rt<4>, 4, 0}, {"rt_u2", rt<2>, 2, 0},
                              {"pipe_u4", pipe<4>, 4, 0}, {"pipe_u2", pipe<2>, 2, 0},
-                             {"pred_u1", pred<1>, 1, 0}, {"pred_u2", pred<2>, 2, 0}};
+                             {"rdonly_u4", rdonly<4>, 4, 0}};
     add_static<3>(vars);
     add_static<4>(vars);
     add_static<6>(vars);
@@ -157,6 +187,7 @@ int main(int argc, char **argv) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
+    printf("# skew %ld (%s)\n", skew, skew < 0 ? "separate allocations" : "one block, inputs k*(n*8+skew) apart");
     printf("# n=%zu per input, %s; GB/s = (P+1)*n*8 / launch time (median of rounds)\n", n,
            cold ? "cold (1 GiB scratch rewritten before each launch)" : "warm (back to back)");
     for (int P : {3, 4, 6, 8}) {
@@ -192,7 +223,7 @@ int main(int argc, char **argv) {
                                bufs[MAXP], in, P);
             double h[4];
             CK(hipMemcpy(h, reinterpret_cast<double *>(bufs[MAXP]) + n - 4, sizeof h, hipMemcpyDeviceToHost));
-            const bool ok = h[3] == (double)P;
+            const bool ok = h[3] == (double)P || v.k == rdonly<4>;
             std::sort(t[vi].begin(), t[vi].end());
             const double ms = t[vi][t[vi].size() / 2];
             printf("P=%d %-8s %8.1f us %7.1f GB/s %s\n", P, v.name, ms * 1e3,

@@ -1,0 +1,83 @@
+"""Join tools/pmc_kernels.py's timing lines with its rocprofv3 passes.
+
+usage: summarize_pmc.py <pmc_kernels.log> <trace_dir> <fetch_dir> <write_dir> <out.json>
+
+Dispatches of the library's kernels (names under shmx::) are taken in
+dispatch order and cut into runs of consecutive launches of one (kernel, grid
+size); run i belongs to the i-th config line of the log (the script launches
+each config's kernel back to back).  HBM bytes per launch = 2 * FETCH_SIZE +
+WRITE_SIZE (KiB; FETCH_SIZE doubled per MI355X_MICROARCH.md "HBM": gfx950
+counts half of a wide streaming read), compared with the algorithmic bytes.
+"""
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+
+
+def rows(d, pat):
+    out = []
+    for f in sorted(glob.glob(os.path.join(d, "**", pat), recursive=True)):
+        with open(f) as fh:
+            out += list(csv.DictReader(fh))
+    return out
+
+
+def runs(d, counter):
+    """[(kernel, grid, [values...])] in dispatch order."""
+    got = [r for r in rows(d, "*counter_collection.csv")
+           if r.get("Counter_Name") == counter and "shmx" in r.get("Kernel_Name", "")]
+    got.sort(key=lambda r: int(r["Dispatch_Id"]))
+    out = []
+    for r in got:
+        key = (r["Kernel_Name"], r.get("Grid_Size", ""))
+        if out and out[-1][0] == key:
+            out[-1][1].append(float(r["Counter_Value"]))
+        else:
+            out.append((key, [float(r["Counter_Value"])]))
+    return out
+
+
+def trace_runs(d):
+    got = [r for r in rows(d, "*kernel_trace.csv") if "shmx" in r.get("Kernel_Name", "")]
+    got.sort(key=lambda r: int(r["Dispatch_Id"]))
+    out = []
+    for r in got:
+        key = (r["Kernel_Name"], r.get("Grid_Size", r.get("Grid_Size_X", "")))
+        us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        if out and out[-1][0] == key:
+            out[-1][1].append(us)
+        else:
+            out.append((key, [us]))
+    return out
+
+
+def main():
+    log, trace, fetch, write, dst = sys.argv[1:6]
+    cfgs = [json.loads(line) for line in open(log) if line.startswith('{"config"')]
+    fr, wr, tr = runs(fetch, "FETCH_SIZE"), runs(write, "WRITE_SIZE"), trace_runs(trace)
+    out = []
+    for i, c in enumerate(cfgs):
+        e = dict(c)
+        if i < len(tr):
+            (name, grid), us = tr[i]
+            e["kernel"] = name[:200]
+            e["grid_size"] = grid
+            e["rocprof_avg_us"] = round(statistics.mean(us[1:] or us), 2)
+        if i < len(fr) and i < len(wr):
+            f = statistics.median(fr[i][1])
+            w = statistics.median(wr[i][1])
+            hbm = 2 * f * 1024 + w * 1024
+            e.update({"FETCH_SIZE_KiB": f, "WRITE_SIZE_KiB": w, "hbm_bytes_per_launch": hbm,
+                      "traffic_over_alg": round(hbm / c["alg_bytes"], 4)})
+        out.append(e)
+    with open(dst, "w") as fh:
+        json.dump({"source": "tools/pmc_kernels.py + rocprofv3 (tools/gpu_pmc_all.sh)",
+                   "configs": out}, fh, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
