@@ -364,18 +364,41 @@ const char *shmemx_reduce_error_string(int err);
  * SHMEMX_ENOMEM. */
 int shmemx_set_fatal_note(const char *text, int exit_code);
 
-/* Typed stream-ordered forms of the 44 entry points. */
+/* Typed stream-ordered forms of all 44 entry points: shmemx_reduce_on_stream
+ * with the type and op in the name, SHMEMX_ALGO_AUTO (or the algorithm set
+ * with shmemx_set_algo / $SHMEM_REDUCE_ALGO).  Return SHMEMX_OK or the error
+ * code (also left in shmemx_reduce_last_error()). */
 #define SHMEMX_DECL_REDUCE_STREAM(Name, Op, T)                                 \
-    void shmemx_##Name##_##Op##_to_all_on_stream(                            \
+    int shmemx_##Name##_##Op##_to_all_on_stream(                             \
         T *target, const T *source, int nreduce, int PE_start,               \
         int logPE_stride, int PE_size, void *stream);
-SHMEMX_DECL_REDUCE_STREAM(double, sum, double)
-SHMEMX_DECL_REDUCE_STREAM(float, sum, float)
-SHMEMX_DECL_REDUCE_STREAM(int, sum, int)
-SHMEMX_DECL_REDUCE_STREAM(long, sum, long)
-SHMEMX_DECL_REDUCE_STREAM(long, and, long)
-SHMEMX_DECL_REDUCE_STREAM(long, or, long)
-SHMEMX_DECL_REDUCE_STREAM(long, xor, long)
+#define SHMEMX_DECL_STREAM_ARITH(Name, T)                                      \
+    SHMEMX_DECL_REDUCE_STREAM(Name, sum, T) SHMEMX_DECL_REDUCE_STREAM(Name, prod, T)
+#define SHMEMX_DECL_STREAM_LOGIC(Name, T)                                      \
+    SHMEMX_DECL_REDUCE_STREAM(Name, and, T) SHMEMX_DECL_REDUCE_STREAM(Name, or, T) \
+    SHMEMX_DECL_REDUCE_STREAM(Name, xor, T)
+#define SHMEMX_DECL_STREAM_MINMAX(Name, T)                                     \
+    SHMEMX_DECL_REDUCE_STREAM(Name, min, T) SHMEMX_DECL_REDUCE_STREAM(Name, max, T)
+SHMEMX_DECL_STREAM_ARITH(short, short)
+SHMEMX_DECL_STREAM_ARITH(int, int)
+SHMEMX_DECL_STREAM_ARITH(long, long)
+SHMEMX_DECL_STREAM_ARITH(longlong, long long)
+SHMEMX_DECL_STREAM_ARITH(float, float)
+SHMEMX_DECL_STREAM_ARITH(double, double)
+SHMEMX_DECL_STREAM_ARITH(longdouble, long double)
+SHMEMX_DECL_STREAM_ARITH(complexd, SHMEMX_COMPLEX(double))
+SHMEMX_DECL_STREAM_ARITH(complexf, SHMEMX_COMPLEX(float))
+SHMEMX_DECL_STREAM_LOGIC(short, short)
+SHMEMX_DECL_STREAM_LOGIC(int, int)
+SHMEMX_DECL_STREAM_LOGIC(long, long)
+SHMEMX_DECL_STREAM_LOGIC(longlong, long long)
+SHMEMX_DECL_STREAM_MINMAX(short, short)
+SHMEMX_DECL_STREAM_MINMAX(int, int)
+SHMEMX_DECL_STREAM_MINMAX(long, long)
+SHMEMX_DECL_STREAM_MINMAX(longlong, long long)
+SHMEMX_DECL_STREAM_MINMAX(float, float)
+SHMEMX_DECL_STREAM_MINMAX(double, double)
+SHMEMX_DECL_STREAM_MINMAX(longdouble, long double)
 
 #ifdef __cplusplus
 }

@@ -283,18 +283,16 @@ int checksum_impl(int type, const void *ptr, size_t nelems, unsigned long long *
     return SHMEMX_OK;
 }
 
-int verify_impl(int type, const void *target, int nreduce, int start, int logstride, int size,
-                int *all_equal) {
-    std::lock_guard<std::recursive_mutex> lk(g_mu);
-    clear_error();
+}  // namespace
+
+// Every member's 8-byte value, in set order (a collective over the set).
+int exchange_u64(int start, int logstride, int size, unsigned long long mine,
+                 std::vector<unsigned long long> &all) {
     SetInfo si;
     if (int rc = set_info(start, logstride, size, si)) return rc;
-    if (!all_equal || nreduce < 0) return set_error(SHMEMX_EINVAL);
-    unsigned long long mine = 0;
-    if (int rc = checksum_impl(type, target, (size_t)nreduce, &mine)) return rc;
-    std::vector<unsigned long long> all(si.P, mine);
+    all.assign(si.P, mine);
     if (collective(si) && !g_state.comm) {
-        // IPC transport: the checksums travel in the node block's descriptors
+        // IPC transport: the values travel in the node block's descriptors
         node::Desc d;
         d.aux = mine;
         node::put_desc(d);
@@ -322,6 +320,22 @@ int verify_impl(int type, const void *target, int nreduce, int start, int logstr
                                 hipMemcpyDeviceToHost, s));
         SHMX_HIP(hipStreamSynchronize(s));
     }
+    return SHMEMX_OK;
+}
+
+namespace {
+
+int verify_impl(int type, const void *target, int nreduce, int start, int logstride, int size,
+                int *all_equal) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    clear_error();
+    SetInfo si;
+    if (int rc = set_info(start, logstride, size, si)) return rc;
+    if (!all_equal || nreduce < 0) return set_error(SHMEMX_EINVAL);
+    unsigned long long mine = 0;
+    if (int rc = checksum_impl(type, target, (size_t)nreduce, &mine)) return rc;
+    std::vector<unsigned long long> all;
+    if (int rc = exchange_u64(start, logstride, size, mine, all)) return rc;
     int eq = 1;
     for (unsigned long long v : all) eq &= v == mine;
     *all_equal = eq;

@@ -111,22 +111,46 @@ SHMX_FORTRAN(sum, comp8, complexd, std::complex<double>)
 SHMX_FORTRAN(prod, comp4, complexf, std::complex<float>)
 SHMX_FORTRAN(prod, comp8, complexd, std::complex<double>)
 
-// Stream-ordered typed forms (header Part 3).
+// Stream-ordered typed forms of all 44 (header Part 3): the error code is
+// returned (and left in shmemx_reduce_last_error()).
 #define SHMX_STREAM(Name, Op, T, TYPE, OPC)                                    \
-    void shmemx_##Name##_##Op##_to_all_on_stream(                            \
+    int shmemx_##Name##_##Op##_to_all_on_stream(                             \
         T *target, const T *source, int nreduce, int PE_start,               \
         int logPE_stride, int PE_size, void *stream)                         \
     {                                                                        \
-        shmx::reduce_on_stream(TYPE, OPC, target, source, nreduce, PE_start, \
-                               logPE_stride, PE_size, SHMEMX_ALGO_AUTO,      \
-                               stream);                                      \
+        return shmx::reduce_on_stream(TYPE, OPC, target, source, nreduce,    \
+                                      PE_start, logPE_stride, PE_size,       \
+                                      SHMEMX_ALGO_AUTO, stream);             \
     }
-SHMX_STREAM(double, sum, double, SHMEMX_TYPE_DOUBLE, SHMEMX_OP_SUM)
-SHMX_STREAM(float, sum, float, SHMEMX_TYPE_FLOAT, SHMEMX_OP_SUM)
-SHMX_STREAM(int, sum, int, SHMEMX_TYPE_INT, SHMEMX_OP_SUM)
-SHMX_STREAM(long, sum, long, SHMEMX_TYPE_LONG, SHMEMX_OP_SUM)
-SHMX_STREAM(long, and, long, SHMEMX_TYPE_LONG, SHMEMX_OP_AND)
-SHMX_STREAM(long, or, long, SHMEMX_TYPE_LONG, SHMEMX_OP_OR)
-SHMX_STREAM(long, xor, long, SHMEMX_TYPE_LONG, SHMEMX_OP_XOR)
+#define SHMX_STREAM_ARITH(Name, T, TYPE)                                       \
+    SHMX_STREAM(Name, sum, T, TYPE, SHMEMX_OP_SUM)                           \
+    SHMX_STREAM(Name, prod, T, TYPE, SHMEMX_OP_PROD)
+#define SHMX_STREAM_LOGIC(Name, T, TYPE)                                       \
+    SHMX_STREAM(Name, and, T, TYPE, SHMEMX_OP_AND)                           \
+    SHMX_STREAM(Name, or, T, TYPE, SHMEMX_OP_OR)                             \
+    SHMX_STREAM(Name, xor, T, TYPE, SHMEMX_OP_XOR)
+#define SHMX_STREAM_MINMAX(Name, T, TYPE)                                      \
+    SHMX_STREAM(Name, min, T, TYPE, SHMEMX_OP_MIN)                           \
+    SHMX_STREAM(Name, max, T, TYPE, SHMEMX_OP_MAX)
+SHMX_STREAM_ARITH(short, short, SHMEMX_TYPE_SHORT)
+SHMX_STREAM_ARITH(int, int, SHMEMX_TYPE_INT)
+SHMX_STREAM_ARITH(long, long, SHMEMX_TYPE_LONG)
+SHMX_STREAM_ARITH(longlong, long long, SHMEMX_TYPE_LONGLONG)
+SHMX_STREAM_ARITH(float, float, SHMEMX_TYPE_FLOAT)
+SHMX_STREAM_ARITH(double, double, SHMEMX_TYPE_DOUBLE)
+SHMX_STREAM_ARITH(longdouble, long double, SHMEMX_TYPE_LONGDOUBLE)
+SHMX_STREAM_ARITH(complexd, std::complex<double>, SHMEMX_TYPE_COMPLEXD)
+SHMX_STREAM_ARITH(complexf, std::complex<float>, SHMEMX_TYPE_COMPLEXF)
+SHMX_STREAM_LOGIC(short, short, SHMEMX_TYPE_SHORT)
+SHMX_STREAM_LOGIC(int, int, SHMEMX_TYPE_INT)
+SHMX_STREAM_LOGIC(long, long, SHMEMX_TYPE_LONG)
+SHMX_STREAM_LOGIC(longlong, long long, SHMEMX_TYPE_LONGLONG)
+SHMX_STREAM_MINMAX(short, short, SHMEMX_TYPE_SHORT)
+SHMX_STREAM_MINMAX(int, int, SHMEMX_TYPE_INT)
+SHMX_STREAM_MINMAX(long, long, SHMEMX_TYPE_LONG)
+SHMX_STREAM_MINMAX(longlong, long long, SHMEMX_TYPE_LONGLONG)
+SHMX_STREAM_MINMAX(float, float, SHMEMX_TYPE_FLOAT)
+SHMX_STREAM_MINMAX(double, double, SHMEMX_TYPE_DOUBLE)
+SHMX_STREAM_MINMAX(longdouble, long double, SHMEMX_TYPE_LONGDOUBLE)
 
 }  // extern "C"

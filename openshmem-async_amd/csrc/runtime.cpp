@@ -434,6 +434,20 @@ bool overlap(const void *a, const void *b, size_t bytes) {
     return x != y && x < y + bytes && y < x + bytes;
 }
 
+// The reference's own trace messages (reduce-op.c:199-210), from the caller's
+// target and source, before any staging.  Like OVERLAP_CHECK (:166-167) an
+// in-place call counts as overlapping; unlike it, the range is the array's
+// bytes, not its byte count taken as an element count (which only widens the
+// check).
+void trace_reference_overlap(const void *target, const void *source, size_t bytes) {
+    if (!log_enabled(LOG_REDUCTION)) return;
+    const char *t = static_cast<const char *>(target), *s = static_cast<const char *>(source);
+    const bool ov = t < s + bytes && s < t + bytes;
+    trace(LOG_REDUCTION, ov ? "target (%p) and source (%p, size %ld) overlap, using temporary target"
+                            : "target (%p) and source (%p, size %ld) do not overlap",
+          target, source, (long)bytes);
+}
+
 static long long count_of(long long n, long long chunk, int i) {
     const long long lo = chunk * i;
     return std::max(0LL, std::min(chunk, n - lo));
@@ -496,11 +510,6 @@ int reduce_device(int type, int op, void *target, const void *source,
                                                          "allreduce", "direct", "signal"};
         trace(LOG_REDUCTION, "type %d op %d nreduce %d set (%d,%d,%d) member %d algo %s chunk %lld",
               type, op, nreduce, start, logstride, size, p.member, algos[p.algo], p.chunk);
-        // the reference's own messages, reduce-op.c:199-210
-        trace(LOG_REDUCTION, overlap(tgt, src, bytes)
-                                 ? "target (%p) and source (%p, size %ld) overlap, using temporary target"
-                                 : "target (%p) and source (%p, size %ld) do not overlap",
-              target, source, (long)bytes);
     }
     // Partially overlapping target/source: reduce from a private copy of the
     // source (the reference's temporary target, reduce-op.c:187-203).
@@ -669,6 +678,8 @@ int reduce_on_stream(int type, int op, void *target, const void *source,
     if (nreduce > 0 && (!device_accessible(target) || !device_accessible(source)))
         return set_error(SHMEMX_EINVAL);
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : g_state.stream;
+    if (nreduce >= 0 && op_valid(type, op))
+        trace_reference_overlap(target, source, type_size(type) * (size_t)nreduce);
     return reduce_device(type, op, target, source, nreduce, start, logstride, size,
                          algo == SHMEMX_ALGO_AUTO ? g_state.algo : algo, s);
 }

@@ -148,6 +148,27 @@ static bool small_bounce_reserve() {
     return true;
 }
 
+// Every member must issue the same sequence of collective calls, as every PE
+// of the reference runs one call sequence (reduce-op.c:213-250).  Device
+// arrays reduce in one call; host arrays above kSmallHostBytes in one call
+// per staging chunk.  Before a collective call of that size the members
+// compare their call counts (one 8-byte exchange); if any differs — one PE
+// passed host arrays, another device arrays — every member returns
+// SHMEMX_ENOTSUP instead of issuing mismatched collectives.
+static bool calls_agree(int start, int logstride, int size, size_t ncalls) {
+    std::vector<unsigned long long> all;
+    if (exchange_u64(start, logstride, size, ncalls, all)) return false;
+    for (unsigned long long v : all) {
+        if (v != ncalls) {
+            trace(LOG_REDUCTION, "members disagree on the call's chunking (%llu vs %zu calls: host "
+                  "and device arrays mixed across PEs): ENOTSUP", v, ncalls);
+            set_error(SHMEMX_ENOTSUP);
+            return false;
+        }
+    }
+    return true;
+}
+
 // The blocking entry point body: host- or device-resident arrays.
 void reduce_blocking(int type, int op, void *target, const void *source,
                      int nreduce, int start, int logstride, int size) {
@@ -168,13 +189,26 @@ void reduce_blocking(int type, int op, void *target, const void *source,
             int rc = make_plan(type, op, 0, start, logstride, size, g_state.pe, g_state.npes,
                                g_state.algo, &p);
             if (rc) set_error(rc);
+            else trace_reference_overlap(target, source, 0);
         }
         return;
     }
     const size_t bytes = type_size(type) * (size_t)nreduce;
     const bool tdev = device_accessible(target), sdev = device_accessible(source);
     hipStream_t s = g_state.stream;
+    const bool collective = size > 1 || g_state.force_collective;
+    shmemx_plan_t plan;
+    {
+        const int rc = make_plan(type, op, nreduce, start, logstride, size, g_state.pe,
+                                 g_state.npes, g_state.algo, &plan);
+        if (rc) {
+            set_error(rc);
+            return;
+        }
+    }
+    trace_reference_overlap(target, source, bytes);   // the caller's arrays
     if (tdev && sdev) {
+        if (collective && bytes > kSmallHostBytes && !calls_agree(start, logstride, size, 1)) return;
         reduce_device(type, op, target, source, nreduce, start, logstride, size, g_state.algo, s);
         SHMX_HIP(hipStreamSynchronize(s));
         switch (signal_error()) {
@@ -188,16 +222,7 @@ void reduce_blocking(int type, int op, void *target, const void *source,
     // in chunks, H2D on one copy stream, the reduction on the library stream,
     // D2H on a second copy stream, so the two PCIe directions and the device
     // work overlap.  Every PE cuts the same chunks, so the collective
-    // sequence matches across PEs.
-    shmemx_plan_t plan;
-    {
-        const int rc = make_plan(type, op, nreduce, start, logstride, size, g_state.pe,
-                                 g_state.npes, g_state.algo, &plan);
-        if (rc) {
-            set_error(rc);
-            return;
-        }
-    }
+    // sequence matches across PEs (calls_agree checks it).
     if (bytes <= kSmallHostBytes && !small_bounce_reserve()) {
         set_error(SHMEMX_ENOMEM);
         return;
@@ -273,6 +298,7 @@ void reduce_blocking(int type, int op, void *target, const void *source,
     const bool host_overlap = !tdev && !sdev && overlap(target, source, bytes);
     if (host_overlap) chunk = (size_t)nreduce;
     const size_t nchunks = ((size_t)nreduce + chunk - 1) / chunk;
+    if (collective && !calls_agree(start, logstride, size, nchunks)) return;
     // How each end reaches the device: directly (device memory), by DMA
     // (page-locked host memory), or through the page-locked bounce ring
     // (pageable memory: CPU copy by the worker pool, then DMA).

@@ -90,6 +90,8 @@ int make_plan(int type, int op, int nreduce, int start, int logstride, int size,
 int reduce_device(int type, int op, void *target, const void *source, int nreduce, int start,
                   int logstride, int size, int algo, hipStream_t s);
 bool overlap(const void *a, const void *b, size_t bytes);   // distinct, overlapping ranges
+// reduce-op.c:199-210's REDUCTION trace line for the caller's arrays
+void trace_reference_overlap(const void *target, const void *source, size_t bytes);
 bool is_member(int pe, int start, int logstride, int size, int *index);
 bool device_accessible(const void *ptr);
 bool host_pinned(const void *ptr);
@@ -132,6 +134,11 @@ int signal_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
 // After the stream has drained: 0, or 1 if a SIGNAL barrier timed out, 2 if
 // a fence before one missed an XCD.  (Clears it.)
 unsigned int signal_error();
+// Every member's 8-byte value in set order: a collective over the active set
+// (collectives.cpp; RCCL all-gather / grouped p2p, or the node block's
+// descriptors on the IPC transport).  Validates the set like a call would.
+int exchange_u64(int start, int logstride, int size, unsigned long long mine,
+                 std::vector<unsigned long long> &all);
 // DIRECT phase times since the last reset (shmemx_direct_stats).
 int direct_stats(double *out, int nout, bool reset);
 // Broadcast and [f]collect on the IPC transport (ipc_coll.cpp): members pull

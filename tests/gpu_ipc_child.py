@@ -554,6 +554,35 @@ elif scenario == "configs8":
         del got, want
     shm.free(BIG_TGT)
     shm.free(BIG_SRC)
+elif scenario == "mixed":
+    # Members passing different memory kinds: host arrays above 256 KiB go in
+    # 16 MiB staging chunks (one collective call each), device arrays in one
+    # call.  The members compare call counts first and all return ENOTSUP
+    # (reduce-op.c:213-250: every PE runs one call sequence), and the job
+    # goes on: matching calls right after are correct.  Small arrays (one
+    # call either way) mix freely.
+    import time
+    for n in (4 * 1024 * 1024 + 3, 40000):
+        srcs = oracle.sources("double", 1, npes, n, base_seed=0x31 + n)
+        want = expected("double", "sum", srcs, (0, 0, npes), "auto")
+        host = pe % 2 == 0
+        src = srcs[pe].copy() if host else torch.from_numpy(srcs[pe].copy()).cuda()
+        tgt = np.zeros(n) if host else torch.zeros(n, dtype=torch.float64, device="cuda")
+        torch.cuda.synchronize()
+        t0 = time.time()
+        shm.to_all("double", "sum", tgt, src, n, 0, 0, npes)
+        err = shm.last_error()
+        ncases += 1
+        big = n * 8 > 256 * 1024
+        if big and (err != 3 or time.time() - t0 > 30):
+            fails.append(f"mixed kinds n={n}: error {err} after {time.time() - t0:.1f} s, want ENOTSUP")
+        got = tgt if host else tgt.cpu().numpy()
+        if big and np.any(got != 0):
+            fails.append(f"mixed kinds n={n}: target written despite ENOTSUP")
+        if not big and (err or not same_bits(got, want)):
+            fails.append(f"mixed kinds n={n} (one call either way): error {err} / wrong result")
+        # the same call with matching kinds right after
+        run_case("double", "sum", n, (0, 0, npes), "auto", "device", 0x77 + n)
 elif scenario == "signal_timeout":
     # one SIGNAL call together (maps and votes), then PE 0 calls again alone:
     # its device barrier must give up after $SHMEMX_SIGNAL_TIMEOUT seconds and

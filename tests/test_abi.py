@@ -178,3 +178,16 @@ def test_direct_stats_without_calls(shm):
     assert st["calls"] == 0
     assert set(st) == {"calls", *shm.DIRECT_PHASES, *shm.FENCE_STATS}
     assert all(v == 0 for v in st.values())
+
+
+def test_typed_stream_forms_for_all_44(shm):
+    """shmemx_<T>_<op>_to_all_on_stream exists for every reference pair and
+    the header declares it returning int."""
+    syms = exported()
+    missing = [f"shmemx_{t}_{o}_to_all_on_stream" for t, o in shm.REFERENCE_PAIRS
+               if f"shmemx_{t}_{o}_to_all_on_stream" not in syms]
+    assert not missing, missing
+    pre = subprocess.run(["gcc", "-E", "-P", "-x", "c", HEADER], check=True,
+                         capture_output=True, text=True).stdout
+    decls = re.findall(r"(\w+)\s+shmemx_\w+_to_all_on_stream\s*\(", pre)
+    assert len(decls) == 44 and set(decls) == {"int"}

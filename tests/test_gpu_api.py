@@ -83,6 +83,27 @@ def test_api_zero_and_invalid(cuda, shm):
     assert shm.last_error() == 1 and (d == 7.0).all()
 
 
+def test_typed_stream_forms_return_error_codes(cuda, shm, oracle):
+    """shmemx_<T>_<op>_to_all_on_stream for all 44 pairs: a valid call returns
+    SHMEMX_OK with the result, a bad one the error code (not void)."""
+    import torch
+    L = shm.lib()
+    n = 1000
+    for t, op in shm.REFERENCE_PAIRS:
+        f = getattr(L, f"shmemx_{t}_{op}_to_all_on_stream")
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_int] * 4 + [ctypes.c_void_p]
+        src = oracle.fill(t, 1, 11, n)
+        s = torch.from_numpy(src.view(np.uint8)).cuda()
+        d = torch.zeros_like(s)
+        assert f(d.data_ptr(), s.data_ptr(), n, 0, 0, 1, None) == 0, (t, op)
+        torch.cuda.synchronize()
+        assert d.cpu().numpy().tobytes() == src.tobytes(), (t, op)
+        assert f(d.data_ptr(), s.data_ptr(), -1, 0, 0, 1, None) == 1, (t, op)      # EINVAL
+        assert shm.last_error() == 1
+        assert f(d.data_ptr(), s.data_ptr(), n, 0, 0, 2, None) == 1, (t, op)       # set beyond npes
+
+
 def test_longdouble_entry_point(cuda, shm, oracle):
     """shmem_longdouble_*_to_all run on the GPU (soft x87, ld80.h): host
     arrays at PE_size = 1 copy the value bytes."""
@@ -314,6 +335,7 @@ def test_trace_facility(cuda, tmp_path):
     code = ("import sys, numpy as np, torch; sys.path.insert(0, %r); import shmem_mi355x as s; "
             "s.init(); a = np.arange(10.0); b = np.zeros(10); "
             "s.to_all('double', 'sum', b, a, 10, 0, 0, 1); s.to_all('double', 'sum', a, a, 10, 0, 0, 1); "
+            "print(hex(b.ctypes.data), hex(a.ctypes.data)); "
             "p = s.malloc(1 << 20); s.free(p); s.finalize()") % os.path.join(repo, "openshmem-async_amd")
     env = dict(os.environ, SHMEM_LOG_LEVELS="reduction;Init,memory", SHMEM_LOG_FILE=str(log))
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
@@ -323,6 +345,12 @@ def test_trace_facility(cuda, tmp_path):
     lines = text.strip().splitlines()
     assert all(re.match(r"^\d+\.\d{8} PE 0: [A-Z]+: ", ln) for ln in lines), text
     assert any(": INIT: PE 0 of 1" in ln for ln in lines)
-    assert any("do not overlap" in ln for ln in lines)
+    # the reference's messages name the caller's host arrays (not staging
+    # buffers), and an in-place call counts as overlapping (OVERLAP_CHECK)
+    b_addr, a_addr = out.stdout.split()[-2:]
+    assert any(f"target ({b_addr}) and source ({a_addr}, size 80) do not overlap" in ln
+               for ln in lines), text
+    assert any(f"target ({a_addr}) and source ({a_addr}, size 80) overlap, using temporary target"
+               in ln for ln in lines), text
     assert any(": MEMORY: shmem_malloc(1048576" in ln for ln in lines)
     assert not any(": BARRIER: " in ln for ln in lines)          # not requested

@@ -233,3 +233,20 @@ def test_ipc_host_kind_heap(tmp_path, npes):
     for r in reports:
         assert r["ncases"] > 0
         assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["ipc", "rccl"])
+def test_mixed_memory_kinds_fail_collectively(tmp_path, transport):
+    """Even PEs pass host arrays, odd PEs device arrays: above 256 KiB the
+    host PEs would issue one collective per 16 MiB staging chunk and the
+    device PEs one, so the members compare call counts and all return
+    ENOTSUP within seconds (no hang); matching calls afterwards work, and
+    small arrays (one call either way) still mix."""
+    env = {"SHMEMX_TRANSPORT": transport}
+    if transport == "rccl":
+        env["FAKE_RCCL"] = os.path.join(HERE, "native", "libfake_rccl.so")
+    reports = run_pes(tmp_path, 2, "mixed", env, timeout=300)
+    for r in reports:
+        assert r["ncases"] == 4
+        assert not r["fails"], f"PE {r['pe']}: {r['fails']}"
