@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--algo", default="auto", choices=list(shm.ALGOS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-reps", type=int, default=20)
+    ap.add_argument("--cpu-table", type=int, default=1,
+                    help="also time every BASELINE.json config on the host (cpu_baseline.table)")
     ap.add_argument("--extras", type=int, default=1, help="also time the other algorithms / API forms")
     ap.add_argument("--extras-timeout", type=float, default=300.0,
                     help="seconds the extras may take before the line is printed without the rest")
@@ -77,6 +79,33 @@ def pmc_traffic(kernel_key: str):
     return None
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            return next(ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name"))
+    except (OSError, StopIteration):
+        return "unknown CPU"
+
+
+def pin_base(P: int) -> int:
+    """First of P consecutive CPUs this process may run on (the box gives a
+    job a CPU share, not the whole host), or -1 to leave the PEs unpinned."""
+    allowed = sorted(os.sched_getaffinity(0))
+    for i in range(len(allowed) - P + 1):
+        if allowed[i + P - 1] - allowed[i] == P - 1:
+            return allowed[i]
+    return -1
+
+
+def cpu_run(oracle, t, op, P, n, reps):
+    """One fork-per-PE run of the oracle: PE 0's per-call times (the first
+    call is a warm-up and is not among them), and the cores used."""
+    base = pin_base(P)
+    times, _ = oracle.reduce_fork(t, op, P, 0, 0, P, n, kind=0, reps=reps, pin_base=base)
+    cores = f"{base}-{base + P - 1}" if base >= 0 else "unpinned"
+    return statistics.median(times), cores
+
+
 def cpu_baseline(n: int, reps: int):
     """Oracle restatement of reduce-op.c, 2 PEs as 2 forked processes over
     shared memory (the GASNet smp model), double sum over n elements; per-PE
@@ -84,22 +113,49 @@ def cpu_baseline(n: int, reps: int):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle  # cpu_baseline leg only
     t0 = time.perf_counter()
-    times, _ = oracle.reduce_fork("double", "sum", 2, 0, 0, 2, n, kind=0, reps=reps, pin_base=0)
+    med, cores = cpu_run(oracle, "double", "sum", 2, n, reps)
     wall = time.perf_counter() - t0
-    med = statistics.median(times)
-    model = "unknown CPU"
-    try:
-        with open("/proc/cpuinfo") as f:
-            model = next(ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name"))
-    except (OSError, StopIteration):
-        pass
     return {"value": round(n * 8 / med / GiB, 4), "unit": "GiB/s", "cores": 2,
             "kind": "port",
             "sample": f"oracle restatement of reduce-op.c (gcc -O2), shmem_double_sum_to_all "
-                      f"nreduce={n} on 2 PEs = 2 processes pinned to cores 0 and 1, shm loopback; "
+                      f"nreduce={n} on 2 PEs = 2 processes pinned to CPUs {cores}, shm loopback; "
                       f"PE 0 per-call time, median of {reps} warm calls "
-                      f"({med * 1e3:.1f} ms/call, {wall:.1f} s wall); host: {model}, "
+                      f"({med * 1e3:.1f} ms/call, {wall:.1f} s wall); host: {cpu_model()}, "
                       f"{os.cpu_count()} logical CPUs"}
+
+
+def cpu_baseline_table(reps: int = 3):
+    """BASELINE.md's CPU-baseline plan, every BASELINE.json config on the
+    host: the oracle restatement of reduce-op.c (gcc -O2) as P forked PE
+    processes pinned to P consecutive CPUs over shared memory (the GASNet
+    smp model, oshrun.in:97-98); one warm-up call, then the median of `reps`
+    calls of PE 0; per-PE algbw = nreduce*sizeof(T)/t.  The float sweep is
+    capped at 16 Mi elements and the median is of 3 calls (BASELINE.md says
+    5), so the table costs about a minute of wall time: 256 Mi floats at 8 PEs
+    alone would hold 8 GiB of host memory for ~30 s."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # cpu_baseline leg only
+    Mi = 1024 * 1024
+    rows = [("int", "sum", 2, 1024, "configs[0]")]
+    rows += [("double", "sum", P, 32 * Mi, "configs[1]" if P == 1 else "configs[2]") for P in (1, 2, 4, 8)]
+    rows += [("long", op, 4, 64 * Mi, "configs[3]") for op in ("and", "or", "xor")]
+    n = 4 * 1024
+    while n <= 16 * Mi:
+        rows.append(("float", "sum", 8, n, "configs[4]"))
+        n *= 4
+    size = {"int": 4, "double": 8, "long": 8, "float": 4}
+    out = []
+    t0 = time.perf_counter()
+    for t, op, P, n, cfg in rows:
+        med, cores = cpu_run(oracle, t, op, P, n, reps if n * size[t] >= 1 << 20 else 4 * reps)
+        out.append({"config": cfg, "call": f"shmem_{t}_{op}_to_all", "nreduce": n, "PEs": P,
+                    "cores": P, "cpus": cores, "ms_per_call": round(med * 1e3, 4),
+                    "per_pe_GiBps": round(n * size[t] / med / GiB, 4)})
+    return {"host": f"{cpu_model()}, {os.cpu_count()} logical CPUs, "
+                    f"{len(os.sched_getaffinity(0))} usable by this job",
+            "method": "oracle restatement of reduce-op.c (gcc -O2), fork-per-PE over shared memory, "
+                      f"PE 0 per-call time, median of {reps} warm calls (x4 below 1 MiB)",
+            "wall_s": round(time.perf_counter() - t0, 1), "rows": out}
 
 
 def host_e2e(n: int):
@@ -146,7 +202,14 @@ def config_extras(world, stream, barrier, max_over_ranks):
     g.manual_seed(0xC0F + int(os.environ.get("RANK", "0")))
     out = {}
 
-    def rate(type_name, op, n, elem, steps):
+    # Working sets under the 256 MiB Infinity Cache (MALL) stay on-die across
+    # back-to-back steps, so a warm rate there is not HBM bandwidth (DESIGN.md
+    # §4.2).  The "cold" rate rewrites a 1 GiB scratch before every step and
+    # times the steps alone with HIP events on the stream: every step starts
+    # from HBM.
+    scratch = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+
+    def rate(type_name, op, n, elem, steps, cold=False):
         x = (torch.randint(-2**62, 2**62, (n,), dtype=torch.int64, device="cuda", generator=g)
              if elem == 8 and type_name == "long" else
              torch.rand(n, dtype=torch.float32, device="cuda", generator=g))
@@ -158,18 +221,42 @@ def config_extras(world, stream, barrier, max_over_ranks):
             fn = lambda: shm.reduce_on_stream(type_name, op, y, x, n, 0, 0, world, "auto", sp)  # noqa: E731
         for _ in range(2):
             fn()
-        w, _ = time_region(fn, steps, stream, barrier)
+        if cold:
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(steps)]
+            barrier()
+            torch.cuda.synchronize()
+            with torch.cuda.stream(stream):
+                for k, (e0, e1) in enumerate(ev):
+                    scratch.fill_(k & 0xFF)
+                    e0.record(stream)
+                    fn()
+                    e1.record(stream)
+            torch.cuda.synchronize()
+            w = sum(e0.elapsed_time(e1) for e0, e1 in ev) * 1e-3
+        else:
+            w, _ = time_region(fn, steps, stream, barrier)
         w = max_over_ranks(w)
         return round(world * n * elem * steps / w / GiB, 2)
 
     for op in ("and", "or", "xor"):
         out[f"long_{op}_64Mi_GiBps"] = rate("long", op, 64 * 1024 * 1024, 8, 10)
-    curve = {}
+    cold, warm = {}, {}
     n = 4 * 1024
     while n <= 256 * 1024 * 1024:
-        curve[str(n)] = rate("float", "sum", n, 4, 20 if n >= 1 << 24 else 50)
+        steps = 20 if n >= 1 << 24 else 50
+        cold[str(n)] = rate("float", "sum", n, 4, steps, cold=True)
+        warm[str(n)] = rate("float", "sum", n, 4, steps)
         n *= 4
-    out["float_sum_GiBps_vs_nreduce"] = curve
+    out["float_sum_GiBps_vs_nreduce"] = cold
+    out["float_sum_GiBps_vs_nreduce_note"] = (
+        "cold: a 1 GiB scratch is rewritten before every step and only the steps are timed "
+        "(HIP events on the stream), so every step reads and writes HBM")
+    out["float_sum_GiBps_vs_nreduce_warm_mall_resident"] = warm
+    out["float_sum_GiBps_vs_nreduce_warm_note"] = (
+        "back to back, no flush: working sets (3 x nreduce x 4 B at N = 1) under 256 MiB are served "
+        "from the Infinity Cache; not HBM bandwidth")
+    del scratch
     return out
 
 
@@ -523,7 +610,15 @@ def main():
 
     cpu = None
     if world == 1 and rank == 0 and not a.no_cpu_baseline:
+        stage(rank, "cpu baseline")
         cpu = cpu_baseline(n, a.cpu_reps)
+        if a.cpu_table:
+            # every BASELINE.json config on the host cores (BASELINE.md's plan);
+            # the P = 1 double-sum row sits beside this N = 1 GPU value
+            try:
+                cpu["table"] = cpu_baseline_table()
+            except Exception as e:   # noqa: BLE001 — a reported baseline, never the headline
+                cpu["table"] = f"error: {type(e).__name__}: {e}"
 
     line = {
         "metric": "GiB/s device-resident shmem_double_sum_to_all, nreduce=32Mi, 1/2/4/8 GPUs",

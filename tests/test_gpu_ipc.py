@@ -21,6 +21,13 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 def start_pes(tmp_path, npes, scenario, extra_env=None):
     boot = str(tmp_path / "uid")
+    # $GPU_TEST_LOGDIR: keep the PEs' logs (one line per case) where the GPU
+    # box hands files back, under a directory per test
+    logdir = os.environ.get("GPU_TEST_LOGDIR")
+    if logdir:
+        test = os.environ.get("PYTEST_CURRENT_TEST", scenario).split(" ")[0]
+        logdir = os.path.join(logdir, "".join(c if c.isalnum() or c in "-_." else "_" for c in test))
+        os.makedirs(logdir, exist_ok=True)
     procs = []
     for pe in range(npes):
         env = dict(os.environ, SHMEM_PE=str(pe), SHMEM_NPES=str(npes), LOCAL_RANK="0",
@@ -30,7 +37,7 @@ def start_pes(tmp_path, npes, scenario, extra_env=None):
         env.pop("WORLD_SIZE", None)
         env.update(extra_env or {})
         out = str(tmp_path / f"pe{pe}.json")
-        log = open(tmp_path / f"pe{pe}.log", "w")
+        log = open(os.path.join(logdir, f"pe{pe}.log") if logdir else tmp_path / f"pe{pe}.log", "w")
         procs.append((subprocess.Popen([sys.executable, os.path.join(HERE, "gpu_ipc_child.py"), out,
                                         scenario], env=env, stdout=log, stderr=subprocess.STDOUT,
                                        start_new_session=True), out, log))
