@@ -6,7 +6,11 @@
  * llWrk, pSync) and requires total == NUM_KEYS_PER_PE * NUM_PES.
  *
  * Like ISx, the arrays are static (host) variables and pSync is initialised
- * to SHMEM_SYNC_VALUE; the library stages them through the GPU.  Exits 0 on
+ * to SHMEM_SYNC_VALUE; the library stages them through the GPU.  With
+ * ISX_SHMEM_MALLOC=1 in the environment the arrays are shmem_malloc'd
+ * instead and written by host code — under SHMEMX_HEAP_MEMORY=mirrored that
+ * is a host view of the HBM heap, and the reductions run device-resident on
+ * its HBM twin (the program then prints the mirror's counters).  Exits 0 on
  * success.  Also checks pSync is left at SHMEM_SYNC_VALUE and that a few
  * other entry points (int/double/long xor) agree with the C definition.
  *
@@ -22,10 +26,10 @@
 
 static long pSync[SHMEM_REDUCE_SYNC_SIZE];
 static long long llWrk[SHMEM_REDUCE_MIN_WRKDATA_SIZE];
-static long long total_num_keys;
-static long long my_bucket_size;
-static double dsrc[1000], dtgt[1000];
-static long lsrc[257], ltgt[257];
+static long long s_total_num_keys;
+static long long s_my_bucket_size;
+static double s_dsrc[1000], s_dtgt[1000];
+static long s_lsrc[257], s_ltgt[257];
 
 int main(void)
 {
@@ -33,13 +37,32 @@ int main(void)
     for (i = 0; i < SHMEM_REDUCE_SYNC_SIZE; ++i) pSync[i] = SHMEM_SYNC_VALUE;
     shmem_init();
     const int me = shmem_my_pe(), npes = shmem_n_pes();
+    long long *ptotal = &s_total_num_keys, *pmine = &s_my_bucket_size;
+    double *dsrc = s_dsrc, *dtgt = s_dtgt;
+    long *lsrc = s_lsrc, *ltgt = s_ltgt;
+    const char *heap = getenv("ISX_SHMEM_MALLOC");
+    if (heap && heap[0] == '1') {   /* symmetric objects from shmem_malloc */
+        ptotal = shmem_malloc(sizeof *ptotal);
+        pmine = shmem_malloc(sizeof *pmine);
+        dsrc = shmem_malloc(1000 * sizeof *dsrc);
+        dtgt = shmem_malloc(1000 * sizeof *dtgt);
+        lsrc = shmem_malloc(257 * sizeof *lsrc);
+        ltgt = shmem_malloc(257 * sizeof *ltgt);
+        if (!ptotal || !pmine || !dsrc || !dtgt || !lsrc || !ltgt) {
+            printf("PE %d: shmem_malloc failed\n", me);
+            return 1;
+        }
+        *ptotal = 0;
+    }
+#define total_num_keys (*ptotal)
+#define my_bucket_size (*pmine)
 
     /* every PE holds NUM_KEYS_PER_PE keys, spread unevenly over the buckets */
     my_bucket_size = (long long)NUM_KEYS_PER_PE + (me % 2 ? -(me * 37) : (me + 1) * 37);
     long long expect_extra = 0;
     for (i = 0; i < npes; ++i) expect_extra += (i % 2 ? -(i * 37) : (i + 1) * 37);
 
-    shmem_longlong_sum_to_all(&total_num_keys, &my_bucket_size, 1, 0, 0, npes, llWrk, pSync);
+    shmem_longlong_sum_to_all(ptotal, pmine, 1, 0, 0, npes, llWrk, pSync);
     if (total_num_keys != (long long)(NUM_KEYS_PER_PE * npes) + expect_extra) {
         printf("PE %d: Verification Failed: total %lld\n", me, total_num_keys);
         fail = 1;
@@ -65,7 +88,14 @@ int main(void)
     for (i = 0; i < SHMEM_REDUCE_SYNC_SIZE; ++i)
         if (pSync[i] != SHMEM_SYNC_VALUE) { printf("PE %d: pSync[%d] changed\n", me, i); fail = 1; }
     if (shmemx_reduce_last_error()) { printf("PE %d: last error %d\n", me, shmemx_reduce_last_error()); fail = 1; }
+    if (heap && heap[0] == '1') {
+        unsigned long long st[5] = {0, 0, 0, 0, 0};
+        shmemx_mirror_stats(st, 5, 0);
+        printf("PE %d: mirror write faults %llu read faults %llu flushed %llu fetched %llu blocks\n", me,
+               st[0], st[1], st[2], st[3]);
+    }
+    const long long total = total_num_keys;
     shmem_finalize();
-    if (!fail) printf("PE %d of %d: ISx verification passed (total %lld)\n", me, npes, total_num_keys);
+    if (!fail) printf("PE %d of %d: ISx verification passed (total %lld)\n", me, npes, total);
     return fail;
 }

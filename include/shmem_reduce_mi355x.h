@@ -307,8 +307,32 @@ int shmemx_reduce_plan(int type, int op, int nreduce, int PE_start,
 /* Address of the symmetric object `addr` (in this PE's symmetric heap) as
  * mapped on this PE for PE `pe`'s copy — a device pointer a HIP kernel here
  * can load from / store to over xGMI (the shmem_ptr idea, querying/ptr.c).
- * NULL if `addr` is not in the heap segment or the peer is not mapped. */
+ * NULL if `addr` is not in the heap segment or the peer is not mapped.  For a
+ * mirrored heap's host-view address: `addr` itself for this PE, the peers'
+ * HBM copies (device addresses) for the others. */
 void *shmemx_heap_ptr(const void *addr, int pe);
+
+/* Mirrored heap ($SHMEMX_HEAP_MEMORY=mirrored): the symmetric heap is HBM and
+ * shmem_malloc returns addresses in a host view of it, so host code reads and
+ * writes symmetric objects as with the reference's host heap
+ * (memory/symmem.c:168-227).  The collectives run on the HBM copy; the view
+ * is kept coherent in 64 KiB blocks (page protection: a block the host stored
+ * to is copied up when a collective next uses it, a block a collective wrote
+ * is copied back when the host next touches it), so only touched blocks
+ * cross PCIe.  Host-view addresses must not be handed to HIP calls directly.
+ *   shmemx_mirror_device_ptr  the HBM twin of a host-view address (for the
+ *                             caller's own kernels), NULL if not in the view;
+ *   shmemx_mirror_sync        copy the host's stores in [addr, addr + bytes)
+ *                             to HBM now;
+ *   shmemx_mirror_invalidate  after the caller's own kernels wrote the HBM
+ *                             twin: the host view re-reads it on next access;
+ *   shmemx_mirror_stats       out[0..4] = write faults, read faults, blocks
+ *                             copied to HBM, blocks copied back, blocks marked
+ *                             device-newer; returns how many were filled. */
+void *shmemx_mirror_device_ptr(const void *addr);
+int shmemx_mirror_sync(const void *addr, size_t bytes);
+int shmemx_mirror_invalidate(const void *addr, size_t bytes);
+int shmemx_mirror_stats(unsigned long long *out, int nout, int reset);
 
 /* Host-side phase times of the DIRECT algorithm since the last reset, for
  * tuning: out[0] = calls, then microseconds summed over them: [1] waiting for

@@ -118,6 +118,9 @@ int barrier_impl(int start, int logstride, int size) {
     SetInfo si;
     if (int rc = set_info(start, logstride, size, si)) return rc;
     hipStream_t s = g_state.stream;
+    // mirrored heap: the host's stores to symmetric objects reach HBM, where
+    // the peers' kernels read them after the barrier
+    heap::flush_view();
     // quiet: everything this PE enqueued before the barrier is complete, and
     // (system-scope fence on every XCD) visible to the peers, whose stores
     // through shmemx_heap_ptr this GPU will then not see through stale lines
@@ -161,9 +164,16 @@ int broadcast_impl(size_t esize, void *target, const void *source, size_t nelems
     if (!bytes || !collective(si)) return SHMEMX_OK;  // the root's target is never written
     if ((si.m == root_idx && !source) || (si.m != root_idx && !target)) return set_error(SHMEMX_EINVAL);
     hipStream_t s = g_state.stream;
-    if (!g_state.comm)   // IPC transport
-        return ipc_broadcast(static_cast<char *>(target), static_cast<const char *>(source), bytes,
-                             root_idx, si.start, si.step, si.P, si.m, s);
+    // mirrored heap: operands in the host view run on their HBM twins
+    void *const user_target = target;
+    if (si.m == root_idx) source = heap::device_operand(source, bytes);
+    else target = heap::device_operand(target, bytes);
+    if (!g_state.comm) {   // IPC transport
+        const int rc = ipc_broadcast(static_cast<char *>(target), static_cast<const char *>(source),
+                                     bytes, root_idx, si.start, si.step, si.P, si.m, s);
+        if (rc == SHMEMX_OK && si.m != root_idx) heap::device_wrote(user_target, bytes);
+        return rc;
+    }
     const int root = si.peer(root_idx);
     const bool is_root = si.m == root_idx;
     DevBuf in, out;
@@ -189,6 +199,7 @@ int broadcast_impl(size_t esize, void *target, const void *source, size_t nelems
         SHMX_NCCL(ncclGroupEnd());
     }
     finish(out, s);
+    if (!is_root) heap::device_wrote(user_target, bytes);
     return SHMEMX_OK;
 }
 
@@ -201,11 +212,17 @@ int collect_impl(size_t esize, void *target, const void *source, size_t nelems, 
     SetInfo si;
     if (int rc = set_info(start, logstride, size, si)) return rc;
     hipStream_t s = g_state.stream;
+    // mirrored heap: operands in the host view run on their HBM twins (the
+    // target's length is known only after the counts are exchanged)
+    void *const user_target = target;
+    if (nelems && source) source = heap::device_operand(source, nelems * esize);
+    if (target) target = heap::device_operand_open(target);
     if (collective(si) && !g_state.comm) {   // IPC transport
         if (nelems && !source) return set_error(SHMEMX_EINVAL);
         size_t total = 0;
         const int rc = ipc_collect(static_cast<char *>(target), static_cast<const char *>(source), esize,
                                    nelems, si.start, si.step, si.P, si.m, &total, s);
+        if (rc == SHMEMX_OK && target) heap::device_wrote(user_target, total);
         trace(LOG_COLLECT, "%s over IPC: %zu bytes mine, %zu in all, set (%d,%d,%d)",
               fixed ? "fcollect" : "collect", nelems * esize, total, start, logstride, size);
         return rc;
@@ -261,6 +278,7 @@ int collect_impl(size_t esize, void *target, const void *source, size_t nelems, 
         }
     }
     finish(out, s);
+    heap::device_wrote(user_target, total);
     return SHMEMX_OK;
 }
 
@@ -272,6 +290,7 @@ int checksum_impl(int type, const void *ptr, size_t nelems, unsigned long long *
     if (!out || type_size(type) == 0) return set_error(SHMEMX_EINVAL);
     hipStream_t s = g_state.stream;
     const size_t bytes = nelems * type_size(type);
+    if (bytes) ptr = heap::device_operand(ptr, bytes);   // mirrored heap: the HBM twin
     DevBuf in = device_in(ptr, bytes, g_state.cws_src, g_state.cws_src_bytes, s);
     if (bytes && !in.dev) return set_error(SHMEMX_ENOMEM);
     unsigned long long *dres = static_cast<unsigned long long *>(

@@ -24,6 +24,7 @@
 #include <cstring>
 #include <unistd.h>
 
+#include "mirror.h"
 #include "shmem_reduce_mi355x.h"
 
 namespace {
@@ -42,7 +43,10 @@ bool g_installed = false;
 std::atomic<const Note *> g_note{nullptr};
 std::atomic<int> g_fired{0};
 
-void on_fatal(int sig) {
+void on_fatal(int sig, siginfo_t *si, void *) {
+    // a fault of the mirrored heap's host view is not fatal: resolve it and
+    // let the access run again (mirror.h)
+    if (sig == SIGSEGV && si && shmx::mirror::handle_fault(si->si_addr)) return;
     const Note *n = g_note.load(std::memory_order_acquire);
     const int code = (n && sig == SIGTERM) ? n->exit_code : 128 + sig;
     if (g_fired.exchange(1)) _exit(code);     // a second signal while writing
@@ -78,7 +82,8 @@ extern "C" int shmemx_set_fatal_note(const char *text, int exit_code) {
     if (!g_installed) {
         struct sigaction sa;
         memset(&sa, 0, sizeof sa);
-        sa.sa_handler = on_fatal;
+        sa.sa_sigaction = on_fatal;
+        sa.sa_flags = SA_SIGINFO | SA_NODEFER;
         sigfillset(&sa.sa_mask);
         for (int i = 0; i < kNumSignals; ++i) sigaction(kSignals[i], &sa, &g_prev[i]);
         g_installed = true;

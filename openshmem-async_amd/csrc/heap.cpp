@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "heap.h"
+#include "mirror.h"
 #include "node.h"
 #include "shmem_reduce_mi355x.h"
 #include "state.h"
@@ -46,18 +47,50 @@ bool host_kind() {
     return h;
 }
 
+// $SHMEMX_HEAP_MEMORY=mirrored: the segment is HBM as by default, and
+// shmem_malloc returns addresses in a host view of it (mirror.h): host code
+// reads and writes symmetric objects as in the reference, the collectives
+// run on the HBM twin, and only the blocks the host touched cross PCIe.
+bool mirrored() {
+    static const bool m = [] {
+        const char *e = std::getenv("SHMEMX_HEAP_MEMORY");
+        return e && std::string(e) == "mirrored";
+    }();
+    return m;
+}
+
 hipError_t seg_alloc(void **p, size_t bytes) {
     return host_kind() ? hipHostMalloc(p, bytes, hipHostMallocDefault) : hipMalloc(p, bytes);
 }
 
 hipError_t seg_free(void *p) { return host_kind() ? hipHostFree(p) : hipFree(p); }
 
+// Private blocks (outside the segment) of a mirrored heap are page-locked
+// host memory, staged per call like any host operand.
+hipError_t priv_alloc(void **p, size_t bytes) {
+    return mirrored() ? hipHostMalloc(p, bytes, hipHostMallocDefault) : seg_alloc(p, bytes);
+}
+hipError_t priv_free(void *p) { return mirrored() ? hipHostFree(p) : seg_free(p); }
+
 struct Heap {
     char *base = nullptr;     // the segment (nullptr until the first allocation)
+    char *view = nullptr;     // its host view (mirrored mode), else nullptr
     bool failed = false;      // the segment could not be allocated
     Arena arena;
     std::map<void *, Private> priv;   // blocks outside the segment
 } g_heap;
+
+// The mirrored heap's copies (mirror::Backend): host stores go up on the
+// library stream; a fetch waits for all device work first (the collective
+// that wrote the block may run on any stream) and copies synchronously.
+void mir_to_device(uint64_t off, const void *host, size_t bytes, void *) {
+    SHMX_HIP(hipMemcpyAsync(g_heap.base + off, host, bytes, hipMemcpyHostToDevice, g_state.stream));
+}
+void mir_to_host(void *host, uint64_t off, size_t bytes, void *) {
+    SHMX_HIP(hipDeviceSynchronize());
+    SHMX_HIP(hipMemcpy(host, g_heap.base + off, bytes, hipMemcpyDeviceToHost));
+}
+void mir_drain(void *) { SHMX_HIP(hipStreamSynchronize(g_state.stream)); }
 
 bool ensure_segment() {
     if (g_heap.base) return true;
@@ -82,12 +115,22 @@ bool ensure_segment() {
     if (host_kind()) {
         std::memset(g_heap.base + (bytes - kSignalBytes), 0, kSignalBytes);
     } else {
-        SHMX_HIP(hipMemset(g_heap.base + (bytes - kSignalBytes), 0, kSignalBytes));
+        // a mirrored heap starts with HBM and host view equal (zero), so
+        // every block starts CLEAN; otherwise only the signal area is zeroed
+        const uint64_t zero_from = mirrored() ? 0 : bytes - kSignalBytes;
+        SHMX_HIP(hipMemset(g_heap.base + zero_from, 0, bytes - zero_from));
         SHMX_HIP(hipDeviceSynchronize());
         node::publish(node::kHeap, p, bytes);   // peers map it after the allocation's barrier
+        if (mirrored()) {
+            if (!mirror::create(g_heap.arena.capacity(), mirror::Backend{mir_to_device, mir_to_host,
+                                                                        mir_drain, nullptr}))
+                fatal("shmem_malloc", "cannot reserve the host view of the mirrored heap");
+            g_heap.view = mirror::host_base();
+        }
     }
-    trace(LOG_MEMORY, "symmetric heap segment: %llu bytes of %s at %p", (unsigned long long)bytes,
-          host_kind() ? "page-locked host memory" : "HBM", p);
+    trace(LOG_MEMORY, "symmetric heap segment: %llu bytes of %s at %p%s%p", (unsigned long long)bytes,
+          host_kind() ? "page-locked host memory" : "HBM", p,
+          g_heap.view ? ", host view at " : "", static_cast<void *>(g_heap.view));
     return true;
 }
 
@@ -96,19 +139,24 @@ bool in_segment(const void *p) {
     return g_heap.base && c >= g_heap.base && c < g_heap.base + g_heap.arena.capacity();
 }
 
+bool in_view(const void *p) {
+    const char *c = static_cast<const char *>(p);
+    return g_heap.view && c >= g_heap.view && c < g_heap.view + g_heap.arena.capacity();
+}
+
 }  // namespace
 
 void *alloc(size_t alignment, size_t bytes) {
     if (!bytes) return nullptr;
     if (ensure_segment()) {
         const uint64_t off = g_heap.arena.alloc(bytes, alignment ? alignment : 1);
-        if (off != Arena::kNone) return g_heap.base + off;
+        if (off != Arena::kNone) return (g_heap.view ? g_heap.view : g_heap.base) + off;
     }
     // Outside the segment: a private block.  Every PE makes the same choice,
     // since the segment's state is the same on every PE.
     const size_t pad = alignment > 256 ? alignment : 0;
     void *base = nullptr;
-    if (seg_alloc(&base, bytes + pad) != hipSuccess) {
+    if (priv_alloc(&base, bytes + pad) != hipSuccess) {
         (void)hipGetLastError();
         return nullptr;
     }
@@ -121,16 +169,18 @@ void *alloc(size_t alignment, size_t bytes) {
 
 bool free(void *p) {
     if (in_segment(p)) return g_heap.arena.free((uint64_t)(static_cast<char *>(p) - g_heap.base));
+    if (in_view(p)) return g_heap.arena.free((uint64_t)(static_cast<char *>(p) - g_heap.view));
     auto it = g_heap.priv.find(p);
     if (it == g_heap.priv.end()) return false;
     SHMX_HIP(hipDeviceSynchronize());
-    SHMX_HIP(seg_free(it->second.base));
+    SHMX_HIP(priv_free(it->second.base));
     g_heap.priv.erase(it);
     return true;
 }
 
 size_t size_of(const void *p) {
     if (in_segment(p)) return g_heap.arena.size_of((uint64_t)(static_cast<const char *>(p) - g_heap.base));
+    if (in_view(p)) return g_heap.arena.size_of((uint64_t)(static_cast<const char *>(p) - g_heap.view));
     auto it = g_heap.priv.find(const_cast<void *>(p));
     return it == g_heap.priv.end() ? 0 : it->second.bytes;
 }
@@ -173,7 +223,7 @@ const std::vector<Range> &main_data() {
 }  // namespace
 
 bool is_symmetric(const void *p) {
-    if (in_segment(p)) return true;
+    if (in_segment(p) || in_view(p)) return true;
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     for (const auto &kv : g_heap.priv) {
         const uintptr_t b = reinterpret_cast<uintptr_t>(kv.first);
@@ -191,8 +241,41 @@ unsigned long long *signal_area() {
 
 uint64_t signal_offset() { return g_heap.arena.capacity(); }
 
+void *device_operand(const void *p, size_t bytes) {
+    if (!in_view(p) || bytes > g_heap.arena.capacity() - (uint64_t)(static_cast<const char *>(p) - g_heap.view))
+        return const_cast<void *>(p);
+    const uint64_t off = (uint64_t)(static_cast<const char *>(p) - g_heap.view);
+    mirror::flush(off, bytes);
+    return g_heap.base + off;
+}
+
+void *device_operand_open(const void *p) {
+    if (!in_view(p)) return const_cast<void *>(p);
+    const uint64_t off = (uint64_t)(static_cast<const char *>(p) - g_heap.view);
+    mirror::flush(off, g_heap.arena.capacity() - off);
+    return g_heap.base + off;
+}
+
+void device_wrote(const void *p, size_t bytes) {
+    if (bytes && in_view(p)) mirror::device_wrote((uint64_t)(static_cast<const char *>(p) - g_heap.view), bytes);
+}
+
+void flush_view() {
+    if (g_heap.view) mirror::flush(0, g_heap.arena.capacity());
+}
+
+bool view_offset(const void *p, uint64_t *off) {
+    if (!in_view(p)) return false;
+    *off = (uint64_t)(static_cast<const char *>(p) - g_heap.view);
+    return true;
+}
+
 void release_all() {
-    for (auto &kv : g_heap.priv) (void)seg_free(kv.second.base);
+    if (g_heap.view) {
+        mirror::destroy();
+        g_heap.view = nullptr;
+    }
+    for (auto &kv : g_heap.priv) (void)priv_free(kv.second.base);
     if (g_heap.base) {
         node::unpublish(node::kHeap);
         (void)seg_free(g_heap.base);

@@ -65,6 +65,21 @@ bool is_symmetric(const void *p);
 // PE.  nullptr if there is no segment.
 unsigned long long *signal_area();
 uint64_t signal_offset();
+// Mirrored heap ($SHMEMX_HEAP_MEMORY=mirrored, mirror.h).  A collective
+// about to read or write [p, p + bytes): if that range lies in the host view,
+// the host's stores in it go to HBM and the HBM twin's address is returned;
+// any other p is returned as it is.
+void *device_operand(const void *p, size_t bytes);
+// The same for an operand whose length is not known yet (a collect target):
+// every host store from p to the end of the view goes to HBM.
+void *device_operand_open(const void *p);
+// After a collective wrote [p, p + bytes) (a host-view address) in HBM: the
+// host view of it is stale until the next host access fetches it.
+void device_wrote(const void *p, size_t bytes);
+// Every host store in the view to HBM (barriers: peers may read it next).
+void flush_view();
+// Offset of a host-view address in the segment; false if not in the view.
+bool view_offset(const void *p, uint64_t *off);
 void release_all();                             // shmem_finalize
 
 }  // namespace heap

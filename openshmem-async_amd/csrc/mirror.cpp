@@ -1,0 +1,240 @@
+// Host view of the HBM symmetric heap: block states, page protection and the
+// fault handler (mirror.h).  Host-only: the copies go through a Backend.
+#include "mirror.h"
+
+#include <sys/mman.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+
+namespace shmx {
+namespace mirror {
+
+namespace {
+
+struct View {
+    char *base = nullptr;
+    size_t bytes = 0;
+    size_t nblocks = 0;
+    uint8_t *state = nullptr;   // one State per block (mmap'd: no allocator in the handler)
+    Backend be{};
+    // the last write fault's run, so a sequential writer unprotects growing
+    // runs instead of faulting once per block
+    size_t run_end = ~size_t(0);
+    size_t run_len = 0;
+    Stats st{};
+} g_view;
+
+std::atomic_flag g_lock = ATOMIC_FLAG_INIT;
+struct sigaction g_prev_segv;
+bool g_installed = false;
+
+struct Guard {
+    Guard() {
+        while (g_lock.test_and_set(std::memory_order_acquire)) {
+        }
+    }
+    ~Guard() { g_lock.clear(std::memory_order_release); }
+};
+
+void protect(size_t b0, size_t nb, int prot) {
+    if (nb) mprotect(g_view.base + b0 * kBlock, nb * kBlock, prot);
+}
+
+size_t block_of(uint64_t off) { return (size_t)(off / kBlock); }
+
+// Blocks [b0, b0 + nb) of the device segment -> host view, then CLEAN.
+void fetch_run(size_t b0, size_t nb) {
+    protect(b0, nb, PROT_READ | PROT_WRITE);
+    g_view.be.to_host(g_view.base + b0 * kBlock, (uint64_t)b0 * kBlock, nb * kBlock, g_view.be.ctx);
+    protect(b0, nb, PROT_READ);
+    std::memset(g_view.state + b0, CLEAN, nb);
+    g_view.st.blocks_fetched += nb;
+}
+
+void on_segv(int sig, siginfo_t *si, void *uc) {
+    if (handle_fault(si->si_addr)) return;
+    // not a fault of the host view: whatever was installed before
+    if (g_prev_segv.sa_flags & SA_SIGINFO) {
+        if (g_prev_segv.sa_sigaction) {
+            g_prev_segv.sa_sigaction(sig, si, uc);
+            return;
+        }
+    } else if (g_prev_segv.sa_handler != SIG_DFL && g_prev_segv.sa_handler != SIG_IGN) {
+        g_prev_segv.sa_handler(sig);
+        return;
+    }
+    // default action: the access faults again and the process dies on it
+    signal(SIGSEGV, SIG_DFL);
+}
+
+}  // namespace
+
+bool create(size_t bytes, const Backend &be) {
+    if (g_view.base || !bytes) return false;
+    const size_t nblocks = (bytes + kBlock - 1) / kBlock;
+    const size_t vbytes = nblocks * kBlock;
+    void *p = mmap(nullptr, vbytes, PROT_READ, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+    if (p == MAP_FAILED) return false;
+    void *s = mmap(nullptr, nblocks, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (s == MAP_FAILED) {
+        munmap(p, vbytes);
+        return false;
+    }
+    g_view.base = static_cast<char *>(p);
+    g_view.bytes = vbytes;
+    g_view.nblocks = nblocks;
+    g_view.state = static_cast<uint8_t *>(s);   // zero: every block CLEAN
+    g_view.be = be;
+    g_view.run_end = ~size_t(0);
+    g_view.run_len = 0;
+    g_view.st = Stats{};
+    if (!g_installed) {
+        struct sigaction sa;
+        std::memset(&sa, 0, sizeof sa);
+        sa.sa_sigaction = on_segv;
+        sa.sa_flags = SA_SIGINFO | SA_NODEFER;
+        sigemptyset(&sa.sa_mask);
+        sigaction(SIGSEGV, &sa, &g_prev_segv);
+        g_installed = true;
+    }
+    return true;
+}
+
+void destroy() {
+    if (!g_view.base) return;
+    if (g_installed) {
+        sigaction(SIGSEGV, &g_prev_segv, nullptr);
+        g_installed = false;
+    }
+    munmap(g_view.base, g_view.bytes);
+    munmap(g_view.state, g_view.nblocks);
+    g_view = View{};
+}
+
+bool active() { return g_view.base != nullptr; }
+char *host_base() { return g_view.base; }
+size_t view_bytes() { return g_view.bytes; }
+
+bool contains(const void *p, size_t bytes) {
+    const char *c = static_cast<const char *>(p);
+    return g_view.base && c >= g_view.base && c < g_view.base + g_view.bytes &&
+           bytes <= (size_t)(g_view.base + g_view.bytes - c);
+}
+
+uint64_t offset_of(const void *p) { return (uint64_t)(static_cast<const char *>(p) - g_view.base); }
+
+size_t flush(uint64_t off, size_t bytes) {
+    if (!g_view.base || !bytes) return 0;
+    Guard g;
+    const size_t b0 = block_of(off), b1 = block_of(off + bytes - 1) + 1;
+    size_t copied = 0;
+    for (size_t b = b0; b < b1 && b < g_view.nblocks;) {
+        if (g_view.state[b] != HOST_NEWER) {
+            ++b;
+            continue;
+        }
+        size_t e = b;
+        while (e < b1 && e < g_view.nblocks && g_view.state[e] == HOST_NEWER) ++e;
+        g_view.be.to_device((uint64_t)b * kBlock, g_view.base + b * kBlock, (e - b) * kBlock,
+                            g_view.be.ctx);
+        // read-only again: the next host store faults and marks it
+        protect(b, e - b, PROT_READ);
+        std::memset(g_view.state + b, CLEAN, e - b);
+        copied += e - b;
+        b = e;
+    }
+    if (copied) g_view.be.drain(g_view.be.ctx);
+    g_view.st.blocks_flushed += copied;
+    if (copied) g_view.run_end = ~size_t(0);
+    return copied;
+}
+
+size_t device_wrote(uint64_t off, size_t bytes) {
+    if (!g_view.base || !bytes) return 0;
+    Guard g;
+    const size_t b0 = block_of(off), b1 = std::min(block_of(off + bytes - 1) + 1, g_view.nblocks);
+    size_t n = 0;
+    for (size_t b = b0; b < b1;) {
+        if (g_view.state[b] == DEVICE_NEWER) {
+            ++b;
+            continue;
+        }
+        size_t e = b;
+        while (e < b1 && g_view.state[e] != DEVICE_NEWER) ++e;
+        // HOST_NEWER here would lose host stores: flush() runs first
+        protect(b, e - b, PROT_NONE);
+        std::memset(g_view.state + b, DEVICE_NEWER, e - b);
+        n += e - b;
+        b = e;
+    }
+    g_view.st.blocks_device_newer += n;
+    return n;
+}
+
+void fetch_all() {
+    if (!g_view.base) return;
+    Guard g;
+    for (size_t b = 0; b < g_view.nblocks;) {
+        if (g_view.state[b] != DEVICE_NEWER) {
+            ++b;
+            continue;
+        }
+        size_t e = b;
+        while (e < g_view.nblocks && g_view.state[e] == DEVICE_NEWER) ++e;
+        fetch_run(b, e - b);
+        b = e;
+    }
+}
+
+bool handle_fault(void *addr) {
+    if (!contains(addr, 1)) return false;
+    Guard g;
+    const size_t b = block_of(offset_of(addr));
+    switch (g_view.state[b]) {
+    case DEVICE_NEWER: {
+        // a load or a store of a block a collective wrote: bring it (and the
+        // DEVICE_NEWER blocks right after it) back; a store faults once more
+        size_t e = b;
+        while (e < g_view.nblocks && e - b < kMaxRunBlocks && g_view.state[e] == DEVICE_NEWER) ++e;
+        fetch_run(b, e - b);
+        g_view.st.read_faults += 1;
+        return true;
+    }
+    case CLEAN: {
+        // a store (CLEAN pages are readable): host newer from here; a
+        // sequential writer gets runs that double up to kMaxRunBlocks
+        size_t want = 1;
+        if (b == g_view.run_end) want = std::min(kMaxRunBlocks, 2 * g_view.run_len);
+        size_t e = b;
+        while (e < g_view.nblocks && e - b < want && g_view.state[e] == CLEAN) ++e;
+        protect(b, e - b, PROT_READ | PROT_WRITE);
+        std::memset(g_view.state + b, HOST_NEWER, e - b);
+        g_view.run_end = e;
+        g_view.run_len = e - b;
+        g_view.st.write_faults += 1;
+        return true;
+    }
+    default:
+        // already HOST_NEWER (another thread resolved it first)
+        protect(b, 1, PROT_READ | PROT_WRITE);
+        return true;
+    }
+}
+
+Stats stats(bool reset) {
+    Guard g;
+    const Stats s = g_view.st;
+    if (reset) g_view.st = Stats{};
+    return s;
+}
+
+State state_of(uint64_t off) {
+    if (!g_view.base || off >= g_view.bytes) return CLEAN;
+    return static_cast<State>(g_view.state[block_of(off)]);
+}
+
+}  // namespace mirror
+}  // namespace shmx

@@ -1,0 +1,92 @@
+// Host view of the HBM symmetric heap ($SHMEMX_HEAP_MEMORY=mirrored).
+//
+// The reference's symmetric heap is host memory (memory/symmem.c:168-227,
+// comms-inline.h:722-801): programs write symmetric objects with plain host
+// stores and hand them to the collectives.  Here the heap lives in HBM (so
+// reductions run device-resident and peers read it over xGMI), and in this
+// mode shmem_malloc returns an address in a HOST VIEW of the same segment —
+// same size, same offsets.  The library keeps the two coherent at block
+// granularity (kBlock bytes), using page protection to learn what the host
+// touched:
+//
+//   CLEAN        host view == HBM; host pages read-only.  A host store
+//                faults: the block (and, for a sequential run, its
+//                neighbours) becomes HOST_NEWER, read-write.
+//   HOST_NEWER   the host wrote it; HBM is stale.  A collective that reads or
+//                writes the block copies it host -> HBM first (flush), then it
+//                is CLEAN again.
+//   DEVICE_NEWER a collective wrote the block in HBM; host pages have no
+//                access.  A host load or store faults: the block (and the
+//                DEVICE_NEWER blocks after it, up to kMaxRunBlocks) is copied
+//                HBM -> host and becomes CLEAN.
+//
+// So data crosses PCIe only for blocks the host actually touched, and a
+// reduction on symmetric objects is the device-resident call: its kernels,
+// DIRECT's peer reads and RCCL all work on the HBM segment.
+//
+// The core (block states, protection, fault handling) is host-only code over
+// a copy backend, testable without a GPU (tests/native/test_mirror.cpp); the
+// library's backend moves blocks with HIP.
+#pragma once
+
+#include <csignal>
+#include <cstddef>
+#include <cstdint>
+
+namespace shmx {
+namespace mirror {
+
+constexpr size_t kBlock = size_t(64) << 10;
+constexpr size_t kMaxRunBlocks = 32;   // a fault moves at most 2 MiB
+
+enum State : uint8_t { CLEAN = 0, HOST_NEWER = 1, DEVICE_NEWER = 2 };
+
+// How blocks move between the host view and the device segment.
+struct Backend {
+    // host view [host, host + bytes) -> device segment at offset off
+    void (*to_device)(uint64_t off, const void *host, size_t bytes, void *ctx);
+    // device segment at offset off -> host view (all device work that may
+    // have written it must be complete before the copy)
+    void (*to_host)(void *host, uint64_t off, size_t bytes, void *ctx);
+    // every to_device issued so far has landed
+    void (*drain)(void *ctx);
+    void *ctx;
+};
+
+// Reserve a host view of `bytes` (rounded up to kBlock), every block CLEAN
+// (the device segment must hold the same bytes: zero), and install the
+// SIGSEGV handler.  false on failure.
+bool create(size_t bytes, const Backend &be);
+void destroy();
+bool active();
+char *host_base();
+size_t view_bytes();
+
+// Is [p, p + bytes) inside the host view?  Offset of p.
+bool contains(const void *p, size_t bytes);
+uint64_t offset_of(const void *p);
+
+// Before a collective reads or writes [off, off + bytes) of the device
+// segment: copy every HOST_NEWER block that overlaps it to the device (whole
+// blocks), mark them CLEAN, and drain.  Returns the blocks copied.
+size_t flush(uint64_t off, size_t bytes);
+// After a collective wrote [off, off + bytes) in HBM: the overlapped blocks
+// become DEVICE_NEWER (call flush on the range first).  Returns the blocks.
+size_t device_wrote(uint64_t off, size_t bytes);
+// Make the whole view current on the host (every DEVICE_NEWER block copied
+// back), e.g. before the view is released.
+void fetch_all();
+
+// The fault hook: true if `addr` is in the host view and the fault was
+// resolved (the faulting access can be retried).  The library's own
+// handlers (and the fatal-note handler) call it before anything else.
+bool handle_fault(void *addr);
+
+struct Stats {
+    uint64_t write_faults, read_faults, blocks_flushed, blocks_fetched, blocks_device_newer;
+};
+Stats stats(bool reset);
+State state_of(uint64_t off);   // tests
+
+}  // namespace mirror
+}  // namespace shmx

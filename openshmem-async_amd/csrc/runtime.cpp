@@ -35,6 +35,7 @@
 
 #include "heap.h"
 #include "internal.h"
+#include "mirror.h"
 #include "node.h"
 #include "shmem_reduce_mi355x.h"
 #include "state.h"
@@ -673,15 +674,24 @@ int reduce_on_stream(int type, int op, void *target, const void *source,
     t_last_error = SHMEMX_OK;
     if (int rc = ensure_init()) return rc;
     if (nreduce > 0 && (!target || !source)) return set_error(SHMEMX_EINVAL);
+    // Operands in the mirrored heap's host view: the host's stores go to HBM
+    // now (host-synchronous), and the call runs on the HBM twins.
+    const size_t bytes = op_valid(type, op) && nreduce > 0 ? type_size(type) * (size_t)nreduce : 0;
+    void *t = bytes ? heap::device_operand(target, bytes) : target;
+    const void *src = bytes ? heap::device_operand(source, bytes) : source;
     // the stream-ordered form takes device memory only (RCCL and the kernels
     // dereference it); host arrays go through the blocking entry points
-    if (nreduce > 0 && (!device_accessible(target) || !device_accessible(source)))
+    if (nreduce > 0 && (!device_accessible(t) || !device_accessible(src)))
         return set_error(SHMEMX_EINVAL);
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : g_state.stream;
     if (nreduce >= 0 && op_valid(type, op))
         trace_reference_overlap(target, source, type_size(type) * (size_t)nreduce);
-    return reduce_device(type, op, target, source, nreduce, start, logstride, size,
-                         algo == SHMEMX_ALGO_AUTO ? g_state.algo : algo, s);
+    const int rc = reduce_device(type, op, t, src, nreduce, start, logstride, size,
+                                 algo == SHMEMX_ALGO_AUTO ? g_state.algo : algo, s);
+    // the host view of the target is stale from here; a host access waits
+    // for the device (mirror fetches synchronise it) and reads the result
+    if (rc == SHMEMX_OK && t != target) heap::device_wrote(target, bytes);
+    return rc;
 }
 
 }  // namespace shmx
@@ -773,10 +783,48 @@ void *shmemx_heap_ptr(const void *addr, int pe) {
     std::lock_guard<std::recursive_mutex> lk(g_mu);
     if (!g_state.inited || pe < 0 || pe >= g_state.npes) return nullptr;
     uint64_t off = 0;
-    if (!heap::offset_of(addr, 1, &off)) return nullptr;
+    if (pe == g_state.pe && heap::view_offset(addr, &off)) return const_cast<void *>(addr);
+    // a host-view address of the mirrored heap names the same offset in the
+    // peers' HBM segments (device addresses, for kernels)
+    if (!heap::offset_of(addr, 1, &off) && !heap::view_offset(addr, &off)) return nullptr;
     if (pe == g_state.pe) return const_cast<void *>(addr);
     char *b = node::peer_base(node::kHeap, pe);
     return b ? b + off : nullptr;
+}
+
+int shmemx_mirror_stats(unsigned long long *out, int nout, int reset) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    if (!out || nout < 0) return set_error(SHMEMX_EINVAL);
+    const mirror::Stats st = mirror::stats(reset != 0);
+    const unsigned long long all[5] = {st.write_faults, st.read_faults, st.blocks_flushed,
+                                       st.blocks_fetched, st.blocks_device_newer};
+    const int k = nout < 5 ? nout : 5;
+    for (int i = 0; i < k; ++i) out[i] = all[i];
+    return k;
+}
+
+void *shmemx_mirror_device_ptr(const void *addr) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    uint64_t off = 0;
+    if (!heap::view_offset(addr, &off)) return nullptr;
+    return heap::device_operand(addr, 0);
+}
+
+int shmemx_mirror_sync(const void *addr, size_t bytes) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    uint64_t off = 0;
+    if (!heap::view_offset(addr, &off)) return set_error(SHMEMX_EINVAL);
+    (void)heap::device_operand(addr, bytes);
+    return SHMEMX_OK;
+}
+
+int shmemx_mirror_invalidate(const void *addr, size_t bytes) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    uint64_t off = 0;
+    if (!heap::view_offset(addr, &off)) return set_error(SHMEMX_EINVAL);
+    (void)heap::device_operand(addr, bytes);   // host stores first: they are not lost
+    heap::device_wrote(addr, bytes);
+    return SHMEMX_OK;
 }
 
 int shmemx_direct_stats(double *out, int nout, int reset) {

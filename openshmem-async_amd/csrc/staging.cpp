@@ -16,6 +16,7 @@
 #include <thread>
 #include <vector>
 
+#include "heap.h"
 #include "internal.h"
 #include "shmem_reduce_mi355x.h"
 #include "state.h"
@@ -169,11 +170,36 @@ static bool calls_agree(int start, int logstride, int size, size_t ncalls) {
     return true;
 }
 
-// The blocking entry point body: host- or device-resident arrays.
+static void reduce_blocking_impl(int type, int op, void *target, const void *source, int nreduce,
+                                 int start, int logstride, int size, bool trace_call);
+
+// The blocking entry point body: host- or device-resident arrays.  Operands
+// in the mirrored heap's host view run on their HBM twins (heap.h).
 void reduce_blocking(int type, int op, void *target, const void *source,
                      int nreduce, int start, int logstride, int size) {
     std::lock_guard<std::recursive_mutex> lk(g_mu);
     clear_error();
+    const size_t sz = type_size(type);
+    if (nreduce > 0 && sz && target && source && op_valid(type, op)) {
+        const size_t bytes = sz * (size_t)nreduce;
+        void *t = heap::device_operand(target, bytes);
+        const void *s = heap::device_operand(source, bytes);
+        if (t != target || s != source) {
+            shmemx_plan_t p;
+            const bool member = make_plan(type, op, nreduce, start, logstride, size, g_state.pe,
+                                          g_state.npes, g_state.algo, &p) == SHMEMX_OK;
+            trace_reference_overlap(target, source, bytes);   // the caller's addresses
+            reduce_blocking_impl(type, op, t, s, nreduce, start, logstride, size, false);
+            if (member && t != target && shmemx_reduce_last_error() == SHMEMX_OK)
+                heap::device_wrote(target, bytes);
+            return;
+        }
+    }
+    reduce_blocking_impl(type, op, target, source, nreduce, start, logstride, size, true);
+}
+
+static void reduce_blocking_impl(int type, int op, void *target, const void *source, int nreduce,
+                                 int start, int logstride, int size, bool trace_call) {
     if (ensure_init()) {
         trace(LOG_FATAL, "reduction called before shmem_init with npes > 1");
         return;
@@ -189,7 +215,7 @@ void reduce_blocking(int type, int op, void *target, const void *source,
             int rc = make_plan(type, op, 0, start, logstride, size, g_state.pe, g_state.npes,
                                g_state.algo, &p);
             if (rc) set_error(rc);
-            else trace_reference_overlap(target, source, 0);
+            else if (trace_call) trace_reference_overlap(target, source, 0);
         }
         return;
     }
@@ -206,7 +232,7 @@ void reduce_blocking(int type, int op, void *target, const void *source,
             return;
         }
     }
-    trace_reference_overlap(target, source, bytes);   // the caller's arrays
+    if (trace_call) trace_reference_overlap(target, source, bytes);   // the caller's arrays
     if (tdev && sdev) {
         if (collective && bytes > kSmallHostBytes && !calls_agree(start, logstride, size, 1)) return;
         reduce_device(type, op, target, source, nreduce, start, logstride, size, g_state.algo, s);

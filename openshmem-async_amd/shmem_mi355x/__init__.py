@@ -127,6 +127,14 @@ def lib() -> ctypes.CDLL:
     L.shmem_realloc.restype = vp
     L.shmem_free.argtypes = [vp]
     L.shmem_free.restype = None
+    L.shmemx_mirror_stats.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), i, i]
+    L.shmemx_mirror_stats.restype = i
+    L.shmemx_mirror_device_ptr.argtypes = [vp]
+    L.shmemx_mirror_device_ptr.restype = vp
+    L.shmemx_mirror_sync.argtypes = [vp, sz]
+    L.shmemx_mirror_sync.restype = i
+    L.shmemx_mirror_invalidate.argtypes = [vp, sz]
+    L.shmemx_mirror_invalidate.restype = i
     L.shmemx_direct_stats.argtypes = [ctypes.POINTER(ctypes.c_double), i, i]
     L.shmemx_direct_stats.restype = i
     L.shmemx_host_register.argtypes = [vp, sz]
@@ -353,6 +361,29 @@ def direct_stats(reset: bool = True) -> dict:
     out = {"calls": buf[0]}
     out.update({name: buf[i + 1] for i, name in enumerate(names[:max(0, k - 1)])})
     return out
+
+
+MIRROR_STATS = ("write_faults", "read_faults", "blocks_flushed", "blocks_fetched",
+                "blocks_device_newer")
+
+
+def mirror_stats(reset: bool = False) -> dict:
+    """shmemx_mirror_stats: the mirrored heap's fault and block counters."""
+    buf = (ctypes.c_ulonglong * len(MIRROR_STATS))()
+    k = lib().shmemx_mirror_stats(buf, len(buf), 1 if reset else 0)
+    return {name: buf[i] for i, name in enumerate(MIRROR_STATS[:k])}
+
+
+def mirror_device_ptr(address: int) -> int:
+    return lib().shmemx_mirror_device_ptr(address) or 0
+
+
+def mirror_sync(address: int, nbytes: int) -> None:
+    _check(lib().shmemx_mirror_sync(address, nbytes), "shmemx_mirror_sync")
+
+
+def mirror_invalidate(address: int, nbytes: int) -> None:
+    _check(lib().shmemx_mirror_invalidate(address, nbytes), "shmemx_mirror_invalidate")
 
 
 def host_register(buf, nbytes: int) -> None:

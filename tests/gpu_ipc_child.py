@@ -147,6 +147,10 @@ def host_view(ptr, dtype, n):
 
 def place(arr, mode, heap_ptr):
     """arr in `mode` memory: (handle passed to the library, reader)."""
+    if mode == "view":   # the mirrored heap's host view: plain host stores
+        v = host_view(heap_ptr, arr.dtype, arr.size)
+        v[:] = arr
+        return heap_ptr, lambda: v.copy()
     if mode == "host":
         a = arr.copy()
         return a, lambda: a
@@ -212,7 +216,8 @@ def run_collect(bits, counts, st, mode, seed):
         fails.append(f"{kind}{bits} counts={counts} set={st} mode={mode} err={shm.last_error()}")
 
 
-CAP = 1 << 23 if os.environ.get("SHMEMX_HEAP_MEMORY") != "host" else 48 << 20   # bytes per heap operand
+MIRRORED = os.environ.get("SHMEMX_HEAP_MEMORY") == "mirrored"
+CAP = 1 << 23 if os.environ.get("SHMEMX_HEAP_MEMORY") not in ("host", "mirrored") else 48 << 20
 HEAP_SRC = shm.malloc(CAP + 64)
 HEAP_TGT = shm.malloc(CAP)
 assert HEAP_SRC and HEAP_TGT, "shmem_malloc failed"
@@ -558,6 +563,73 @@ elif scenario == "configs8":
         del got, want
     shm.free(BIG_TGT)
     shm.free(BIG_SRC)
+elif scenario == "mirrored":
+    # $SHMEMX_HEAP_MEMORY=mirrored: shmem_malloc returns host-view addresses
+    # of the HBM heap.  Host code writes the sources with plain stores (numpy
+    # over the view), the blocking drop-in calls run on the HBM twins
+    # (DIRECT reads the peers' HBM on the IPC transport), and host code reads
+    # the targets back — against the oracle, bit for bit; only the blocks the
+    # host touched cross PCIe.
+    assert MIRRORED
+    import time
+    shm.direct_stats(reset=True)
+    for (t, op) in shm.REFERENCE_PAIRS:
+        for st in active_sets():
+            seed += 1
+            run_case(t, op, 1013, st, "auto", "hostheap", seed)
+    for n in (1, 65, (40 << 20) // 8 + 3):
+        seed += 1
+        run_case("double", "sum", n, (0, 0, npes), "auto", "hostheap", seed)
+    # in place on the view
+    n = 200003
+    srcs = oracle.sources("long", 1, npes, n, base_seed=0x515)
+    v = host_view(HEAP_SRC, np.int64, n)
+    v[:] = srcs[pe]
+    shm.to_all("long", "xor", HEAP_SRC, HEAP_SRC, n, 0, 0, npes)
+    ncases += 1
+    if shm.last_error() or not same_bits(v.copy(), oracle.reduce_sim("long", "xor", srcs, 0, 0, npes)[0]):
+        fails.append(f"mirrored in place long xor n={n}: error {shm.last_error()} / wrong result")
+    # untouched sources do not move again: the second identical call copies
+    # nothing host -> HBM, and reading the target back fetches only its blocks
+    n = (32 << 20) // 8
+    srcs = oracle.sources("double", 1, npes, n, base_seed=0x616)
+    src, tgt = host_view(HEAP_SRC, np.float64, n), host_view(HEAP_TGT, np.float64, n)
+    src[:] = srcs[pe]
+    want = oracle.reduce_sim("double", "sum", srcs, 0, 0, npes)[0]
+    shm.to_all("double", "sum", HEAP_TGT, HEAP_SRC, n, 0, 0, npes)
+    ncases += 1
+    if not same_bits(tgt.copy(), want):
+        fails.append("mirrored 32 MiB double sum: wrong result")
+    shm.mirror_stats(reset=True)
+    t0 = time.time()
+    shm.to_all("double", "sum", HEAP_TGT, HEAP_SRC, n, 0, 0, npes)
+    dt = time.time() - t0
+    st = shm.mirror_stats(reset=True)
+    nblk = (n * 8) // (64 << 10)          # the target spans nblk or nblk + 1 blocks
+    if st["blocks_flushed"] != 0 or st["blocks_device_newer"] not in (nblk, nblk + 1):
+        fails.append(f"mirrored repeat call moved blocks: {st}")
+    got = tgt.copy()
+    st = shm.mirror_stats(reset=True)
+    if not same_bits(got, want) or st["blocks_fetched"] not in (nblk, nblk + 1):
+        fails.append(f"mirrored read-back: {st}")
+    print(f"repeat 32 MiB call on untouched mirrored operands: {dt * 1e3:.2f} ms", flush=True)
+    # SIGNAL (device barriers) on the view addresses: the twins are symmetric
+    seed += 1
+    srcs = oracle.sources("float", 1, npes, 70001, base_seed=seed)
+    host_view(HEAP_SRC, np.float32, 70001)[:] = srcs[pe]
+    shm.reduce_on_stream("float", "sum", HEAP_TGT, HEAP_SRC, 70001, 0, 0, npes, "signal")
+    ncases += 1
+    if not same_bits(host_view(HEAP_TGT, np.float32, 70001).copy(),
+                     oracle.reduce_sim("float", "sum", srcs, 0, 0, npes)[0]):
+        fails.append("mirrored SIGNAL float sum: wrong result")
+    # broadcast and collect on view addresses
+    for st in active_sets():
+        seed += 1
+        run_bcast(64, 1031, 0, st, "view", seed)
+        seed += 1
+        run_collect(32, [(37 * (q + 1)) % 101 for q in range(npes)], st, "view", seed)
+    if npes > 1 and not shm.direct_stats(reset=False)["calls"] and os.environ.get("SHMEMX_TRANSPORT") == "ipc":
+        fails.append("mirrored calls did not run DIRECT on the HBM twins")
 elif scenario == "mixed":
     # Members passing different memory kinds: host arrays above 256 KiB go in
     # 16 MiB staging chunks (one collective call each), device arrays in one

@@ -1,0 +1,144 @@
+// Host test of the mirrored heap's core (openshmem-async_amd/csrc/mirror.cpp):
+// block states, page protection and the SIGSEGV path, with a memcpy backend
+// standing in for HIP (the "device segment" is a plain host buffer).  Random
+// sequences of host stores / loads and collective-style flush + device
+// writes are checked against a model: after every step the host view reads
+// what the model says, flush pushes exactly the blocks the host stored to,
+// and nothing else crosses the "PCIe" backend.
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "mirror.h"
+
+namespace M = shmx::mirror;
+
+static int fails = 0;
+#define CHECK(c)                                                        \
+    do {                                                                \
+        if (!(c)) {                                                     \
+            std::printf("FAIL %s:%d %s\n", __FILE__, __LINE__, #c);    \
+            ++fails;                                                    \
+        }                                                               \
+    } while (0)
+
+static std::vector<unsigned char> g_dev;   // the "device segment"
+static volatile size_t g_h2d = 0, g_d2h = 0;   // bytes moved
+
+static void to_device(uint64_t off, const void *host, size_t bytes, void *) {
+    std::memcpy(g_dev.data() + off, host, bytes);
+    g_h2d += bytes;
+}
+static void to_host(void *host, uint64_t off, size_t bytes, void *) {
+    std::memcpy(host, g_dev.data() + off, bytes);
+    g_d2h += bytes;
+}
+static void drain(void *) {}
+
+int main(int argc, char **argv) {
+    const int iters = argc > 1 ? std::atoi(argv[1]) : 2000;
+    const size_t nblocks = 96, bytes = nblocks * M::kBlock;
+    g_dev.assign(bytes, 0);
+    CHECK(M::create(bytes, M::Backend{to_device, to_host, drain, nullptr}));
+    // volatile: the fault handler changes the backend's counters and the
+    // view's protection behind the compiler's back
+    volatile unsigned char *h = reinterpret_cast<volatile unsigned char *>(M::host_base());
+    CHECK(M::view_bytes() == bytes);
+    // model: the value every byte must read as on the host (the truth)
+    std::vector<unsigned char> truth(bytes, 0);
+
+    // fresh view: zeros, CLEAN, loads never fault
+    for (size_t i = 0; i < bytes; i += 4093) CHECK(h[i] == 0);
+    CHECK(M::stats(false).write_faults == 0 && M::stats(false).read_faults == 0);
+
+    // a store faults once and marks its block HOST_NEWER
+    h[5] = 7;
+    truth[5] = 7;
+    CHECK(M::state_of(5) == M::HOST_NEWER);
+    CHECK(M::stats(false).write_faults == 1);
+    // a flush of a range that overlaps it pushes exactly that block
+    CHECK(M::flush(0, 16) == 1);
+    CHECK(g_h2d == M::kBlock && g_dev[5] == 7);
+    CHECK(M::state_of(5) == M::CLEAN);
+    CHECK(M::flush(0, bytes) == 0);   // nothing dirty any more
+
+    // a sequential writer gets doubling runs: far fewer faults than blocks
+    M::stats(true);
+    for (size_t i = 0; i < 40 * M::kBlock; ++i) {
+        h[8 * M::kBlock + i] = (unsigned char)(i * 13);
+        truth[8 * M::kBlock + i] = (unsigned char)(i * 13);
+    }
+    const auto ws = M::stats(false).write_faults;
+    CHECK(ws >= 2 && ws <= 8);
+    std::printf("sequential 40 blocks: %llu write faults\n", (unsigned long long)ws);
+
+    // a "collective" writes blocks 10..19 on the device: flush first, then
+    // the host view of them faults and reads the device bytes
+    g_h2d = 0;
+    M::flush(10 * M::kBlock, 10 * M::kBlock);
+    for (size_t i = 10 * M::kBlock; i < 20 * M::kBlock; ++i) {
+        g_dev[i] = (unsigned char)(i * 7 + 1);
+        truth[i] = g_dev[i];
+    }
+    CHECK(M::device_wrote(10 * M::kBlock, 10 * M::kBlock) == 10);
+    CHECK(M::state_of(10 * M::kBlock) == M::DEVICE_NEWER);
+    g_d2h = 0;
+    CHECK(h[15 * M::kBlock + 3] == truth[15 * M::kBlock + 3]);   // a load faults, fetches a run
+    CHECK(g_d2h == 5 * M::kBlock);                               // blocks 15..19
+    CHECK(M::state_of(15 * M::kBlock) == M::CLEAN && M::state_of(14 * M::kBlock) == M::DEVICE_NEWER);
+    h[11 * M::kBlock] = 99;                                       // a store: fetch, then dirty
+    truth[11 * M::kBlock] = 99;
+    CHECK(M::state_of(11 * M::kBlock) == M::HOST_NEWER);
+    CHECK(h[11 * M::kBlock + 1] == truth[11 * M::kBlock + 1]);
+
+    // random interleavings against the model
+    std::mt19937_64 rng(12345);
+    for (int it = 0; it < iters; ++it) {
+        const int what = (int)(rng() % 4);
+        const size_t off = rng() % bytes;
+        const size_t len = 1 + rng() % (3 * M::kBlock);
+        const size_t n = off + len > bytes ? bytes - off : len;
+        if (what == 0) {            // host stores
+            for (size_t i = off; i < off + n; i += 1 + rng() % 997) {
+                const unsigned char v = (unsigned char)rng();
+                h[i] = v;
+                truth[i] = v;
+            }
+        } else if (what == 1) {     // host loads
+            for (size_t i = off; i < off + n; i += 1 + rng() % 991) CHECK(h[i] == truth[i]);
+        } else if (what == 2) {     // a collective reads the range on the device
+            M::flush(off, n);
+            for (size_t i = off; i < off + n; i += 1 + rng() % 983) CHECK(g_dev[i] == truth[i]);
+        } else {                    // a collective writes the range on the device
+            M::flush(off, n);
+            // the device holds the whole blocks' truth after the flush
+            const size_t b0 = off / M::kBlock * M::kBlock;
+            const size_t b1 = (off + n + M::kBlock - 1) / M::kBlock * M::kBlock;
+            for (size_t i = b0; i < b1 && i < bytes; i += 1 + rng() % 977)
+                CHECK(M::state_of(i) != M::HOST_NEWER && (M::state_of(i) == M::DEVICE_NEWER || g_dev[i] == truth[i]));
+            for (size_t i = off; i < off + n; ++i) {
+                g_dev[i] = (unsigned char)(i ^ it);
+                truth[i] = g_dev[i];
+            }
+            M::device_wrote(off, n);
+        }
+        if (fails > 20) break;
+    }
+    // everything back on the host, and equal to the model
+    M::fetch_all();
+    CHECK(std::memcmp(const_cast<unsigned char *>(h), truth.data(), bytes) == 0);
+    const auto st = M::stats(false);
+    std::printf("stats: %llu write faults, %llu read faults, %llu flushed, %llu fetched blocks\n",
+                (unsigned long long)st.write_faults, (unsigned long long)st.read_faults,
+                (unsigned long long)st.blocks_flushed, (unsigned long long)st.blocks_fetched);
+    M::destroy();
+    if (fails) {
+        std::printf("%d failures\n", fails);
+        return 1;
+    }
+    std::printf("ok %d\n", iters);
+    return 0;
+}

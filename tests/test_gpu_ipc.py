@@ -172,10 +172,15 @@ def test_ipc_direct_staged_in_chunks(tmp_path):
 
 
 @pytest.mark.gpu
-def test_isx_c_program_four_pes(tmp_path):
+@pytest.mark.parametrize("heap", ["static", "mirrored"])
+def test_isx_c_program_four_pes(tmp_path, heap):
     """The C99 ISx verification program (examples/isx_verify.c: the
-    reference's known-answer check, isx.c:615-624, on static host arrays) as
-    four PE processes, shmem_init bootstrapping through a file."""
+    reference's known-answer check, isx.c:615-624) as four PE processes,
+    shmem_init bootstrapping through a file.  "static": static host arrays,
+    as ISx has them.  "mirrored": the arrays are shmem_malloc'd and written
+    by host code on a $SHMEMX_HEAP_MEMORY=mirrored heap; the reduction trace
+    shows every call running DIRECT on HBM (device pointers, no staging) and
+    the mirror moved the touched blocks both ways."""
     repo = os.path.dirname(HERE)
     libdir = os.path.join(repo, "openshmem-async_amd")
     exe = tmp_path / "isx_verify"
@@ -188,6 +193,9 @@ def test_isx_c_program_four_pes(tmp_path):
         env.update(SHMEM_PE=str(pe), SHMEM_NPES=str(npes), LOCAL_RANK="0",
                    SHMEM_BOOTSTRAP_FILE=str(tmp_path / "uid"), SHMEMX_TRANSPORT="ipc",
                    SHMEMX_BARRIER_TIMEOUT="120")
+        if heap == "mirrored":
+            env.update(ISX_SHMEM_MALLOC="1", SHMEMX_HEAP_MEMORY="mirrored",
+                       SHMEM_LOG_LEVELS="reduction", SHMEM_LOG_FILE=str(tmp_path / f"trace{pe}.log"))
         procs.append(subprocess.Popen([str(exe)], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT, text=True, start_new_session=True))
     try:
@@ -200,6 +208,13 @@ def test_isx_c_program_four_pes(tmp_path):
     for pe, (p, out) in enumerate(zip(procs, outs)):
         assert p.returncode == 0, f"PE {pe}: {out[-2000:]}"
         assert f"PE {pe} of {npes}: ISx verification passed" in out
+        if heap == "mirrored":
+            import re
+            m = re.search(r"flushed (\d+) fetched (\d+) blocks", out)
+            assert m and int(m.group(1)) > 0 and int(m.group(2)) > 0, out
+            trace = open(tmp_path / f"trace{pe}.log").read()
+            calls = [ln for ln in trace.splitlines() if " algo " in ln]
+            assert len(calls) == 3 and all("algo direct" in ln for ln in calls), trace
 
 
 @pytest.mark.gpu
@@ -257,3 +272,22 @@ def test_mixed_memory_kinds_fail_collectively(tmp_path, transport):
     for r in reports:
         assert r["ncases"] == 4
         assert not r["fails"], f"PE {r['pe']}: {r['fails']}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport,npes", [("ipc", 1), ("ipc", 4), ("rccl", 3)])
+def test_mirrored_heap(tmp_path, transport, npes):
+    """$SHMEMX_HEAP_MEMORY=mirrored: shmem_malloc returns a host view of the
+    HBM heap; host code writes and reads symmetric objects with plain stores
+    and loads, the collectives run device-resident on the HBM twins (DIRECT
+    over the peers' HBM on the IPC transport), only touched blocks cross
+    PCIe (a repeated call on untouched sources copies nothing up), against
+    the oracle for every reference pair and active set, SIGNAL, in place,
+    broadcast and collect."""
+    env = {"SHMEMX_TRANSPORT": transport, "SHMEMX_HEAP_MEMORY": "mirrored"}
+    if transport == "rccl":
+        env["FAKE_RCCL"] = os.path.join(HERE, "native", "libfake_rccl.so")
+    reports = run_pes(tmp_path, npes, "mirrored", env, timeout=600)
+    for r in reports:
+        assert r["ncases"] > 0
+        assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
