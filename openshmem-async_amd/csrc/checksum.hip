@@ -14,7 +14,7 @@
 // splitmix64 finaliser.  XOR makes it order-free (any grid), the index makes
 // it position-aware.
 //
-// Kernel shape: 16-byte loads per lane (2 words), a per-lane XOR, a wave XOR
+// Kernel shape: 16-byte loads per lane (2 words), 4 in flight, a per-lane XOR, a wave XOR
 // reduction by DPP within 16-lane rows and v_readlane across rows, the 4 wave
 // partials combined in LDS, one 64-bit atomic XOR per workgroup.
 #include <hip/hip_runtime.h>
@@ -30,12 +30,22 @@ namespace {
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kCkBlock = 256;
+constexpr int kCkUnroll = 4;
 
 __device__ __forceinline__ uint64_t mix64(uint64_t w, uint64_t j) {
     uint64_t z = w + (j + 1) * 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
+}
+
+// The two words of 16-byte vector i (words 2i and 2i + 1).
+template <bool LD>
+__device__ __forceinline__ uint64_t mix_pair(u32x4 x, size_t i) {
+    const uint64_t w0 = ((uint64_t)x[1] << 32) | x[0];
+    uint64_t w1 = ((uint64_t)x[3] << 32) | x[2];
+    if (LD) w1 &= 0xFFFFull;  // bytes 8-9 are sign/exponent, 10-15 padding
+    return mix64(w0, 2 * i) ^ mix64(w1, 2 * i + 1);
 }
 
 // XOR over the 64 lanes with DPP inside each 16-lane row (quad_perm
@@ -65,13 +75,17 @@ __global__ __launch_bounds__(kCkBlock) void checksum_kernel(const unsigned char 
     uint64_t h = 0;
     const size_t npairs = nwords / 2;
     const u32x4 *v = reinterpret_cast<const u32x4 *>(data);
-    for (size_t i = tid; i < npairs; i += nthr) {
-        const u32x4 x = __builtin_nontemporal_load(v + i);
-        uint64_t w0 = ((uint64_t)x[1] << 32) | x[0];
-        uint64_t w1 = ((uint64_t)x[3] << 32) | x[2];
-        if (LD) w1 &= 0xFFFFull;  // bytes 8-9 are sign/exponent, 10-15 padding
-        h ^= mix64(w0, 2 * i) ^ mix64(w1, 2 * i + 1);
+    // kCkUnroll independent 16-B loads in flight per lane before any mixing
+    // (the splitmix64 arithmetic is long enough to hide one load, not four)
+    size_t i = tid;
+    for (; i + (size_t)(kCkUnroll - 1) * nthr < npairs; i += (size_t)kCkUnroll * nthr) {
+        u32x4 x[kCkUnroll];
+#pragma unroll
+        for (int u = 0; u < kCkUnroll; ++u) x[u] = __builtin_nontemporal_load(v + i + u * nthr);
+#pragma unroll
+        for (int u = 0; u < kCkUnroll; ++u) h ^= mix_pair<LD>(x[u], i + u * nthr);
     }
+    for (; i < npairs; i += nthr) h ^= mix_pair<LD>(__builtin_nontemporal_load(v + i), i);
     if (tid == 0) {
         if (nwords & 1) {  // odd word count (only when !LD)
             uint64_t w = 0;
@@ -110,8 +124,8 @@ hipError_t launch_checksum(int type, const void *ptr, size_t n, unsigned long lo
     // 16-byte loads need a 16-byte aligned base; otherwise hash bytewise
     // through the tail path is too slow, so require it (hipMalloc gives 256).
     if ((reinterpret_cast<uintptr_t>(ptr) & 15u) != 0) return hipErrorInvalidValue;
-    size_t blocks = (nwords / 2 + kCkBlock - 1) / kCkBlock;
-    if (blocks > 4096) blocks = 4096;
+    size_t blocks = (nwords / 2 + kCkBlock * kCkUnroll - 1) / (kCkBlock * kCkUnroll);
+    if (blocks > 8192) blocks = 8192;
     if (blocks < 1) blocks = 1;
     const unsigned char *p = static_cast<const unsigned char *>(ptr);
     if (ld)

@@ -2,6 +2,7 @@
 #include <hip/hip_runtime.h>
 #include <link.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -80,15 +81,67 @@ struct Heap {
     std::map<void *, Private> priv;   // blocks outside the segment
 } g_heap;
 
-// The mirrored heap's copies (mirror::Backend): host stores go up on the
-// library stream; a fetch waits for all device work first (the collective
-// that wrote the block may run on any stream) and copies synchronously.
+// The mirrored heap's copies (mirror::Backend) go through a page-locked
+// bounce buffer: HIP never touches the view's pages itself.  (A pageable
+// hipMemcpy pins them, and every later change of their protection then
+// costs a driver invalidation: 28 ms per 32 MiB, profiles/r02_mirror_probe.)
+// Host stores go up in kMirStage halves, CPU copy of one half overlapping the
+// DMA of the other, on the library stream; a fetch waits for all device work
+// first (the collective that wrote the block may run on any stream), then
+// DMA into the bounce buffer (double-buffered) and the copy pool into the
+// view (this runs in the SIGSEGV handler; a busy pool means a plain memcpy).
+constexpr size_t kMirStage = size_t(8) << 20;
+struct MirStage {
+    char *buf = nullptr;
+    hipEvent_t done[2] = {nullptr, nullptr};
+    bool used[2] = {false, false};
+    int next = 0;
+} g_mst;
+
+void mir_stage_ready() {
+    if (g_mst.buf) return;
+    void *p = nullptr;
+    SHMX_HIP(hipHostMalloc(&p, kMirStage, hipHostMallocDefault));
+    g_mst.buf = static_cast<char *>(p);
+    for (hipEvent_t &e : g_mst.done) SHMX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+}
+
 void mir_to_device(uint64_t off, const void *host, size_t bytes, void *) {
-    SHMX_HIP(hipMemcpyAsync(g_heap.base + off, host, bytes, hipMemcpyHostToDevice, g_state.stream));
+    mir_stage_ready();
+    const size_t half = kMirStage / 2;
+    const char *src = static_cast<const char *>(host);
+    for (size_t done = 0; done < bytes; done += half) {
+        const size_t n = std::min(half, bytes - done);
+        const int h = g_mst.next;
+        g_mst.next ^= 1;
+        if (g_mst.used[h]) SHMX_HIP(hipEventSynchronize(g_mst.done[h]));
+        parallel_copy(g_mst.buf + h * half, src + done, n);
+        SHMX_HIP(hipMemcpyAsync(g_heap.base + off + done, g_mst.buf + h * half, n, hipMemcpyHostToDevice,
+                                g_state.stream));
+        SHMX_HIP(hipEventRecord(g_mst.done[h], g_state.stream));
+        g_mst.used[h] = true;
+    }
 }
 void mir_to_host(void *host, uint64_t off, size_t bytes, void *) {
+    mir_stage_ready();
     SHMX_HIP(hipDeviceSynchronize());
-    SHMX_HIP(hipMemcpy(host, g_heap.base + off, bytes, hipMemcpyDeviceToHost));
+    // halves in turn: the DMA of chunk k + 1 overlaps the CPU copy of chunk k
+    const size_t half = kMirStage / 2;
+    char *dst = static_cast<char *>(host);
+    const size_t nchunks = (bytes + half - 1) / half;
+    auto dma = [&](size_t k) {
+        const size_t n = std::min(half, bytes - k * half);
+        SHMX_HIP(hipMemcpyAsync(g_mst.buf + (k & 1) * half, g_heap.base + off + k * half, n,
+                                hipMemcpyDeviceToHost, g_state.stream));
+        SHMX_HIP(hipEventRecord(g_mst.done[k & 1], g_state.stream));
+    };
+    dma(0);
+    for (size_t k = 0; k < nchunks; ++k) {
+        if (k + 1 < nchunks) dma(k + 1);
+        SHMX_HIP(hipEventSynchronize(g_mst.done[k & 1]));
+        parallel_copy(dst + k * half, g_mst.buf + (k & 1) * half, std::min(half, bytes - k * half));
+    }
+    g_mst.used[0] = g_mst.used[1] = false;   // every DMA has landed
 }
 void mir_drain(void *) { SHMX_HIP(hipStreamSynchronize(g_state.stream)); }
 
@@ -274,6 +327,11 @@ void release_all() {
     if (g_heap.view) {
         mirror::destroy();
         g_heap.view = nullptr;
+    }
+    if (g_mst.buf) {
+        (void)hipHostFree(g_mst.buf);
+        for (hipEvent_t e : g_mst.done) (void)hipEventDestroy(e);
+        g_mst = MirStage{};
     }
     for (auto &kv : g_heap.priv) (void)priv_free(kv.second.base);
     if (g_heap.base) {

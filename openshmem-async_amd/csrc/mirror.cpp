@@ -24,6 +24,8 @@ struct View {
     // runs instead of faulting once per block
     size_t run_end = ~size_t(0);
     size_t run_len = 0;
+    size_t fetch_end = ~size_t(0);   // the same for loads of DEVICE_NEWER blocks
+    size_t fetch_len = 0;
     Stats st{};
 } g_view;
 
@@ -88,8 +90,8 @@ bool create(size_t bytes, const Backend &be) {
     g_view.nblocks = nblocks;
     g_view.state = static_cast<uint8_t *>(s);   // zero: every block CLEAN
     g_view.be = be;
-    g_view.run_end = ~size_t(0);
-    g_view.run_len = 0;
+    g_view.run_end = g_view.fetch_end = ~size_t(0);
+    g_view.run_len = g_view.fetch_len = 0;
     g_view.st = Stats{};
     if (!g_installed) {
         struct sigaction sa;
@@ -197,17 +199,21 @@ bool handle_fault(void *addr) {
     case DEVICE_NEWER: {
         // a load or a store of a block a collective wrote: bring it (and the
         // DEVICE_NEWER blocks right after it) back; a store faults once more
+        size_t want = 1;
+        if (b == g_view.fetch_end) want = std::min(kMaxFetchRun, 2 * g_view.fetch_len);
         size_t e = b;
-        while (e < g_view.nblocks && e - b < kMaxRunBlocks && g_view.state[e] == DEVICE_NEWER) ++e;
+        while (e < g_view.nblocks && e - b < want && g_view.state[e] == DEVICE_NEWER) ++e;
         fetch_run(b, e - b);
+        g_view.fetch_end = e;
+        g_view.fetch_len = e - b;
         g_view.st.read_faults += 1;
         return true;
     }
     case CLEAN: {
         // a store (CLEAN pages are readable): host newer from here; a
-        // sequential writer gets runs that double up to kMaxRunBlocks
+        // sequential writer gets runs that double up to kMaxWriteRun
         size_t want = 1;
-        if (b == g_view.run_end) want = std::min(kMaxRunBlocks, 2 * g_view.run_len);
+        if (b == g_view.run_end) want = std::min(kMaxWriteRun, 2 * g_view.run_len);
         size_t e = b;
         while (e < g_view.nblocks && e - b < want && g_view.state[e] == CLEAN) ++e;
         protect(b, e - b, PROT_READ | PROT_WRITE);

@@ -17,7 +17,8 @@
 //                is CLEAN again.
 //   DEVICE_NEWER a collective wrote the block in HBM; host pages have no
 //                access.  A host load or store faults: the block (and the
-//                DEVICE_NEWER blocks after it, up to kMaxRunBlocks) is copied
+//                DEVICE_NEWER blocks after it, a doubling run on sequential
+//                faults up to kMaxFetchRun) is copied
 //                HBM -> host and becomes CLEAN.
 //
 // So data crosses PCIe only for blocks the host actually touched, and a
@@ -37,7 +38,11 @@ namespace shmx {
 namespace mirror {
 
 constexpr size_t kBlock = size_t(64) << 10;
-constexpr size_t kMaxRunBlocks = 32;   // a fault moves at most 2 MiB
+// Sequential access gets doubling runs per fault: stores unprotect up to
+// kMaxWriteRun blocks at once (a run past the written range costs only its
+// flush), loads fetch up to kMaxFetchRun DEVICE_NEWER blocks.
+constexpr size_t kMaxWriteRun = 32;    // 2 MiB
+constexpr size_t kMaxFetchRun = 128;   // 8 MiB
 
 enum State : uint8_t { CLEAN = 0, HOST_NEWER = 1, DEVICE_NEWER = 2 };
 

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -73,9 +74,11 @@ class CopyPool {
         cv_.notify_all();
         for (auto &t : workers_) t.join();
     }
-    // memcpy split over the pool; returns when every piece is done
+    // memcpy split over the pool; returns when every piece is done.  One
+    // caller at a time: a second concurrent caller (the mirrored heap's fault
+    // handler on another thread) copies on its own.
     void copy(void *dst, const void *src, size_t bytes) {
-        if (bytes < (size_t(4) << 20) || nthreads_ == 1) {
+        if (bytes < (size_t(4) << 20) || nthreads_ == 1 || busy_.exchange(true, std::memory_order_acquire)) {
             std::memcpy(dst, src, bytes);
             return;
         }
@@ -91,6 +94,7 @@ class CopyPool {
         piece(0);
         std::unique_lock<std::mutex> lk(mu_);
         done_.wait(lk, [this] { return pending_ == 0; });
+        busy_.store(false, std::memory_order_release);
     }
 
   private:
@@ -116,6 +120,7 @@ class CopyPool {
         }
     }
     unsigned nthreads_ = 1;
+    std::atomic<bool> busy_{false};
     std::vector<std::thread> workers_;
     std::mutex mu_;
     std::condition_variable cv_, done_;
@@ -128,7 +133,7 @@ class CopyPool {
 };
 }  // namespace
 
-static void parallel_copy(void *dst, const void *src, size_t bytes) {
+void parallel_copy(void *dst, const void *src, size_t bytes) {
     static CopyPool pool;
     pool.copy(dst, src, bytes);
 }

@@ -82,6 +82,10 @@ void trace(int level, const char *fmt, ...);
     } while (0)
 
 int ensure_init();                  // single-PE auto-init; ENOINIT if npes > 1
+// memcpy split over the staging pool's CPU threads (staging.cpp); a caller
+// that finds the pool busy copies alone (the mirrored heap's fault handler
+// uses it too)
+void parallel_copy(void *dst, const void *src, size_t bytes);
 // The plan of one call (shmemx_reduce_plan) and the device-resident engine
 // (runtime.cpp); the host staging of the blocking entry points (staging.cpp)
 // runs the engine chunk by chunk.

@@ -87,8 +87,9 @@ int main(int argc, char **argv) {
     CHECK(M::state_of(10 * M::kBlock) == M::DEVICE_NEWER);
     g_d2h = 0;
     CHECK(h[15 * M::kBlock + 3] == truth[15 * M::kBlock + 3]);   // a load faults, fetches a run
-    CHECK(g_d2h == 5 * M::kBlock);                               // blocks 15..19
-    CHECK(M::state_of(15 * M::kBlock) == M::CLEAN && M::state_of(14 * M::kBlock) == M::DEVICE_NEWER);
+    CHECK(g_d2h == M::kBlock);                                   // block 15 alone (a first fault)
+    CHECK(M::state_of(15 * M::kBlock) == M::CLEAN && M::state_of(16 * M::kBlock) == M::DEVICE_NEWER);
+    CHECK(h[16 * M::kBlock] == truth[16 * M::kBlock] && g_d2h == 3 * M::kBlock);   // sequential: 2 more
     h[11 * M::kBlock] = 99;                                       // a store: fetch, then dirty
     truth[11 * M::kBlock] = 99;
     CHECK(M::state_of(11 * M::kBlock) == M::HOST_NEWER);
