@@ -4,6 +4,7 @@
 #include <fcntl.h>
 #include <sched.h>
 #include <sys/mman.h>
+#include <time.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -64,6 +65,21 @@ double barrier_timeout_s() {
 }
 
 char g_ipc_error[160] = "no IPC error";
+
+// Waiting for a peer: spin first (a barrier between busy PEs completes in
+// microseconds), then yield, then sleep in growing steps up to 100 us, so
+// PEs that wait long — more PE processes than free CPUs, a peer still
+// copying — do not take the CPU from the ones doing the work.
+void backoff(unsigned spins) {
+    if (spins < 512) return;
+    if (spins < 2048) {
+        sched_yield();
+        return;
+    }
+    const unsigned us = spins < 2048 + 64 ? 5u : (spins < 2048 + 512 ? 20u : 100u);
+    struct timespec ts = {0, (long)us * 1000};
+    nanosleep(&ts, nullptr);
+}
 
 void close_peer(Region r, int q) {
     Mapping &mp = g_node.peer[r][q];
@@ -128,14 +144,13 @@ void barrier(int start, int step, int P) {
         sh->flag[q][me].fetch_add(1, std::memory_order_acq_rel);
     }
     const auto t0 = std::chrono::steady_clock::now();
+    unsigned spins = 0;
     for (int i = 0; i < P; ++i) {
         const int q = start + i * step;
         if (q == me) continue;
-        unsigned spins = 0;
         while (sh->flag[me][q].load(std::memory_order_acquire) < g_node.entered[q]) {
-            if (++spins < 256) continue;
-            sched_yield();
-            if ((spins & 1023) == 0 &&
+            backoff(++spins);
+            if ((spins & 255) == 0 &&
                 std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() >
                     barrier_timeout_s()) {
                 char why[96];

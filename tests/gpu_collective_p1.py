@@ -1,7 +1,8 @@
 """Child process for test_gpu_api.py::test_rccl_schedules_one_rank: with
 SHMEMX_FORCE_COLLECTIVE=1 a one-PE job runs the full RCCL / ALLREDUCE / A2A /
 GATHER schedules (RCCL communicator of one rank), so every RCCL call of the
-path executes on a one-GPU box.  Prints "ok" or raises."""
+path executes on a one-GPU box; host arrays take the collective path's
+bounce and staging copies.  Prints "ok" or raises."""
 import os
 import sys
 
@@ -34,4 +35,27 @@ for t, op, algos in [("double", "sum", ("rccl", "allreduce", "a2a", "gather", "d
             shm.reduce_on_stream(t, op, s, s, n, 0, 0, 1, algo)       # in place
             torch.cuda.synchronize()
             assert s.cpu().numpy().tobytes() == raw.tobytes(), (t, op, n, algo, "in place")
+
+# Host arrays through the collective path's small-message bounce (copy
+# kernels bounce -> staging -> bounce around the one-rank RCCL call): host ->
+# device, device -> host, host -> host in place and partially overlapping,
+# and fresh data on every call through the same bounce buffers; bytewise
+# against the oracle (a one-member set is a copy, reduce-op.c:213-216).
+for t in ("long", "double", "short"):
+    for n in (1, 7, 32768):
+        for k in range(3):                       # fresh data each call
+            src = oracle.fill(t, 1, 40 + k + n, n)
+            want = oracle.reduce_sim(t, "sum", src[None, :], 0, 0, 1)[0]
+            d = torch.zeros(n, dtype=getattr(torch, {"long": "int64", "double": "float64",
+                                                    "short": "int16"}[t]), device="cuda")
+            shm.to_all(t, "sum", d, src, n, 0, 0, 1)                 # host -> device
+            assert shm.last_error() == 0 and d.cpu().numpy().tobytes() == want.tobytes(), (t, n, k, "h2d")
+            h = np.zeros_like(src)
+            shm.to_all(t, "sum", h, d, n, 0, 0, 1)                   # device -> host
+            assert h.tobytes() == want.tobytes(), (t, n, k, "d2h")
+            buf = np.concatenate([src, np.zeros(5, src.dtype)])
+            shm.to_all(t, "sum", buf, buf, n, 0, 0, 1)               # host, in place
+            assert buf[:n].tobytes() == want.tobytes(), (t, n, k, "in place")
+            shm.to_all(t, "sum", buf[3:], buf, n, 0, 0, 1)           # host, partial overlap
+            assert buf[3:n + 3].tobytes() == want.tobytes(), (t, n, k, "overlap")
 print("ok")

@@ -22,6 +22,7 @@
 
 #include <fcntl.h>
 #include <sched.h>
+#include <time.h>
 #include <sys/mman.h>
 #include <unistd.h>
 
@@ -97,8 +98,22 @@ struct P2p {
 
 // Progress every pending send/recv until all are complete; messages between
 // one pair in one direction go in call order, in mailbox-sized pieces.
+// Waiting: spin, then yield, then sleep in growing steps, so 8 ranks waiting
+// on each other do not starve the ones copying (the box gives a job a CPU
+// share, not a CPU per rank).
+void backoff(unsigned spins) {
+    if (spins < 256) return;
+    if (spins < 1024) {
+        sched_yield();
+        return;
+    }
+    struct timespec ts = {0, (long)(spins < 1024 + 64 ? 5 : 50) * 1000};
+    nanosleep(&ts, nullptr);
+}
+
 void run(const ncclComm *c, std::vector<P2p> &ops) {
     const auto t0 = std::chrono::steady_clock::now();
+    unsigned idle = 0;
     for (;;) {
         bool left = false, progressed = false;
         for (size_t i = 0; i < ops.size(); ++i) {
@@ -128,10 +143,12 @@ void run(const ncclComm *c, std::vector<P2p> &ops) {
             progressed = true;
         }
         if (!left) return;
-        if (!progressed) {
+        if (progressed) {
+            idle = 0;
+        } else {
             if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120))
                 die("no progress for 120 s (unmatched send/recv)");
-            sched_yield();
+            backoff(++idle);
         }
     }
 }
@@ -294,9 +311,10 @@ ncclResult_t ncclCommInitRank(ncclComm_t *out, int nranks, ncclUniqueId id, int 
     auto *h = reinterpret_cast<Header *>(c->base);
     h->attached.fetch_add(1);
     const auto t0 = std::chrono::steady_clock::now();
+    unsigned spins = 0;
     while (h->attached.load() < nranks) {
         if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120)) die("ranks missing at init");
-        sched_yield();
+        backoff(++spins);
     }
     if (rank == 0) shm_unlink(name.c_str());   // every rank has it mapped
     *out = c;
