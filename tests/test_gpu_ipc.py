@@ -33,6 +33,14 @@ def start_pes(tmp_path, npes, scenario, extra_env=None):
         env = dict(os.environ, SHMEM_PE=str(pe), SHMEM_NPES=str(npes), LOCAL_RANK="0",
                    SHMEM_BOOTSTRAP_FILE=boot, SHMEMX_TRANSPORT="ipc",
                    SHMEMX_BARRIER_TIMEOUT="120")
+        # All PEs share one GPU here, each process with its own hardware
+        # queues: 8 PEs x 4 queues (the box's GPU_MAX_HW_QUEUES) plus the test
+        # runner's own oversubscribe the GPU's queue slots, and every copy and
+        # sync then waits its queue's turn (8-PE tests crawled, minutes per
+        # case, in the full suite only).  Two queues per PE keep the total
+        # well inside.
+        if npes > 4:
+            env["GPU_MAX_HW_QUEUES"] = "2"
         env.pop("RANK", None)
         env.pop("WORLD_SIZE", None)
         env.update(extra_env or {})
