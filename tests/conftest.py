@@ -19,6 +19,21 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu)")
 
 
+def pytest_collection_modifyitems(session, config, items):
+    """Run the multi-process GPU tests (tests/test_gpu_ipc.py: up to 8 PE
+    processes sharing the GPU) before any test that opens a HIP context in the
+    runner itself.  The GPU serves a limited number of processes at once
+    (eight compute address spaces); a ninth — the runner, once an in-process
+    GPU test has run — puts the hardware scheduler into time-slicing, and the
+    8-PE tests then crawl (minutes per case).  The runner never touches the GPU
+    for the multi-process tests, so running them first keeps them at 8."""
+    first = [it for it in items if it.nodeid.startswith("tests/test_gpu_ipc.py")
+             or "test_gpu_ipc.py::" in it.nodeid]
+    if first:
+        rest = [it for it in items if it not in first]
+        items[:] = first + rest
+
+
 def _ensure_built():
     """Build the HIP library (hipcc, gfx950) and the oracle if a fresh
     checkout lacks them (built .so files are not in git)."""
