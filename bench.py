@@ -352,7 +352,9 @@ def direct_extra(world, n, src, sp, stream, barrier, max_over_ranks, steps, algo
         w = max_over_ranks(w)
         st = shm.direct_stats(reset=True)
         calls = st.pop("calls")
-        phases = {k: round(max_over_ranks(v / calls), 1) for k, v in st.items()} if calls else {}
+        phases = {k: round(max_over_ranks(st[k] / calls), 1) for k in shm.DIRECT_PHASES} if calls else {}
+        # every fence that handed data between GPUs reached every XCD
+        fences = {k: int(max_over_ranks(st.get(k, 0.0))) for k in shm.FENCE_STATS}
         remote = (world - 1) / world * nbytes          # bytes each PE pulls per phase
         for k in ("fold", "gather"):
             if phases.get(f"{k}_us"):
@@ -373,6 +375,7 @@ def direct_extra(world, n, src, sp, stream, barrier, max_over_ranks, steps, algo
                "ms_per_call": round(w / steps * 1e3, 3), "correct": ok}
         if phases:
             out["phases_per_call_max_over_ranks"] = phases
+        out["fences_max_over_ranks"] = fences
         return out
     except shm.ShmemError as e:
         return str(e)

@@ -473,8 +473,13 @@ void *pshmem_realloc(void *ptr, size_t size) {
     }
     void *p = heap_alloc(0, size);
     if (p) {
+        // the old contents move on the device (a mirrored heap's host stores
+        // go up first, and the new block's host view is refreshed from HBM)
         const size_t keep = old_bytes < size ? old_bytes : size;
-        SHMX_HIP(hipMemcpy(p, ptr, keep, hipMemcpyDeviceToDevice));
+        void *dst = heap::device_operand(p, keep);
+        const void *src = heap::device_operand(ptr, keep);
+        SHMX_HIP(hipMemcpy(dst, src, keep, hipMemcpyDefault));
+        heap::device_wrote(p, keep);
         heap_free(ptr);
     }
     pshmem_barrier_all();

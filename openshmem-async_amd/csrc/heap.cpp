@@ -81,21 +81,24 @@ struct Heap {
     std::map<void *, Private> priv;   // blocks outside the segment
 } g_heap;
 
-// The mirrored heap's copies (mirror::Backend) go through a page-locked
-// bounce buffer: HIP never touches the view's pages itself.  (A pageable
-// hipMemcpy pins them, and every later change of their protection then
-// costs a driver invalidation: 28 ms per 32 MiB, profiles/r02_mirror_probe.)
-// Host stores go up in kMirStage halves, CPU copy of one half overlapping the
-// DMA of the other, on the library stream; a fetch waits for all device work
-// first (the collective that wrote the block may run on any stream), then
-// DMA into the bounce buffer (double-buffered) and the copy pool into the
-// view (this runs in the SIGSEGV handler; a busy pool means a plain memcpy).
+// The mirrored heap's copies (mirror::Backend) work on the view's alias
+// (mirror.h), never on the view's own pages: a pageable hipMemcpy pins the
+// pages it touches, and every later protection change of pinned view pages
+// costs a driver invalidation (28 ms per repeated 32 MiB call, profiles/
+// r02_mirror_probe_pageable.txt).  The alias is page-locked in 256 MiB
+// regions the first time a copy touches them, and the DMA engines then move
+// blocks straight between HBM and its pages; a region HIP refuses to lock
+// goes through a page-locked bounce buffer instead (CPU copy of one half
+// overlapping the DMA of the other).  A fetch first waits for all device
+// work: the collective that wrote the block may run on any stream.
+constexpr size_t kMirRegion = size_t(256) << 20;
 constexpr size_t kMirStage = size_t(8) << 20;
 struct MirStage {
     char *buf = nullptr;
     hipEvent_t done[2] = {nullptr, nullptr};
     bool used[2] = {false, false};
     int next = 0;
+    std::vector<uint8_t> region;   // 0 untried, 1 page-locked, 2 refused
 } g_mst;
 
 void mir_stage_ready() {
@@ -106,42 +109,82 @@ void mir_stage_ready() {
     for (hipEvent_t &e : g_mst.done) SHMX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
 }
 
-void mir_to_device(uint64_t off, const void *host, size_t bytes, void *) {
-    mir_stage_ready();
-    const size_t half = kMirStage / 2;
-    const char *src = static_cast<const char *>(host);
-    for (size_t done = 0; done < bytes; done += half) {
-        const size_t n = std::min(half, bytes - done);
-        const int h = g_mst.next;
-        g_mst.next ^= 1;
-        if (g_mst.used[h]) SHMX_HIP(hipEventSynchronize(g_mst.done[h]));
-        parallel_copy(g_mst.buf + h * half, src + done, n);
-        SHMX_HIP(hipMemcpyAsync(g_heap.base + off + done, g_mst.buf + h * half, n, hipMemcpyHostToDevice,
-                                g_state.stream));
-        SHMX_HIP(hipEventRecord(g_mst.done[h], g_state.stream));
-        g_mst.used[h] = true;
+// Is the alias region holding offset `off` page-locked (locking it now)?
+bool mir_locked(uint64_t off) {
+    const size_t r = (size_t)(off / kMirRegion);
+    if (g_mst.region.size() <= r) g_mst.region.resize(r + 1, 0);
+    if (g_mst.region[r] == 0) {
+        const size_t len = std::min<size_t>(kMirRegion, mirror::view_bytes() - r * kMirRegion);
+        const bool ok = hipHostRegister(mirror::alias_base() + r * kMirRegion, len,
+                                        hipHostRegisterDefault) == hipSuccess;
+        if (!ok) (void)hipGetLastError();
+        g_mst.region[r] = ok ? 1 : 2;
+        trace(LOG_MEMORY, "mirrored heap: alias region %zu (%zu bytes) %s", r, len,
+              ok ? "page-locked" : "not page-locked (bounce buffer)");
+    }
+    return g_mst.region[r] == 1;
+}
+
+// [off, off + bytes) cut at region boundaries
+template <typename F>
+void mir_by_region(uint64_t off, size_t bytes, F f) {
+    while (bytes) {
+        const size_t n = std::min<size_t>(bytes, kMirRegion - off % kMirRegion);
+        f(off, n, mir_locked(off));
+        off += n;
+        bytes -= n;
     }
 }
-void mir_to_host(void *host, uint64_t off, size_t bytes, void *) {
-    mir_stage_ready();
+
+void mir_to_device(uint64_t off, size_t bytes, void *) {
+    mir_by_region(off, bytes, [](uint64_t o, size_t len, bool locked) {
+        const char *src = mirror::alias_base() + o;
+        if (locked) {
+            SHMX_HIP(hipMemcpyAsync(g_heap.base + o, src, len, hipMemcpyHostToDevice, g_state.stream));
+            return;
+        }
+        mir_stage_ready();
+        const size_t half = kMirStage / 2;
+        for (size_t done = 0; done < len; done += half) {
+            const size_t n = std::min(half, len - done);
+            const int h = g_mst.next;
+            g_mst.next ^= 1;
+            if (g_mst.used[h]) SHMX_HIP(hipEventSynchronize(g_mst.done[h]));
+            parallel_copy(g_mst.buf + h * half, src + done, n);
+            SHMX_HIP(hipMemcpyAsync(g_heap.base + o + done, g_mst.buf + h * half, n,
+                                    hipMemcpyHostToDevice, g_state.stream));
+            SHMX_HIP(hipEventRecord(g_mst.done[h], g_state.stream));
+            g_mst.used[h] = true;
+        }
+    });
+}
+
+void mir_to_host(uint64_t off, size_t bytes, void *) {
     SHMX_HIP(hipDeviceSynchronize());
-    // halves in turn: the DMA of chunk k + 1 overlaps the CPU copy of chunk k
-    const size_t half = kMirStage / 2;
-    char *dst = static_cast<char *>(host);
-    const size_t nchunks = (bytes + half - 1) / half;
-    auto dma = [&](size_t k) {
-        const size_t n = std::min(half, bytes - k * half);
-        SHMX_HIP(hipMemcpyAsync(g_mst.buf + (k & 1) * half, g_heap.base + off + k * half, n,
-                                hipMemcpyDeviceToHost, g_state.stream));
-        SHMX_HIP(hipEventRecord(g_mst.done[k & 1], g_state.stream));
-    };
-    dma(0);
-    for (size_t k = 0; k < nchunks; ++k) {
-        if (k + 1 < nchunks) dma(k + 1);
-        SHMX_HIP(hipEventSynchronize(g_mst.done[k & 1]));
-        parallel_copy(dst + k * half, g_mst.buf + (k & 1) * half, std::min(half, bytes - k * half));
-    }
-    g_mst.used[0] = g_mst.used[1] = false;   // every DMA has landed
+    mir_by_region(off, bytes, [](uint64_t o, size_t len, bool locked) {
+        char *dst = mirror::alias_base() + o;
+        if (locked) {
+            SHMX_HIP(hipMemcpy(dst, g_heap.base + o, len, hipMemcpyDeviceToHost));
+            return;
+        }
+        mir_stage_ready();
+        // halves in turn: the DMA of chunk k + 1 overlaps the CPU copy of chunk k
+        const size_t half = kMirStage / 2;
+        const size_t nchunks = (len + half - 1) / half;
+        auto dma = [&](size_t k) {
+            const size_t n = std::min(half, len - k * half);
+            SHMX_HIP(hipMemcpyAsync(g_mst.buf + (k & 1) * half, g_heap.base + o + k * half, n,
+                                    hipMemcpyDeviceToHost, g_state.stream));
+            SHMX_HIP(hipEventRecord(g_mst.done[k & 1], g_state.stream));
+        };
+        dma(0);
+        for (size_t k = 0; k < nchunks; ++k) {
+            if (k + 1 < nchunks) dma(k + 1);
+            SHMX_HIP(hipEventSynchronize(g_mst.done[k & 1]));
+            parallel_copy(dst + k * half, g_mst.buf + (k & 1) * half, std::min(half, len - k * half));
+        }
+        g_mst.used[0] = g_mst.used[1] = false;   // every DMA has landed
+    });
 }
 void mir_drain(void *) { SHMX_HIP(hipStreamSynchronize(g_state.stream)); }
 
@@ -325,14 +368,16 @@ bool view_offset(const void *p, uint64_t *off) {
 
 void release_all() {
     if (g_heap.view) {
+        for (size_t r = 0; r < g_mst.region.size(); ++r)
+            if (g_mst.region[r] == 1) (void)hipHostUnregister(mirror::alias_base() + r * kMirRegion);
         mirror::destroy();
         g_heap.view = nullptr;
     }
     if (g_mst.buf) {
         (void)hipHostFree(g_mst.buf);
         for (hipEvent_t e : g_mst.done) (void)hipEventDestroy(e);
-        g_mst = MirStage{};
     }
+    g_mst = MirStage{};
     for (auto &kv : g_heap.priv) (void)priv_free(kv.second.base);
     if (g_heap.base) {
         node::unpublish(node::kHeap);

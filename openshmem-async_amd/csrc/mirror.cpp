@@ -16,6 +16,7 @@ namespace {
 
 struct View {
     char *base = nullptr;
+    char *alias = nullptr;      // the same pages, always read-write
     size_t bytes = 0;
     size_t nblocks = 0;
     uint8_t *state = nullptr;   // one State per block (mmap'd: no allocator in the handler)
@@ -47,10 +48,10 @@ void protect(size_t b0, size_t nb, int prot) {
 
 size_t block_of(uint64_t off) { return (size_t)(off / kBlock); }
 
-// Blocks [b0, b0 + nb) of the device segment -> host view, then CLEAN.
+// Blocks [b0, b0 + nb) of the device segment -> host view (through the
+// alias: the view stays inaccessible until the bytes are there), then CLEAN.
 void fetch_run(size_t b0, size_t nb) {
-    protect(b0, nb, PROT_READ | PROT_WRITE);
-    g_view.be.to_host(g_view.base + b0 * kBlock, (uint64_t)b0 * kBlock, nb * kBlock, g_view.be.ctx);
+    g_view.be.to_host((uint64_t)b0 * kBlock, nb * kBlock, g_view.be.ctx);
     protect(b0, nb, PROT_READ);
     std::memset(g_view.state + b0, CLEAN, nb);
     g_view.st.blocks_fetched += nb;
@@ -78,14 +79,24 @@ bool create(size_t bytes, const Backend &be) {
     if (g_view.base || !bytes) return false;
     const size_t nblocks = (bytes + kBlock - 1) / kBlock;
     const size_t vbytes = nblocks * kBlock;
-    void *p = mmap(nullptr, vbytes, PROT_READ, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
-    if (p == MAP_FAILED) return false;
+    const int fd = memfd_create("shmemx_mirror", MFD_CLOEXEC);
+    if (fd < 0) return false;
+    if (ftruncate(fd, (off_t)vbytes) != 0) {
+        close(fd);
+        return false;
+    }
+    void *p = mmap(nullptr, vbytes, PROT_READ, MAP_SHARED, fd, 0);
+    void *a = mmap(nullptr, vbytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);   // the mappings keep the pages
     void *s = mmap(nullptr, nblocks, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-    if (s == MAP_FAILED) {
-        munmap(p, vbytes);
+    if (p == MAP_FAILED || a == MAP_FAILED || s == MAP_FAILED) {
+        if (p != MAP_FAILED) munmap(p, vbytes);
+        if (a != MAP_FAILED) munmap(a, vbytes);
+        if (s != MAP_FAILED) munmap(s, nblocks);
         return false;
     }
     g_view.base = static_cast<char *>(p);
+    g_view.alias = static_cast<char *>(a);
     g_view.bytes = vbytes;
     g_view.nblocks = nblocks;
     g_view.state = static_cast<uint8_t *>(s);   // zero: every block CLEAN
@@ -112,12 +123,14 @@ void destroy() {
         g_installed = false;
     }
     munmap(g_view.base, g_view.bytes);
+    munmap(g_view.alias, g_view.bytes);
     munmap(g_view.state, g_view.nblocks);
     g_view = View{};
 }
 
 bool active() { return g_view.base != nullptr; }
 char *host_base() { return g_view.base; }
+char *alias_base() { return g_view.alias; }
 size_t view_bytes() { return g_view.bytes; }
 
 bool contains(const void *p, size_t bytes) {
@@ -140,8 +153,7 @@ size_t flush(uint64_t off, size_t bytes) {
         }
         size_t e = b;
         while (e < b1 && e < g_view.nblocks && g_view.state[e] == HOST_NEWER) ++e;
-        g_view.be.to_device((uint64_t)b * kBlock, g_view.base + b * kBlock, (e - b) * kBlock,
-                            g_view.be.ctx);
+        g_view.be.to_device((uint64_t)b * kBlock, (e - b) * kBlock, g_view.be.ctx);
         // read-only again: the next host store faults and marks it
         protect(b, e - b, PROT_READ);
         std::memset(g_view.state + b, CLEAN, e - b);

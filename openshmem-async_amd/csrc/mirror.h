@@ -46,25 +46,31 @@ constexpr size_t kMaxFetchRun = 128;   // 8 MiB
 
 enum State : uint8_t { CLEAN = 0, HOST_NEWER = 1, DEVICE_NEWER = 2 };
 
-// How blocks move between the host view and the device segment.
+// How blocks move between the host view and the device segment.  The view
+// is one memfd mapped twice: the protected view the program uses, and an
+// ALIAS of the same pages that is always read-write.  The backend reads and
+// writes the alias, so the copies never need the view unprotected, and a
+// DMA engine may work on the alias (page-locked once) while the view's
+// protection changes — its pages' virtual range is a different one.
 struct Backend {
-    // host view [host, host + bytes) -> device segment at offset off
-    void (*to_device)(uint64_t off, const void *host, size_t bytes, void *ctx);
-    // device segment at offset off -> host view (all device work that may
-    // have written it must be complete before the copy)
-    void (*to_host)(void *host, uint64_t off, size_t bytes, void *ctx);
+    // alias [off, off + bytes) -> device segment at offset off
+    void (*to_device)(uint64_t off, size_t bytes, void *ctx);
+    // device segment at offset off -> alias (all device work that may have
+    // written it must be complete before the copy)
+    void (*to_host)(uint64_t off, size_t bytes, void *ctx);
     // every to_device issued so far has landed
     void (*drain)(void *ctx);
     void *ctx;
 };
 
-// Reserve a host view of `bytes` (rounded up to kBlock), every block CLEAN
-// (the device segment must hold the same bytes: zero), and install the
-// SIGSEGV handler.  false on failure.
+// Reserve a host view of `bytes` (rounded up to kBlock) and its alias, every
+// block CLEAN (the device segment must hold the same bytes: zero), and
+// install the SIGSEGV handler.  false on failure.
 bool create(size_t bytes, const Backend &be);
 void destroy();
 bool active();
 char *host_base();
+char *alias_base();
 size_t view_bytes();
 
 // Is [p, p + bytes) inside the host view?  Offset of p.

@@ -628,6 +628,15 @@ elif scenario == "mirrored":
         run_bcast(64, 1031, 0, st, "view", seed)
         seed += 1
         run_collect(32, [(37 * (q + 1)) % 101 for q in range(npes)], st, "view", seed)
+    # shmem_realloc keeps the contents the host wrote through the view
+    ncases += 1
+    p1 = shm.malloc(1000 * 8)
+    v1 = host_view(p1, np.int64, 1000)
+    v1[:] = np.arange(1000) * 3 + pe
+    p2 = shm.realloc(p1, 3000 * 8)
+    if not p2 or not np.array_equal(host_view(p2, np.int64, 1000).copy(), np.arange(1000) * 3 + pe):
+        fails.append("mirrored shmem_realloc lost the host-written contents")
+    shm.free(p2)
     if npes > 1 and not shm.direct_stats(reset=False)["calls"] and os.environ.get("SHMEMX_TRANSPORT") == "ipc":
         fails.append("mirrored calls did not run DIRECT on the HBM twins")
 elif scenario == "mixed":

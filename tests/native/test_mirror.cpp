@@ -28,12 +28,13 @@ static int fails = 0;
 static std::vector<unsigned char> g_dev;   // the "device segment"
 static volatile size_t g_h2d = 0, g_d2h = 0;   // bytes moved
 
-static void to_device(uint64_t off, const void *host, size_t bytes, void *) {
-    std::memcpy(g_dev.data() + off, host, bytes);
+// the backend works on the view's always-writable alias
+static void to_device(uint64_t off, size_t bytes, void *) {
+    std::memcpy(g_dev.data() + off, M::alias_base() + off, bytes);
     g_h2d += bytes;
 }
-static void to_host(void *host, uint64_t off, size_t bytes, void *) {
-    std::memcpy(host, g_dev.data() + off, bytes);
+static void to_host(uint64_t off, size_t bytes, void *) {
+    std::memcpy(M::alias_base() + off, g_dev.data() + off, bytes);
     g_d2h += bytes;
 }
 static void drain(void *) {}
