@@ -107,20 +107,24 @@ def cpu_run(oracle, t, op, P, n, reps):
 
 
 def cpu_baseline(n: int, reps: int):
-    """Oracle restatement of reduce-op.c, 2 PEs as 2 forked processes over
-    shared memory (the GASNet smp model), double sum over n elements; per-PE
-    algbw n*8/t of PE 0, median over `reps` warm calls."""
+    """The same workload as the N = 1 GPU step, on one host core: the
+    reference's local reduction write_to = op(write_to, pWrk) over n doubles
+    (reduce-op.c:224-245, 64-element pWrk staging, an indirect call per
+    element) in the oracle restatement; algbw n*8/t like the GPU value, median
+    over `reps` warm folds.  The whole call at 2..8 PEs is in the table."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle  # cpu_baseline leg only
+    base = pin_base(1)
     t0 = time.perf_counter()
-    med, cores = cpu_run(oracle, "double", "sum", 2, n, reps)
+    med = statistics.median(oracle.fold_time("double", "sum", n, reps=reps, pin=base))
     wall = time.perf_counter() - t0
-    return {"value": round(n * 8 / med / GiB, 4), "unit": "GiB/s", "cores": 2,
+    return {"value": round(n * 8 / med / GiB, 4), "unit": "GiB/s", "cores": 1,
             "kind": "port",
-            "sample": f"oracle restatement of reduce-op.c (gcc -O2), shmem_double_sum_to_all "
-                      f"nreduce={n} on 2 PEs = 2 processes pinned to CPUs {cores}, shm loopback; "
-                      f"PE 0 per-call time, median of {reps} warm calls "
-                      f"({med * 1e3:.1f} ms/call, {wall:.1f} s wall); host: {cpu_model()}, "
+            "sample": f"oracle restatement of reduce-op.c (gcc -O2): the local reduce of "
+                      f"shmem_double_sum_to_all, write_to = write_to + pWrk over nreduce={n} "
+                      f"(64-element pWrk staging, indirect call per element, :224-245), the N = 1 "
+                      f"GPU step's workload, one process pinned to CPU {base}; median of {reps} "
+                      f"warm folds ({med * 1e3:.1f} ms/fold, {wall:.1f} s wall); host: {cpu_model()}, "
                       f"{os.cpu_count()} logical CPUs"}
 
 
@@ -146,6 +150,12 @@ def cpu_baseline_table(reps: int = 3):
     size = {"int": 4, "double": 8, "long": 8, "float": 4}
     out = []
     t0 = time.perf_counter()
+    base = pin_base(1)
+    fold = statistics.median(oracle.fold_time("double", "sum", 32 * Mi, reps=reps, pin=base))
+    out.append({"config": "configs[1]", "call": "local reduce of shmem_double_sum_to_all "
+                "(write_to = write_to + pWrk, the N = 1 GPU step)", "nreduce": 32 * Mi, "PEs": 1,
+                "cores": 1, "cpus": str(base), "ms_per_call": round(fold * 1e3, 4),
+                "per_pe_GiBps": round(32 * Mi * 8 / fold / GiB, 4)})
     for t, op, P, n, cfg in rows:
         med, cores = cpu_run(oracle, t, op, P, n, reps if n * size[t] >= 1 << 20 else 4 * reps)
         out.append({"config": cfg, "call": f"shmem_{t}_{op}_to_all", "nreduce": n, "PEs": P,

@@ -47,6 +47,8 @@ def lib() -> ctypes.CDLL:
                                          ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_uint64)]
         L.oracle_reduce_fork.restype = i
+        L.oracle_fold_time.argtypes = [i, i, i, i, i, ctypes.POINTER(ctypes.c_double)]
+        L.oracle_fold_time.restype = i
         L.oracle_fill.argtypes = [i, i, ctypes.c_uint64, vp, ctypes.c_size_t]
         L.oracle_fill.restype = None
         L.oracle_splitmix64.argtypes = [ctypes.c_uint64, ctypes.c_uint64]
@@ -176,6 +178,16 @@ def reduce_fork(type_name: str, op: str, npes: int, PE_start: int, logPE_stride:
     if rc != 0:
         raise RuntimeError("oracle_reduce_fork failed")
     return list(times), list(hashes)
+
+
+def fold_time(type_name: str, op: str, nreduce: int, reps: int = 5, pin: int = -1) -> list:
+    """The reference's per-peer fold step alone (acc = op(acc, in), pWrk
+    staging, indirect call per element): per-fold seconds."""
+    times = (ctypes.c_double * reps)()
+    rc = lib().oracle_fold_time(TYPES[type_name], OPS[op], nreduce, reps, pin, times)
+    if rc != 0:
+        raise RuntimeError("oracle_fold_time failed")
+    return list(times)
 
 
 def value_hash(type_name: str, arr: np.ndarray) -> int:

@@ -383,6 +383,47 @@ static uint64_t orc_hash_elems(int type, const void *p, size_t n)
     return h;
 }
 
+static double orc_now(void);
+
+/* ------------------------------------------------ the local fold alone -- */
+/* The per-peer step of the reference's loop (reduce-op.c:224-245) on its
+ * own, write_to = op(write_to, peer) over nreduce elements through the
+ * 64-element pWrk staging and the per-element indirect call: the CPU twin of
+ * the 1-GPU bench step.  One process, optionally pinned to core `pin`; one
+ * warm-up fold, then `reps` timed folds; per-fold seconds to times_out.   */
+int oracle_fold_time(int type, int op, int nreduce, int reps, int pin, double *times_out)
+{
+    orc_kernel_t k;
+    if (orc_kernel(type, op, &k) || nreduce < 0 || reps < 1 || reps > 64) return -1;
+    cpu_set_t old;
+    CPU_ZERO(&old);
+    const int have_old = sched_getaffinity(0, sizeof(old), &old) == 0;
+    if (pin >= 0) {
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        CPU_SET(pin, &set);
+        sched_setaffinity(0, sizeof(set), &set);
+    }
+    const size_t bytes = oracle_type_size(type) * (size_t)nreduce;
+    char *acc = malloc(bytes ? bytes : 1), *in = malloc(bytes ? bytes : 1);
+    int rc = -1;
+    if (acc && in) {
+        oracle_fill(type, 0, 0x5EED0000ULL, acc, (size_t)nreduce);
+        oracle_fill(type, 0, 0x5EED0001ULL, in, (size_t)nreduce);
+        k.fold(k.fn, acc, in, nreduce);                   /* warm-up, first touch */
+        for (int r = 0; r < reps; ++r) {
+            const double t0 = orc_now();
+            k.fold(k.fn, acc, in, nreduce);
+            times_out[r] = orc_now() - t0;
+        }
+        rc = 0;
+    }
+    free(acc);
+    free(in);
+    if (pin >= 0 && have_old) sched_setaffinity(0, sizeof(old), &old);
+    return rc;
+}
+
 /* ------------------------------------------------ fork-per-PE harness ---- */
 /* One process per PE, every PE's source/target in one MAP_SHARED mapping, the
  * barrier a process-shared pthread barrier over the active set: the model of

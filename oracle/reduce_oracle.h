@@ -56,6 +56,14 @@ int oracle_reduce_sim(int type, int op, int npes, int PE_start,
  * pin_base >= 0 pins PE p to core (pin_base + p) % ncpu.
  * Returns 0 on success.
  */
+/*
+ * The reference's per-peer fold step alone (reduce-op.c:224-245): acc =
+ * op(acc, in) over nreduce elements with the 64-element pWrk staging and an
+ * indirect call per element, in this process (pinned to core `pin` if >= 0).
+ * One warm-up fold, then `reps` timed folds (seconds each) to times_out.
+ */
+int oracle_fold_time(int type, int op, int nreduce, int reps, int pin, double *times_out);
+
 int oracle_reduce_fork(int type, int op, int npes, int PE_start,
                        int logPE_stride, int PE_size, int nreduce,
                        int fill_kind, uint64_t base_seed, int reps,

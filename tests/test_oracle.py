@@ -217,3 +217,13 @@ def test_config1_int_sum_1024_two_pes_fork(oracle):
     srcs = oracle.sources("int", 1, 2, 1024)
     want = (srcs[0].astype(np.int64) + srcs[1]).astype(np.int32)     # wraps like C
     assert hashes[0] == hashes[1] == oracle.value_hash("int", want)
+
+
+def test_fold_time_is_the_local_reduce(oracle):
+    """oracle_fold_time (bench.py's cpu_baseline: the N = 1 GPU step's
+    workload on one core) runs the reference's per-peer fold and reports one
+    positive time per repetition; bad arguments are refused."""
+    t = oracle.fold_time("double", "sum", 100000, reps=3, pin=-1)
+    assert len(t) == 3 and all(x > 0 for x in t)
+    with pytest.raises(RuntimeError):
+        oracle.fold_time("double", "xor", 10, reps=1)
