@@ -119,7 +119,12 @@ bool create(size_t bytes, const Backend &be) {
 void destroy() {
     if (!g_view.base) return;
     if (g_installed) {
-        sigaction(SIGSEGV, &g_prev_segv, nullptr);
+        // put back what was there before, unless someone installed a handler
+        // over ours since (it chains to ours, which then finds no view)
+        struct sigaction cur;
+        if (sigaction(SIGSEGV, nullptr, &cur) == 0 && (cur.sa_flags & SA_SIGINFO) &&
+            cur.sa_sigaction == on_segv)
+            sigaction(SIGSEGV, &g_prev_segv, nullptr);
         g_installed = false;
     }
     munmap(g_view.base, g_view.bytes);
