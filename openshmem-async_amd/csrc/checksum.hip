@@ -14,9 +14,10 @@
 // splitmix64 finaliser.  XOR makes it order-free (any grid), the index makes
 // it position-aware.
 //
-// Kernel shape: 16-byte loads per lane (2 words), 4 in flight, a per-lane XOR, a wave XOR
+// Kernel shape: 16-byte loads per lane (2 words), a per-lane XOR, a wave XOR
 // reduction by DPP within 16-lane rows and v_readlane across rows, the 4 wave
-// partials combined in LDS, one 64-bit atomic XOR per workgroup.
+// partials combined in LDS, one partial per workgroup in its own slot, and a
+// one-workgroup kernel XORing the partials (same DPP + LDS reduction).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -30,22 +31,30 @@ namespace {
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kCkBlock = 256;
-constexpr int kCkUnroll = 4;
+
+constexpr uint64_t kPhi = 0x9E3779B97F4A7C15ull;
 
 __device__ __forceinline__ uint64_t mix64(uint64_t w, uint64_t j) {
-    uint64_t z = w + (j + 1) * 0x9E3779B97F4A7C15ull;
+    uint64_t z = w + (j + 1) * kPhi;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
     return z ^ (z >> 31);
 }
 
-// The two words of 16-byte vector i (words 2i and 2i + 1).
+// splitmix64's finaliser of z = w + (j + 1) * phi, the position term given.
+__device__ __forceinline__ uint64_t fmix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// The two words of 16-byte vector i (words 2i and 2i + 1); c = (2i + 1) * phi.
 template <bool LD>
-__device__ __forceinline__ uint64_t mix_pair(u32x4 x, size_t i) {
+__device__ __forceinline__ uint64_t mix_pair(u32x4 x, uint64_t c) {
     const uint64_t w0 = ((uint64_t)x[1] << 32) | x[0];
     uint64_t w1 = ((uint64_t)x[3] << 32) | x[2];
     if (LD) w1 &= 0xFFFFull;  // bytes 8-9 are sign/exponent, 10-15 padding
-    return mix64(w0, 2 * i) ^ mix64(w1, 2 * i + 1);
+    return fmix(w0 + c) ^ fmix(w1 + c + kPhi);
 }
 
 // XOR over the 64 lanes with DPP inside each 16-lane row (quad_perm
@@ -68,24 +77,21 @@ __device__ __forceinline__ uint64_t wave_xor(uint64_t v) {
 // 16-byte long double slots down to their 10 value bytes.
 template <bool LD>
 __global__ __launch_bounds__(kCkBlock) void checksum_kernel(const unsigned char *data, size_t nwords,
-                                                            size_t tail, unsigned long long *out) {
+                                                            size_t tail, unsigned long long *partials) {
     __shared__ unsigned long long part[kCkBlock / 64];
     const size_t tid = (size_t)blockIdx.x * kCkBlock + threadIdx.x;
     const size_t nthr = (size_t)gridDim.x * kCkBlock;
     uint64_t h = 0;
     const size_t npairs = nwords / 2;
     const u32x4 *v = reinterpret_cast<const u32x4 *>(data);
-    // kCkUnroll independent 16-B loads in flight per lane before any mixing
-    // (the splitmix64 arithmetic is long enough to hide one load, not four)
-    size_t i = tid;
-    for (; i + (size_t)(kCkUnroll - 1) * nthr < npairs; i += (size_t)kCkUnroll * nthr) {
-        u32x4 x[kCkUnroll];
-#pragma unroll
-        for (int u = 0; u < kCkUnroll; ++u) x[u] = __builtin_nontemporal_load(v + i + u * nthr);
-#pragma unroll
-        for (int u = 0; u < kCkUnroll; ++u) h ^= mix_pair<LD>(x[u], i + u * nthr);
-    }
-    for (; i < npairs; i += nthr) h ^= mix_pair<LD>(__builtin_nontemporal_load(v + i), i);
+    // The position term (j + 1) * phi of word j = 2i (+1) advances by
+    // 2 * nthr * phi per grid-stride step: carried, not multiplied (a 64-bit
+    // multiply is several quarter-rate instructions on CDNA; the hash is
+    // VALU-heavy enough to share the bound with HBM).
+    uint64_t c = (2 * (uint64_t)tid + 1) * kPhi;
+    const uint64_t dc = 2 * (uint64_t)nthr * kPhi;
+    for (size_t i = tid; i < npairs; i += nthr, c += dc)
+        h ^= mix_pair<LD>(__builtin_nontemporal_load(v + i), c);
     if (tid == 0) {
         if (nwords & 1) {  // odd word count (only when !LD)
             uint64_t w = 0;
@@ -106,7 +112,26 @@ __global__ __launch_bounds__(kCkBlock) void checksum_kernel(const unsigned char 
         unsigned long long b = 0;
 #pragma unroll
         for (int w = 0; w < kCkBlock / 64; ++w) b ^= part[w];
-        if (b) atomicXor(out, b);
+        partials[blockIdx.x] = b;   // one slot per block: no contended atomic
+    }
+}
+
+// The block partials XORed by one workgroup (DPP wave reduction + LDS), the
+// result in *out.  A same-address atomic per block cost ~15 ns each, 60 us
+// for 4096 blocks: more than streaming the 256 MiB (profiles/r02_checksum_lab.txt).
+__global__ __launch_bounds__(kCkBlock) void checksum_finish_kernel(const unsigned long long *partials,
+                                                                   int nparts, unsigned long long *out) {
+    __shared__ unsigned long long part[kCkBlock / 64];
+    uint64_t h = 0;
+    for (int i = threadIdx.x; i < nparts; i += kCkBlock) h ^= partials[i];
+    h = wave_xor(h);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = h;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long b = 0;
+#pragma unroll
+        for (int w = 0; w < kCkBlock / 64; ++w) b ^= part[w];
+        *out = b;
     }
 }
 
@@ -116,24 +141,26 @@ hipError_t launch_checksum(int type, const void *ptr, size_t n, unsigned long lo
                            hipStream_t stream) {
     const size_t sz = type_size(type);
     if (!sz || !out) return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(out, 0, sizeof *out, stream);
-    if (e != hipSuccess || n == 0) return e;
+    if (n == 0) return hipMemsetAsync(out, 0, sizeof *out, stream);
     const size_t bytes = n * sz;
     const bool ld = type == SHMEMX_TYPE_LONGDOUBLE;
     const size_t nwords = bytes / 8, tail = bytes % 8;
     // 16-byte loads need a 16-byte aligned base; otherwise hash bytewise
     // through the tail path is too slow, so require it (hipMalloc gives 256).
     if ((reinterpret_cast<uintptr_t>(ptr) & 15u) != 0) return hipErrorInvalidValue;
-    size_t blocks = (nwords / 2 + kCkBlock * kCkUnroll - 1) / (kCkBlock * kCkUnroll);
-    if (blocks > 8192) blocks = 8192;
+    size_t blocks = (nwords / 2 + kCkBlock - 1) / kCkBlock;
+    if (blocks > (size_t)kChecksumMaxBlocks) blocks = kChecksumMaxBlocks;
     if (blocks < 1) blocks = 1;
     const unsigned char *p = static_cast<const unsigned char *>(ptr);
+    unsigned long long *partials = out + 1;
     if (ld)
         hipLaunchKernelGGL(checksum_kernel<true>, dim3((unsigned)blocks), dim3(kCkBlock), 0, stream, p,
-                           nwords, tail, out);
+                           nwords, tail, partials);
     else
         hipLaunchKernelGGL(checksum_kernel<false>, dim3((unsigned)blocks), dim3(kCkBlock), 0, stream, p,
-                           nwords, tail, out);
+                           nwords, tail, partials);
+    hipLaunchKernelGGL(checksum_finish_kernel, dim3(1), dim3(kCkBlock), 0, stream, partials, (int)blocks,
+                       out);
     return hipGetLastError();
 }
 

@@ -294,7 +294,7 @@ int checksum_impl(int type, const void *ptr, size_t nelems, unsigned long long *
     DevBuf in = device_in(ptr, bytes, g_state.cws_src, g_state.cws_src_bytes, s);
     if (bytes && !in.dev) return set_error(SHMEMX_ENOMEM);
     unsigned long long *dres = static_cast<unsigned long long *>(
-        grow(g_state.token, g_state.token_bytes, 4096));
+        grow(g_state.token, g_state.token_bytes, sizeof(unsigned long long) * (1 + kChecksumMaxBlocks)));
     if (!dres) return set_error(SHMEMX_ENOMEM);
     if (launch_checksum(type, in.dev, nelems, dres, s) != hipSuccess) return set_error(SHMEMX_EINVAL);
     SHMX_HIP(hipMemcpyAsync(out, dres, sizeof *out, hipMemcpyDeviceToHost, s));

@@ -74,7 +74,9 @@ struct SignalArgs {
 hipError_t launch_signal(const SignalArgs &a, hipStream_t stream);
 
 // Position-aware 64-bit checksum of n elements of `type` at device address
-// ptr (16-byte aligned) into *out (device memory), stream-ordered.
+// ptr (16-byte aligned) into out[0] (device memory, with room for
+// kChecksumMaxBlocks more words of block partials after it), stream-ordered.
+constexpr int kChecksumMaxBlocks = 4096;
 hipError_t launch_checksum(int type, const void *ptr, size_t n, unsigned long long *out,
                            hipStream_t stream);
 
