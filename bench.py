@@ -36,6 +36,10 @@ import torch
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "openshmem-async_amd"))
+# The bench's operands are shmem_malloc'd blocks handed to the fold kernel and
+# RCCL directly: the HBM heap's device addresses (the library's default is the
+# mirrored heap, whose host view is for reference-style host code).
+os.environ.setdefault("SHMEMX_HEAP_MEMORY", "device")
 import shmem_mi355x as shm  # noqa: E402
 
 GiB = float(1 << 30)

@@ -8,7 +8,7 @@
  * Like ISx, the arrays are static (host) variables and pSync is initialised
  * to SHMEM_SYNC_VALUE; the library stages them through the GPU.  With
  * ISX_SHMEM_MALLOC=1 in the environment the arrays are shmem_malloc'd
- * instead and written by host code — under SHMEMX_HEAP_MEMORY=mirrored that
+ * instead and written by host code — under the default (mirrored) heap that
  * is a host view of the HBM heap, and the reductions run device-resident on
  * its HBM twin (the program then prints the mirror's counters).  Exits 0 on
  * success.  Also checks pSync is left at SHMEM_SYNC_VALUE and that a few

@@ -145,9 +145,12 @@ int pshmem_n_pes(void);
 /* Part 2b: the collectives next to the reductions and the symmetric heap   */
 /* (SURVEY.md §8f).  Reference prototypes: shmem.h:595-651 (barrier),       */
 /* :1654-1684 (broadcast, [f]collect), :821-941 (symmetric heap).  The heap */
-/* is HBM: shmem_malloc returns device memory, collectively.  With          */
-/* $SHMEMX_HEAP_MEMORY=host it is page-locked host memory instead, as the   */
-/* reference's heap is, so host code can dereference symmetric objects.    */
+/* is one HBM segment per PE; by default shmem_malloc returns addresses in  */
+/* a host view of it (the mirrored heap, below), so host code dereferences  */
+/* symmetric objects as with the reference's host heap while collectives    */
+/* run on HBM.  $SHMEMX_HEAP_MEMORY=device returns the HBM addresses        */
+/* themselves (for programs whose own kernels use them); =host makes the    */
+/* heap page-locked host memory.                                            */
 
 #ifndef SHMEM_BCAST_SYNC_SIZE
 #define SHMEM_BCAST_SYNC_SIZE   64L
@@ -312,8 +315,9 @@ int shmemx_reduce_plan(int type, int op, int nreduce, int PE_start,
  * HBM copies (device addresses) for the others. */
 void *shmemx_heap_ptr(const void *addr, int pe);
 
-/* Mirrored heap ($SHMEMX_HEAP_MEMORY=mirrored): the symmetric heap is HBM and
- * shmem_malloc returns addresses in a host view of it, so host code reads and
+/* Mirrored heap (the default; $SHMEMX_HEAP_MEMORY=mirrored): the symmetric
+ * heap is HBM and shmem_malloc returns addresses in a host view of it, so
+ * host code reads and
  * writes symmetric objects as with the reference's host heap
  * (memory/symmem.c:168-227).  The collectives run on the HBM copy; the view
  * is kept coherent in 64 KiB blocks (page protection: a block the host stored

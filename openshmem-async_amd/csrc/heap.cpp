@@ -33,32 +33,37 @@ struct Private {
     size_t bytes;   // what the caller asked for
 };
 
-// $SHMEMX_HEAP_MEMORY=host: the segment (and any private block) is
-// page-locked host memory instead of HBM, as the reference's heap is
-// (comms-inline.h:752-769).  Host code can then write and read symmetric
-// objects directly, as reference programs do; reductions on them take the
-// pinned host pipeline.  Peers cannot map host segments, so shmemx_heap_ptr
-// returns NULL for them (as the reference's shmem_ptr always does) and
-// DIRECT/SIGNAL are not used on them.
-bool host_kind() {
-    static const bool h = [] {
-        const char *e = std::getenv("SHMEMX_HEAP_MEMORY");
-        return e && std::string(e) == "host";
-    }();
-    return h;
-}
+// $SHMEMX_HEAP_MEMORY picks what shmem_malloc hands out:
+//   mirrored (default)  the segment is HBM and shmem_malloc returns addresses
+//                       in a host view of it (mirror.h): host code reads and
+//                       writes symmetric objects as in the reference (whose
+//                       heap is host memory, memory/symmem.c:168-227), the
+//                       collectives run on the HBM twin, and only the blocks
+//                       the host touched cross PCIe;
+//   device (or hbm)     the HBM segment itself: device addresses, for
+//                       programs whose own kernels use symmetric objects;
+//   host                page-locked host memory instead of HBM
+//                       (comms-inline.h:752-769): reductions on it take the
+//                       pinned host pipeline; peers cannot map host segments,
+//                       so shmemx_heap_ptr returns NULL for them (as the
+//                       reference's shmem_ptr always does) and DIRECT/SIGNAL
+//                       are not used on them.
+enum HeapMode { kMirrored, kDevice, kHost };
 
-// $SHMEMX_HEAP_MEMORY=mirrored: the segment is HBM as by default, and
-// shmem_malloc returns addresses in a host view of it (mirror.h): host code
-// reads and writes symmetric objects as in the reference, the collectives
-// run on the HBM twin, and only the blocks the host touched cross PCIe.
-bool mirrored() {
-    static const bool m = [] {
+HeapMode heap_mode() {
+    static const HeapMode m = [] {
         const char *e = std::getenv("SHMEMX_HEAP_MEMORY");
-        return e && std::string(e) == "mirrored";
+        const std::string v = e ? e : "";
+        if (v.empty() || v == "mirrored") return kMirrored;
+        if (v == "device" || v == "hbm") return kDevice;
+        if (v == "host") return kHost;
+        fatal("shmem_malloc", "SHMEMX_HEAP_MEMORY must be mirrored, device (hbm) or host");
     }();
     return m;
 }
+
+bool host_kind() { return heap_mode() == kHost; }
+bool mirrored() { return heap_mode() == kMirrored; }
 
 hipError_t seg_alloc(void **p, size_t bytes) {
     return host_kind() ? hipHostMalloc(p, bytes, hipHostMallocDefault) : hipMalloc(p, bytes);

@@ -65,7 +65,7 @@ bool is_symmetric(const void *p);
 // PE.  nullptr if there is no segment.
 unsigned long long *signal_area();
 uint64_t signal_offset();
-// Mirrored heap ($SHMEMX_HEAP_MEMORY=mirrored, mirror.h).  A collective
+// Mirrored heap (the default, mirror.h).  A collective
 // about to read or write [p, p + bytes): if that range lies in the host view,
 // the host's stores in it go to HBM and the HBM twin's address is returned;
 // any other p is returned as it is.

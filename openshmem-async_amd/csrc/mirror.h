@@ -1,4 +1,5 @@
-// Host view of the HBM symmetric heap ($SHMEMX_HEAP_MEMORY=mirrored).
+// Host view of the HBM symmetric heap (the default heap mode;
+// $SHMEMX_HEAP_MEMORY=mirrored).
 //
 // The reference's symmetric heap is host memory (memory/symmem.c:168-227,
 // comms-inline.h:722-801): programs write symmetric objects with plain host

@@ -14,6 +14,12 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "openshmem-async_amd"))
 sys.path.insert(0, os.path.join(REPO, "oracle"))
 
+# The tests hand shmem_malloc'd blocks to HIP copies and kernels directly, so
+# they run with the HBM heap's device addresses; the library's default (a
+# mirrored heap whose host view reference-style host code writes) and the
+# host-kind heap have tests of their own that set the variable explicitly.
+os.environ.setdefault("SHMEMX_HEAP_MEMORY", "device")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu)")

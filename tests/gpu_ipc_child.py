@@ -216,8 +216,8 @@ def run_collect(bits, counts, st, mode, seed):
         fails.append(f"{kind}{bits} counts={counts} set={st} mode={mode} err={shm.last_error()}")
 
 
-MIRRORED = os.environ.get("SHMEMX_HEAP_MEMORY") == "mirrored"
-CAP = 1 << 23 if os.environ.get("SHMEMX_HEAP_MEMORY") not in ("host", "mirrored") else 48 << 20
+MIRRORED = os.environ.get("SHMEMX_HEAP_MEMORY", "mirrored") == "mirrored"   # the default
+CAP = 1 << 23 if not (MIRRORED or os.environ.get("SHMEMX_HEAP_MEMORY") == "host") else 48 << 20
 HEAP_SRC = shm.malloc(CAP + 64)
 HEAP_TGT = shm.malloc(CAP)
 assert HEAP_SRC and HEAP_TGT, "shmem_malloc failed"

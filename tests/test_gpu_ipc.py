@@ -43,7 +43,11 @@ def start_pes(tmp_path, npes, scenario, extra_env=None):
             env["GPU_MAX_HW_QUEUES"] = "2"
         env.pop("RANK", None)
         env.pop("WORLD_SIZE", None)
-        env.update(extra_env or {})
+        for k, v in (extra_env or {}).items():   # None: unset
+            if v is None:
+                env.pop(k, None)
+            else:
+                env[k] = v
         out = str(tmp_path / f"pe{pe}.json")
         log = open(os.path.join(logdir, f"pe{pe}.log") if logdir else tmp_path / f"pe{pe}.log", "w")
         procs.append((subprocess.Popen([sys.executable, os.path.join(HERE, "gpu_ipc_child.py"), out,
@@ -283,16 +287,18 @@ def test_mixed_memory_kinds_fail_collectively(tmp_path, transport):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("transport,npes", [("ipc", 1), ("ipc", 4), ("rccl", 3)])
-def test_mirrored_heap(tmp_path, transport, npes):
+@pytest.mark.parametrize("transport,npes,mode", [("ipc", 1, "mirrored"), ("ipc", 4, "mirrored"),
+                                                ("rccl", 3, "mirrored"), ("ipc", 2, None)])
+def test_mirrored_heap(tmp_path, transport, npes, mode):
     """$SHMEMX_HEAP_MEMORY=mirrored: shmem_malloc returns a host view of the
     HBM heap; host code writes and reads symmetric objects with plain stores
     and loads, the collectives run device-resident on the HBM twins (DIRECT
     over the peers' HBM on the IPC transport), only touched blocks cross
     PCIe (a repeated call on untouched sources copies nothing up), against
     the oracle for every reference pair and active set, SIGNAL, in place,
-    broadcast and collect."""
-    env = {"SHMEMX_TRANSPORT": transport, "SHMEMX_HEAP_MEMORY": "mirrored"}
+    broadcast and collect.  mode None: the variable unset — the mirrored
+    heap is the library's default."""
+    env = {"SHMEMX_TRANSPORT": transport, "SHMEMX_HEAP_MEMORY": mode}
     if transport == "rccl":
         env["FAKE_RCCL"] = os.path.join(HERE, "native", "libfake_rccl.so")
     reports = run_pes(tmp_path, npes, "mirrored", env, timeout=600)
