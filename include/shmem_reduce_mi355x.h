@@ -330,12 +330,19 @@ void *shmemx_heap_ptr(const void *addr, int pe);
  *                             to HBM now;
  *   shmemx_mirror_invalidate  after the caller's own kernels wrote the HBM
  *                             twin: the host view re-reads it on next access;
+ *   shmemx_mirror_acquire     make [addr, addr + bytes) current in the view
+ *                             (and, with for_write, writable) now, for code
+ *                             that cannot take the page fault: a system call
+ *                             given a view address (write(2) of a result,
+ *                             read(2) into a source) fails with EFAULT on a
+ *                             block the library has not opened;
  *   shmemx_mirror_stats       out[0..4] = write faults, read faults, blocks
  *                             copied to HBM, blocks copied back, blocks marked
  *                             device-newer; returns how many were filled. */
 void *shmemx_mirror_device_ptr(const void *addr);
 int shmemx_mirror_sync(const void *addr, size_t bytes);
 int shmemx_mirror_invalidate(const void *addr, size_t bytes);
+int shmemx_mirror_acquire(const void *addr, size_t bytes, int for_write);
 int shmemx_mirror_stats(unsigned long long *out, int nout, int reset);
 
 /* Host-side phase times of the DIRECT algorithm since the last reset, for

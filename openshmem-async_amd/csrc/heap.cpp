@@ -361,6 +361,13 @@ void device_wrote(const void *p, size_t bytes) {
     if (bytes && in_view(p)) mirror::device_wrote((uint64_t)(static_cast<const char *>(p) - g_heap.view), bytes);
 }
 
+bool host_acquire(const void *p, size_t bytes, bool write) {
+    if (!in_view(p) || bytes > g_heap.arena.capacity() - (uint64_t)(static_cast<const char *>(p) - g_heap.view))
+        return false;
+    mirror::acquire((uint64_t)(static_cast<const char *>(p) - g_heap.view), bytes, write);
+    return true;
+}
+
 void flush_view() {
     if (g_heap.view) mirror::flush(0, g_heap.arena.capacity());
 }

@@ -76,6 +76,10 @@ void *device_operand_open(const void *p);
 // After a collective wrote [p, p + bytes) (a host-view address) in HBM: the
 // host view of it is stale until the next host access fetches it.
 void device_wrote(const void *p, size_t bytes);
+// shmemx_mirror_acquire: [p, p + bytes) of the view made current (and, with
+// `write`, writable) for host code that cannot take a page fault; false if
+// the range is not in the view.
+bool host_acquire(const void *p, size_t bytes, bool write);
 // Every host store in the view to HBM (barriers: peers may read it next).
 void flush_view();
 // Offset of a host-view address in the segment; false if not in the view.

@@ -193,6 +193,27 @@ size_t device_wrote(uint64_t off, size_t bytes) {
     return n;
 }
 
+size_t acquire(uint64_t off, size_t bytes, bool write) {
+    if (!g_view.base || !bytes) return 0;
+    Guard g;
+    const size_t b0 = block_of(off), b1 = std::min(block_of(off + bytes - 1) + 1, g_view.nblocks);
+    size_t fetched = 0;
+    for (size_t b = b0; b < b1;) {
+        size_t e = b;
+        while (e < b1 && g_view.state[e] == g_view.state[b]) ++e;
+        if (g_view.state[b] == DEVICE_NEWER) {
+            fetch_run(b, e - b);
+            fetched += e - b;
+        }
+        if (write && g_view.state[b] == CLEAN) {
+            protect(b, e - b, PROT_READ | PROT_WRITE);
+            std::memset(g_view.state + b, HOST_NEWER, e - b);
+        }
+        b = e;
+    }
+    return fetched;
+}
+
 void fetch_all() {
     if (!g_view.base) return;
     Guard g;

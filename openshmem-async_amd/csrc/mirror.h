@@ -85,6 +85,12 @@ size_t flush(uint64_t off, size_t bytes);
 // After a collective wrote [off, off + bytes) in HBM: the overlapped blocks
 // become DEVICE_NEWER (call flush on the range first).  Returns the blocks.
 size_t device_wrote(uint64_t off, size_t bytes);
+// Make [off, off + bytes) accessible to host code that cannot take the page
+// fault — system calls (write(2) of a result, read(2) into a source), other
+// libraries' DMA: DEVICE_NEWER blocks are copied back (readable, CLEAN), and
+// with `write` every block becomes HOST_NEWER (read-write).  Returns the
+// blocks copied back.
+size_t acquire(uint64_t off, size_t bytes, bool write);
 // Make the whole view current on the host (every DEVICE_NEWER block copied
 // back), e.g. before the view is released.
 void fetch_all();

@@ -827,6 +827,12 @@ int shmemx_mirror_invalidate(const void *addr, size_t bytes) {
     return SHMEMX_OK;
 }
 
+int shmemx_mirror_acquire(const void *addr, size_t bytes, int for_write) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    if (!heap::host_acquire(addr, bytes, for_write != 0)) return set_error(SHMEMX_EINVAL);
+    return SHMEMX_OK;
+}
+
 int shmemx_direct_stats(double *out, int nout, int reset) {
     std::lock_guard<std::recursive_mutex> lk(g_mu);
     if (!out || nout < 0) {

@@ -135,6 +135,8 @@ def lib() -> ctypes.CDLL:
     L.shmemx_mirror_sync.restype = i
     L.shmemx_mirror_invalidate.argtypes = [vp, sz]
     L.shmemx_mirror_invalidate.restype = i
+    L.shmemx_mirror_acquire.argtypes = [vp, sz, i]
+    L.shmemx_mirror_acquire.restype = i
     L.shmemx_direct_stats.argtypes = [ctypes.POINTER(ctypes.c_double), i, i]
     L.shmemx_direct_stats.restype = i
     L.shmemx_host_register.argtypes = [vp, sz]
@@ -384,6 +386,13 @@ def mirror_sync(address: int, nbytes: int) -> None:
 
 def mirror_invalidate(address: int, nbytes: int) -> None:
     _check(lib().shmemx_mirror_invalidate(address, nbytes), "shmemx_mirror_invalidate")
+
+
+def mirror_acquire(address: int, nbytes: int, for_write: bool = False) -> None:
+    """shmemx_mirror_acquire: open [address, address + nbytes) of the view to
+    code that cannot take the page fault (system calls)."""
+    _check(lib().shmemx_mirror_acquire(address, nbytes, 1 if for_write else 0),
+           "shmemx_mirror_acquire")
 
 
 def host_register(buf, nbytes: int) -> None:

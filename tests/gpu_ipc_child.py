@@ -613,6 +613,29 @@ elif scenario == "mirrored":
     if not same_bits(got, want) or st["blocks_fetched"] not in (nblk, nblk + 1):
         fails.append(f"mirrored read-back: {st}")
     print(f"repeat 32 MiB call on untouched mirrored operands: {dt * 1e3:.2f} ms", flush=True)
+    # a system call given a view address does not take the page fault: on the
+    # target a collective just wrote it fails with EFAULT, and
+    # shmemx_mirror_acquire opens the range first (write(2) of a result)
+    import ctypes
+    import errno
+    import tempfile
+    shm.to_all("double", "sum", HEAP_TGT, HEAP_SRC, n, 0, 0, npes)
+    nb = 1 << 20
+    with tempfile.TemporaryFile() as f:
+        raw = (ctypes.c_char * nb).from_address(HEAP_TGT)
+        try:
+            os.write(f.fileno(), raw)
+            fails.append("mirrored: write(2) of a device-newer target did not fail")
+        except OSError as e:
+            if e.errno != errno.EFAULT:
+                fails.append(f"mirrored: write(2) failed with {e}, want EFAULT")
+        shm.mirror_acquire(HEAP_TGT, nb)
+        if os.write(f.fileno(), raw) != nb:
+            fails.append("mirrored: short write(2) after shmemx_mirror_acquire")
+        f.seek(0)
+        if not same_bits(np.frombuffer(f.read(), dtype=np.float64), want[:nb // 8]):
+            fails.append("mirrored: write(2) after shmemx_mirror_acquire wrote wrong bytes")
+    ncases += 1
     # SIGNAL (device barriers) on the view addresses: the twins are symmetric
     seed += 1
     srcs = oracle.sources("float", 1, npes, 70001, base_seed=seed)

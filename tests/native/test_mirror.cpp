@@ -5,6 +5,9 @@
 // writes are checked against a model: after every step the host view reads
 // what the model says, flush pushes exactly the blocks the host stored to,
 // and nothing else crosses the "PCIe" backend.
+#include <unistd.h>
+
+#include <cerrno>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -95,6 +98,44 @@ int main(int argc, char **argv) {
     truth[11 * M::kBlock] = 99;
     CHECK(M::state_of(11 * M::kBlock) == M::HOST_NEWER);
     CHECK(h[11 * M::kBlock + 1] == truth[11 * M::kBlock + 1]);
+
+    // system calls do not take the page fault: on a block the library has
+    // not opened they fail with EFAULT, and acquire() opens the range
+    {
+        int fds[2];
+        CHECK(pipe(fds) == 0);
+        M::flush(40 * M::kBlock, 2 * M::kBlock);
+        for (size_t i = 40 * M::kBlock; i < 42 * M::kBlock; ++i) {
+            g_dev[i] = (unsigned char)(i * 5 + 3);
+            truth[i] = g_dev[i];
+        }
+        M::device_wrote(40 * M::kBlock, 2 * M::kBlock);
+        const char *v = M::host_base();
+        errno = 0;
+        CHECK(write(fds[1], v + 40 * M::kBlock + 100, 1000) == -1 && errno == EFAULT);
+        CHECK(M::acquire(40 * M::kBlock + 100, 1000, false) == 1);   // one block back
+        CHECK(M::state_of(40 * M::kBlock) == M::CLEAN && M::state_of(41 * M::kBlock) == M::DEVICE_NEWER);
+        CHECK(write(fds[1], v + 40 * M::kBlock + 100, 1000) == 1000);
+        unsigned char buf[1000];
+        CHECK(read(fds[0], buf, 1000) == 1000);
+        CHECK(std::memcmp(buf, truth.data() + 40 * M::kBlock + 100, 1000) == 0);
+        // read(2) into a CLEAN (read-only) block: EFAULT until acquired for writing
+        std::memset(buf, 0x5A, sizeof buf);
+        CHECK(write(fds[1], buf, 1000) == 1000);
+        errno = 0;
+        CHECK(read(fds[0], const_cast<char *>(v) + 40 * M::kBlock + 7, 1000) == -1 && errno == EFAULT);
+        CHECK(M::acquire(40 * M::kBlock + 7, 1000, true) == 0);
+        CHECK(M::state_of(40 * M::kBlock) == M::HOST_NEWER);
+        CHECK(read(fds[0], const_cast<char *>(v) + 40 * M::kBlock + 7, 1000) == 1000);
+        std::memset(truth.data() + 40 * M::kBlock + 7, 0x5A, 1000);
+        g_h2d = 0;
+        CHECK(M::flush(40 * M::kBlock, 1) == 1 && g_dev[40 * M::kBlock + 7] == 0x5A);
+        // acquire for writing across a DEVICE_NEWER block fetches it first
+        CHECK(M::acquire(41 * M::kBlock, 10, true) == 1 && M::state_of(41 * M::kBlock) == M::HOST_NEWER);
+        CHECK(h[41 * M::kBlock + 5] == truth[41 * M::kBlock + 5]);
+        close(fds[0]);
+        close(fds[1]);
+    }
 
     // random interleavings against the model
     std::mt19937_64 rng(12345);
