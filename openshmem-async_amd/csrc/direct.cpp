@@ -222,6 +222,16 @@ void node_sync(int start, int step, int P, hipStream_t s, double *stream_us, dou
     if (barrier_us) *barrier_us += now_us() - t1;
 }
 
+void node_done(int start, int step, int P, hipStream_t s, double *stream_us, double *barrier_us,
+               double since_us) {
+    const double t0 = since_us >= 0 ? since_us : now_us();
+    SHMX_HIP(hipStreamSynchronize(s));
+    const double t1 = now_us();
+    node::barrier(start, step, P);
+    if (stream_us) *stream_us += t1 - t0;
+    if (barrier_us) *barrier_us += now_us() - t1;
+}
+
 int direct_stats(double *out, int nout, bool reset) {
     // [calls, 6 phase times, host fences, host refills, device fence
     // checks, device fences that missed an XCD]
@@ -372,7 +382,7 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
             const double tf = now_us();
             fold_chain(type, op, out, ins.data(), P, cnt, s);
             // reduce-op.c:250: no member reads my source any more
-            node_sync(start, step, P, s, &g_phase_us[kFold], &g_phase_us[kExitBarrier], tf);
+            node_done(start, step, P, s, &g_phase_us[kFold], &g_phase_us[kExitBarrier], tf);
             if (stage_tgt)
                 SHMX_HIP(hipMemcpyAsync(tgt + c0 * sz, scratch_tgt, cnt * sz, hipMemcpyDeviceToDevice, s));
             continue;
@@ -406,7 +416,7 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
         const double tg = now_us();
         SHMX_HIP(launch_gather(from.data(), to.data(), len.data(), (int)from.size(), s));
         // reduce-op.c:250: no member reads my slice any more
-        node_sync(start, step, P, s, &g_phase_us[kGather], &g_phase_us[kExitBarrier], tg);
+        node_done(start, step, P, s, &g_phase_us[kGather], &g_phase_us[kExitBarrier], tg);
     }
     if (local_write && stage_tgt) SHMX_HIP(hipStreamSynchronize(s));
     return SHMEMX_OK;

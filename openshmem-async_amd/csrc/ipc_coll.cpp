@@ -93,7 +93,7 @@ int ipc_broadcast(char *target, const char *source, size_t bytes, int root_idx, 
             std::vector<size_t> len{cnt};
             pull(from, to, len, s);
         }
-        node_sync(start, step, P, s);   // the root's copy is no longer read
+        node_done(start, step, P, s);   // the root's copy is no longer read
     }
     if (tstaged) {
         SHMX_HIP(hipMemcpyAsync(target, dst, bytes, hipMemcpyDeviceToHost, s));
@@ -163,7 +163,7 @@ int ipc_collect(char *target, const char *source, size_t esize, size_t nelems, i
             n.push_back(std::min(H, len[i] - r * H));
         }
         pull(from, to, n, s);
-        node_sync(start, step, P, s);   // nobody reads this round's copies any more
+        node_done(start, step, P, s);   // nobody reads this round's copies any more
     }
     if (tstaged) {
         SHMX_HIP(hipMemcpyAsync(target, dst, total, hipMemcpyDeviceToHost, s));

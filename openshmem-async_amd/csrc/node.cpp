@@ -66,20 +66,29 @@ double barrier_timeout_s() {
 
 char g_ipc_error[160] = "no IPC error";
 
-// Waiting for a peer: spin first (a barrier between busy PEs completes in
-// microseconds), then yield, then sleep in growing steps up to 100 us, so
-// PEs that wait long — more PE processes than free CPUs, a peer still
-// copying — do not take the CPU from the ones doing the work.
-void backoff(unsigned spins) {
-    if (spins < 512) return;
-    if (spins < 2048) {
-        sched_yield();
-        return;
+// Waiting for a peer, by elapsed time: spin for the first 200 us (a barrier
+// between busy PEs completes in microseconds, and a sleep — even a 5 us
+// nanosleep, which the kernel's timer slack stretches to ~55 us — would add
+// more than the whole barrier costs), then yield up to 10 ms, then sleep in
+// 50 us steps, so PEs that wait long (more PE processes than free CPUs, a
+// peer still copying) do not take the CPU from the ones doing the work.
+struct Backoff {
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    unsigned spins = 0;
+    double waited_s = 0;
+    void step() {
+        if ((++spins & 63) == 0)
+            waited_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (waited_s < 200e-6) {
+            __builtin_ia32_pause();
+        } else if (waited_s < 10e-3) {
+            sched_yield();
+        } else {
+            struct timespec ts = {0, 50 * 1000};
+            nanosleep(&ts, nullptr);
+        }
     }
-    const unsigned us = spins < 2048 + 64 ? 5u : (spins < 2048 + 512 ? 20u : 100u);
-    struct timespec ts = {0, (long)us * 1000};
-    nanosleep(&ts, nullptr);
-}
+};
 
 void close_peer(Region r, int q) {
     Mapping &mp = g_node.peer[r][q];
@@ -143,16 +152,13 @@ void barrier(int start, int step, int P) {
         ++g_node.entered[q];
         sh->flag[q][me].fetch_add(1, std::memory_order_acq_rel);
     }
-    const auto t0 = std::chrono::steady_clock::now();
-    unsigned spins = 0;
+    Backoff bo;
     for (int i = 0; i < P; ++i) {
         const int q = start + i * step;
         if (q == me) continue;
         while (sh->flag[me][q].load(std::memory_order_acquire) < g_node.entered[q]) {
-            backoff(++spins);
-            if ((spins & 255) == 0 &&
-                std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() >
-                    barrier_timeout_s()) {
+            bo.step();
+            if (bo.waited_s > barrier_timeout_s()) {
                 char why[96];
                 snprintf(why, sizeof why, "PE %d never reached the barrier", q);
                 fatal("node barrier", why);

@@ -127,6 +127,12 @@ FenceRecords fence_records();
 // steady-clock stamp in microseconds, if >= 0) and in the barrier.
 void node_sync(int start, int step, int P, hipStream_t s, double *stream_us = nullptr,
                double *barrier_us = nullptr, double since_us = -1);
+// The end of a pull phase: this PE's kernels have finished reading the
+// peers' arrays (hipStreamSynchronize, no fence: nothing is handed over —
+// the next phase that publishes data runs node_sync, whose fence also drops
+// any peer lines this PE's L2 still holds), then the host barrier.
+void node_done(int start, int step, int P, hipStream_t s, double *stream_us = nullptr,
+               double *barrier_us = nullptr, double since_us = -1);
 // Map the peers' regions a collective reads (node::peer_base), voting across
 // the set the first time a combination is met; false on every member alike
 // if any member failed (direct.cpp).
