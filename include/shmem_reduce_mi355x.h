@@ -353,7 +353,8 @@ int shmemx_mirror_stats(unsigned long long *out, int nout, int reset);
  * system-fence coverage counters (every XCD must run the fence that hands
  * data to the peers): [7] fences checked on the host, [8] of them run again
  * because a block did not reach some XCD, [9] fences checked by the SIGNAL
- * device barrier, [10] of them incomplete (the call fails).  Fills at most
+ * device barrier, [10] of them incomplete (the call fails); [11] one-shot
+ * calls (DIRECT or SIGNAL) that ran as one fused launch.  Fills at most
  * nout values and returns how many; reset != 0 zeroes the counters. */
 int shmemx_direct_stats(double *out, int nout, int reset);
 

@@ -110,6 +110,7 @@ namespace {
 enum Phase { kEntryWait, kEntryBarrier, kFold, kFoldBarrier, kGather, kExitBarrier, kNumPhases };
 double g_phase_us[kNumPhases];
 double g_calls;
+double g_fused_calls;   // one-shot calls that ran as one fused launch (DIRECT and SIGNAL)
 
 double now_us() {
     return std::chrono::duration<double, std::micro>(
@@ -156,6 +157,7 @@ struct FenceState {
     unsigned int *host_seen = nullptr;         // host-coherent, kFenceBlocks words
     unsigned int *dev_seen = nullptr;          // device, kFenceBlocks words
     unsigned long long *dev_stats = nullptr;   // device: [checks, incomplete]
+    unsigned int *gsync = nullptr;             // device: fused kernel's grid barrier
     int nxcc = 0;
     double host_checks = 0, host_refills = 0;
 } g_fence;
@@ -176,6 +178,10 @@ void ensure_fence() {
     SHMX_HIP(hipMemset(d, 0, kFenceBlocks * sizeof(unsigned int)));
     SHMX_HIP(hipMalloc(&st, 2 * sizeof(unsigned long long)));
     SHMX_HIP(hipMemset(st, 0, 2 * sizeof(unsigned long long)));
+    void *gs = nullptr;
+    SHMX_HIP(hipMalloc(&gs, 2 * sizeof(unsigned int)));
+    SHMX_HIP(hipMemset(gs, 0, 2 * sizeof(unsigned int)));
+    g_fence.gsync = static_cast<unsigned int *>(gs);
     SHMX_HIP(hipDeviceSynchronize());
     g_fence.host_seen = static_cast<unsigned int *>(h);
     g_fence.dev_seen = static_cast<unsigned int *>(d);
@@ -208,7 +214,7 @@ void fence_and_wait(hipStream_t s) {
 
 FenceRecords fence_records() {
     ensure_fence();
-    return FenceRecords{g_fence.dev_seen, g_fence.nxcc, g_fence.dev_stats};
+    return FenceRecords{g_fence.dev_seen, g_fence.nxcc, g_fence.dev_stats, g_fence.gsync};
 }
 
 void node_sync(int start, int step, int P, hipStream_t s, double *stream_us, double *barrier_us,
@@ -232,10 +238,36 @@ void node_done(int start, int step, int P, hipStream_t s, double *stream_us, dou
     if (barrier_us) *barrier_us += now_us() - t1;
 }
 
+void count_fused_call() { g_fused_calls += 1; }
+
+bool signal_args(int start, int step, int P, SignalArgs *sa) {
+    unsigned long long *mine = heap::signal_area();
+    if (!mine || P > kMaxFoldInputs) return false;
+    *sa = SignalArgs{};
+    sa->mine = mine;
+    sa->P = P;
+    sa->me = g_state.pe;
+    sa->timeout_ticks = signal_timeout_ticks();
+    sa->err = signal_error_word();
+    const FenceRecords fr = fence_records();
+    sa->seen = fr.seen;
+    sa->nxcc = fr.nxcc;
+    sa->fence_stats = fr.stats;
+    const uint64_t sig = heap::signal_offset();
+    for (int i = 0; i < P; ++i) {
+        const int q = start + i * step;
+        char *b = node::peer_base(node::kHeap, q);
+        if (!b) return false;
+        sa->pe[i] = q;
+        sa->peer[i] = reinterpret_cast<const unsigned long long *>(b + sig);
+    }
+    return true;
+}
+
 int direct_stats(double *out, int nout, bool reset) {
     // [calls, 6 phase times, host fences, host refills, device fence
-    // checks, device fences that missed an XCD]
-    double all[1 + kNumPhases + 4] = {g_calls};
+    // checks, device fences that missed an XCD, fused one-shot calls]
+    double all[1 + kNumPhases + 5] = {g_calls};
     for (int i = 0; i < kNumPhases; ++i) all[1 + i] = g_phase_us[i];
     unsigned long long dev[2] = {0, 0};
     if (g_fence.dev_stats) {
@@ -246,12 +278,14 @@ int direct_stats(double *out, int nout, bool reset) {
     all[2 + kNumPhases] = g_fence.host_refills;
     all[3 + kNumPhases] = (double)dev[0];
     all[4 + kNumPhases] = (double)dev[1];
+    all[5 + kNumPhases] = g_fused_calls;
     const int k = std::min(nout, (int)(sizeof all / sizeof all[0]));
     for (int i = 0; i < k; ++i) out[i] = all[i];
     if (reset) {
         g_calls = 0;
         for (double &v : g_phase_us) v = 0;
         g_fence.host_checks = g_fence.host_refills = 0;
+        g_fused_calls = 0;
         if (g_fence.dev_stats) SHMX_HIP(hipMemset(g_fence.dev_stats, 0, sizeof dev));
     }
     return k;
@@ -268,6 +302,7 @@ void direct_release() {
         (void)hipHostFree(g_fence.host_seen);
         (void)hipFree(g_fence.dev_seen);
         (void)hipFree(g_fence.dev_stats);
+        (void)hipFree(g_fence.gsync);
         g_fence = FenceState{};
     }
     if (!g_scratch.base) return;
@@ -275,6 +310,50 @@ void direct_release() {
     (void)hipFree(g_scratch.base);
     g_scratch = Scratch{};
 }
+
+namespace {
+
+// DIRECT's one shot as one fused launch (launch_signal_fold): every member's
+// source (heap or staged scratch, per the descriptors) and every member's
+// heap segment (the signal counters) mapped, then the launch and one wait.
+int direct_fused(int type, int op, char *tgt, const char *src, size_t n, int start, int step, int P,
+                 const std::vector<node::Desc> &desc, bool stage_tgt, hipStream_t s) {
+    (void)src;
+    std::vector<std::pair<node::Region, int>> regs;
+    for (int i = 0; i < P; ++i) {
+        regs.emplace_back(static_cast<node::Region>(desc[i].src.region), start + i * step);
+        regs.emplace_back(node::kHeap, start + i * step);
+    }
+    if (!map_regions(regs, start, step, P)) {
+        trace(LOG_REDUCTION, "DIRECT: a member could not map a peer region (%s)", node::last_ipc_error());
+        return set_error(SHMEMX_ENOTSUP);
+    }
+    SignalFoldArgs fa{};
+    if (!signal_args(start, step, P, &fa.sig)) fatal("DIRECT", "a mapped peer heap went missing");
+    fa.gsync = fence_records().gsync;
+    const size_t sz = type_size(type);
+    char *const scratch_tgt = g_scratch.base + g_scratch.bytes / 2;
+    fa.out = stage_tgt ? scratch_tgt : tgt;
+    for (int i = 0; i < P; ++i)
+        fa.ins[i] = node::peer_base(static_cast<node::Region>(desc[i].src.region), start + i * step) +
+                    desc[i].src.off;
+    fa.nins = P;
+    fa.n = n;
+    const double t0 = now_us();
+    SHMX_HIP(launch_signal_fold(type, op, fa, s));   // reduce-op.c:217-250
+    if (stage_tgt) SHMX_HIP(hipMemcpyAsync(tgt, scratch_tgt, n * sz, hipMemcpyDeviceToDevice, s));
+    SHMX_HIP(hipStreamSynchronize(s));
+    g_phase_us[kFold] += now_us() - t0;
+    count_fused_call();
+    switch (signal_error()) {
+    case 0: break;
+    case 2: fatal("DIRECT reduction", "a system fence before a device barrier missed an XCD");
+    default: fatal("DIRECT reduction", "a member never reached the device barrier");
+    }
+    return SHMEMX_OK;
+}
+
+}  // namespace
 
 int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int start,
                   int logstride, const shmemx_plan_t &p, bool own_order, hipStream_t s) {
@@ -321,22 +400,45 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     // count: bit 0 "I stage through scratch", bit 1 "my target starts inside
     // my source" — then chunks must run last to first, as memmove would, or
     // a chunk's copy-out overwrites source elements of the next chunk
-    d.count = (stage_src || stage_tgt ? 1 : 0) | (partial && tgt > src ? 2 : 0);
+    // bit 2: "I can take the fused one-shot launch" (I have the signal
+    // counters, at the top of my heap segment)
+    d.count = (stage_src || stage_tgt ? 1 : 0) | (partial && tgt > src ? 2 : 0) |
+              (one_shot && heap::signal_area() ? 4 : 0);
     node::put_desc(d);
     // One chunk (n <= cmax, known alike everywhere): stage it right away.
     const bool single = n <= cmax;
     if (single && stage_src)
         SHMX_HIP(hipMemcpyAsync(g_scratch.base, src, bytes, hipMemcpyDeviceToDevice, s));
     g_calls += 1;
-    // my source (and its staging) is complete; reduce-op.c:217
-    node_sync(start, step, P, s, &g_phase_us[kEntryWait], &g_phase_us[kEntryBarrier]);
+    std::vector<node::Desc> desc(P);
+    auto read_descs = [&] {
+        for (int i = 0; i < P; ++i) desc[i] = i == m ? d : node::get_desc(pe_of(i));
+    };
+    if (one_shot) {
+        // The descriptors first, with no fence: when every member can, the
+        // whole call is one fused launch (system fence on every XCD, device
+        // barrier, fold, device barrier — launch_signal_fold) and one wait,
+        // instead of two fenced host syncs around the fold.  All members see
+        // the same descriptors, so all take the same path.
+        const double t0 = now_us();
+        node::barrier(start, step, P);
+        g_phase_us[kEntryBarrier] += now_us() - t0;
+        read_descs();
+        bool fuse = true;
+        for (int i = 0; i < P; ++i) fuse &= (desc[i].count & 4) != 0;
+        if (fuse) return direct_fused(type, op, tgt, src, n, start, step, P, desc, stage_tgt, s);
+        // my source (and its staging) is complete; reduce-op.c:217
+        node_sync(start, step, P, s, &g_phase_us[kEntryWait], &g_phase_us[kEntryBarrier]);
+    } else {
+        // my source (and its staging) is complete; reduce-op.c:217
+        node_sync(start, step, P, s, &g_phase_us[kEntryWait], &g_phase_us[kEntryBarrier]);
+        read_descs();
+    }
 
     // Every member reads the same descriptors, so all cut the same chunks
     // and walk them in the same direction.
-    std::vector<node::Desc> desc(P);
     bool chunked = false, backwards = false;
     for (int i = 0; i < P; ++i) {
-        desc[i] = i == m ? d : node::get_desc(pe_of(i));
         chunked |= (desc[i].count & 1) != 0;
         backwards |= (desc[i].count & 2) != 0;
     }

@@ -592,7 +592,145 @@ __global__ __launch_bounds__(64) void signal_kernel(SignalArgs a) {
     }
 }
 
+// ------------------------------------------------ fused one-shot (SIGNAL)
+// Thread 0 of the last block to arrive: bump my counter for every peer
+// (system-scope release: everything this GPU's blocks fenced before arriving
+// is in memory first), then wait for every peer's counter for me.
+__device__ void peer_handshake(const SignalArgs &a) {
+    unsigned long long want[kMaxFoldInputs];
+    for (int i = 0; i < a.P; ++i) {
+        if (a.pe[i] == a.me) continue;
+        unsigned long long *c = a.mine + a.pe[i];
+        want[i] = __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) + 1;
+        __hip_atomic_store(c, want[i], __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (int i = 0; i < a.P; ++i) {
+        if (a.pe[i] == a.me) continue;
+        const unsigned long long *theirs = a.peer[i] + a.me;
+        while (__hip_atomic_load(theirs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < want[i]) {
+            if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+                __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                return;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope
+}
+
+// Grid arrival (thread 0 of each block).  Returns true in the last block to
+// arrive, which runs `last` and then releases the others (if `wait`).
+template <typename F>
+__device__ __forceinline__ void grid_arrive(unsigned int *gsync, bool wait, F last) {
+    const unsigned int gen0 = __hip_atomic_load(gsync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned int old =
+        __hip_atomic_fetch_add(gsync, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == gridDim.x - 1) {
+        last();
+        __hip_atomic_store(gsync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(gsync + 1, gen0 + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (wait) {
+        while (__hip_atomic_load(gsync + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen0)
+            __builtin_amdgcn_s_sleep(1);
+    }
+}
+
+template <typename T, int OP>
+__global__ __launch_bounds__(kBlock) void signal_fold_kernel(SignalFoldArgs a) {
+    if (threadIdx.x == 0) {
+        // entry: this block's XCD writes back its L2 and drops stale peer
+        // lines, and says which XCD it was
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");   // system scope
+        const unsigned int xcc = (unsigned int)__builtin_amdgcn_s_getreg(kXccIdReg) & 15u;
+        __hip_atomic_store(a.sig.seen + blockIdx.x, kFenceSeen | xcc, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        grid_arrive(a.gsync, true, [&] {
+            unsigned int mask = 0;
+            for (unsigned int b = 0; b < gridDim.x; ++b) {
+                const unsigned int r =
+                    __hip_atomic_load(a.sig.seen + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (r & kFenceSeen) mask |= 1u << (r & 15u);
+                __hip_atomic_store(a.sig.seen + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            atomicAdd(a.sig.fence_stats, 1ull);
+            if (__builtin_popcount(mask) < a.sig.nxcc) {
+                atomicAdd(a.sig.fence_stats + 1, 1ull);
+                __hip_atomic_store(a.sig.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            peer_handshake(a.sig);   // reduce-op.c:217
+        });
+    }
+    __syncthreads();
+    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x, nthr = (size_t)gridDim.x * kBlock;
+    T *out = static_cast<T *>(a.out);
+    for (size_t i = tid; i < a.n; i += nthr) {
+        T acc = static_cast<const T *>(a.ins[0])[i];
+        for (int k = 1; k < a.nins; ++k) acc = Op<T, OP>::ap(acc, static_cast<const T *>(a.ins[k])[i]);
+        out[i] = acc;
+    }
+    __syncthreads();
+    // exit: the last block to finish reading tells the peers (reduce-op.c:250)
+    if (threadIdx.x == 0) grid_arrive(a.gsync, false, [&] { peer_handshake(a.sig); });
+}
+
+template <typename T, int OP>
+hipError_t sf_launch(const SignalFoldArgs &a, hipStream_t s) {
+    hipLaunchKernelGGL((signal_fold_kernel<T, OP>), dim3(kFenceBlocks), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t sf_ops(int op, const SignalFoldArgs &a, hipStream_t s) {
+    constexpr bool integral = std::is_integral<T>::value;
+    constexpr bool cplx = std::is_same<T, cplxd>::value || std::is_same<T, cplxf>::value;
+    switch (op) {
+    case SHMEMX_OP_SUM: return sf_launch<T, SHMEMX_OP_SUM>(a, s);
+    case SHMEMX_OP_PROD: return sf_launch<T, SHMEMX_OP_PROD>(a, s);
+    case SHMEMX_OP_AND:
+        if constexpr (integral) return sf_launch<T, SHMEMX_OP_AND>(a, s);
+        break;
+    case SHMEMX_OP_OR:
+        if constexpr (integral) return sf_launch<T, SHMEMX_OP_OR>(a, s);
+        break;
+    case SHMEMX_OP_XOR:
+        if constexpr (integral) return sf_launch<T, SHMEMX_OP_XOR>(a, s);
+        break;
+    case SHMEMX_OP_MIN:
+        if constexpr (!cplx) return sf_launch<T, SHMEMX_OP_MIN>(a, s);
+        break;
+    case SHMEMX_OP_MAX:
+        if constexpr (!cplx) return sf_launch<T, SHMEMX_OP_MAX>(a, s);
+        break;
+    default: break;
+    }
+    return hipErrorInvalidValue;
+}
+
 }  // namespace
+
+hipError_t launch_signal_fold(int type, int op, const SignalFoldArgs &a, hipStream_t stream) {
+    if (!op_on_device(type, op) || a.nins < 1 || a.nins > kMaxFoldInputs || !a.out || !a.gsync ||
+        !a.sig.seen || !a.sig.fence_stats || a.sig.P < 1 || a.sig.P > kMaxFoldInputs || !a.sig.mine ||
+        !a.sig.err)
+        return hipErrorInvalidValue;
+    for (int k = 0; k < a.nins; ++k)
+        if (!a.ins[k]) return hipErrorInvalidValue;
+    for (int i = 0; i < a.sig.P; ++i)
+        if (a.sig.pe[i] != a.sig.me && !a.sig.peer[i]) return hipErrorInvalidValue;
+    switch (type) {
+    case SHMEMX_TYPE_SHORT: return sf_ops<short>(op, a, stream);
+    case SHMEMX_TYPE_INT: return sf_ops<int>(op, a, stream);
+    case SHMEMX_TYPE_LONG:
+    case SHMEMX_TYPE_LONGLONG: return sf_ops<long>(op, a, stream);
+    case SHMEMX_TYPE_FLOAT: return sf_ops<float>(op, a, stream);
+    case SHMEMX_TYPE_DOUBLE: return sf_ops<double>(op, a, stream);
+    case SHMEMX_TYPE_LONGDOUBLE: return sf_ops<ld80>(op, a, stream);
+    case SHMEMX_TYPE_COMPLEXD: return sf_ops<cplxd>(op, a, stream);
+    case SHMEMX_TYPE_COMPLEXF: return sf_ops<cplxf>(op, a, stream);
+    default: return hipErrorInvalidValue;
+    }
+}
 
 hipError_t launch_signal(const SignalArgs &a, hipStream_t stream) {
     if (a.P < 1 || a.P > kMaxFoldInputs || !a.mine || !a.err) return hipErrorInvalidValue;

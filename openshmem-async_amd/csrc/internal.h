@@ -73,6 +73,26 @@ struct SignalArgs {
 };
 hipError_t launch_signal(const SignalArgs &a, hipStream_t stream);
 
+// The one-shot reduction of a small array as ONE launch (SIGNAL's one shot,
+// and DIRECT's when every member can take it): kFenceBlocks blocks each run
+// the system fence and record their XCD; the last block to arrive checks
+// the XCD coverage and does the entry handshake with the peers (the signal
+// counters of SignalArgs); every block then folds its share of
+// out[i] = op(...op(ins[0][i], ins[1][i])..., ins[nins-1][i]); the last block
+// to finish does the exit handshake.  gsync: 2 words of device memory, zero
+// at the first launch and left zero (an arrival counter, a generation).
+// sig.seen must hold kFenceBlocks words.  Launches on one GPU must not
+// overlap (stream order, or one stream).
+struct SignalFoldArgs {
+    SignalArgs sig;
+    unsigned int *gsync;
+    void *out;
+    const void *ins[kMaxFoldInputs];
+    int nins;
+    size_t n;
+};
+hipError_t launch_signal_fold(int type, int op, const SignalFoldArgs &a, hipStream_t stream);
+
 // Position-aware 64-bit checksum of n elements of `type` at device address
 // ptr (16-byte aligned) into out[0] (device memory, with room for
 // kChecksumMaxBlocks more words of block partials after it), stream-ordered.

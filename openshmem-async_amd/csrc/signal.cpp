@@ -57,7 +57,9 @@ size_t oneshot_bytes() {
     return b;
 }
 
-unsigned long long timeout_ticks() {   // s_memrealtime runs at 100 MHz
+}  // namespace
+
+unsigned long long signal_timeout_ticks() {   // s_memrealtime runs at 100 MHz
     static const unsigned long long t = [] {
         const char *e = std::getenv("SHMEMX_SIGNAL_TIMEOUT");
         const double s = e ? std::atof(e) : 0.0;
@@ -66,8 +68,8 @@ unsigned long long timeout_ticks() {   // s_memrealtime runs at 100 MHz
     return t;
 }
 
-// Host-mapped error word the signal kernel sets on a timeout.
-unsigned int *error_word() {
+// Host-mapped error word the signal kernels set on a timeout.
+unsigned int *signal_error_word() {
     static unsigned int *w = [] {
         void *p = nullptr;
         SHMX_HIP(hipHostMalloc(&p, sizeof(unsigned int), hipHostMallocCoherent));
@@ -77,10 +79,8 @@ unsigned int *error_word() {
     return w;
 }
 
-}  // namespace
-
 unsigned int signal_error() {
-    volatile unsigned int *w = error_word();
+    volatile unsigned int *w = signal_error_word();
     const unsigned int e = *w;
     *w = 0;
     return e;
@@ -97,8 +97,7 @@ int signal_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     const bool partial = tgt != src && tgt < src + bytes && src < tgt + bytes;
     if (partial || !heap::offset_of(src, bytes, &soff) || !heap::offset_of(tgt, bytes, &toff))
         return set_error(SHMEMX_ENOTSUP);
-    unsigned long long *mine = heap::signal_area();
-    if (!mine) return set_error(SHMEMX_ENOTSUP);
+    if (!heap::signal_area()) return set_error(SHMEMX_ENOTSUP);
     // The peers' heap segments: mapped (and voted on) the first time this set
     // meets them, plain lookups afterwards.
     std::vector<std::pair<node::Region, int>> regs;
@@ -107,36 +106,29 @@ int signal_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
         trace(LOG_REDUCTION, "SIGNAL: a member could not map a peer heap (%s)", node::last_ipc_error());
         return set_error(SHMEMX_ENOTSUP);
     }
+    SignalArgs sa;
+    if (!signal_args(start, step, P, &sa)) return set_error(SHMEMX_ENOTSUP);
     std::vector<char *> hb(P);
-    SignalArgs sa{};
-    sa.mine = mine;
-    sa.P = P;
-    sa.me = g_state.pe;
-    sa.timeout_ticks = timeout_ticks();
-    sa.err = error_word();
-    const FenceRecords fr = fence_records();
-    sa.seen = fr.seen;
-    sa.nxcc = fr.nxcc;
-    sa.fence_stats = fr.stats;
-    const uint64_t sig = heap::signal_offset();
-    for (int i = 0; i < P; ++i) {
-        const int q = start + i * step;
-        hb[i] = node::peer_base(node::kHeap, q);
-        sa.pe[i] = q;
-        sa.peer[i] = reinterpret_cast<const unsigned long long *>(hb[i] + sig);
+    for (int i = 0; i < P; ++i) hb[i] = node::peer_base(node::kHeap, start + i * step);
+    const void *ins[kMaxFoldInputs];
+    if (tgt != src && bytes <= oneshot_bytes()) {
+        // barrier, fold of every whole source, barrier: one fused launch
+        SignalFoldArgs fa{};
+        fa.sig = sa;
+        fa.gsync = fence_records().gsync;
+        fa.out = tgt;
+        for (int i = 0; i < P; ++i) fa.ins[i] = hb[i] + soff;
+        fa.nins = P;
+        fa.n = n;
+        SHMX_HIP(launch_signal_fold(type, op, fa, s));   // reduce-op.c:217-250
+        count_fused_call();
+        return SHMEMX_OK;
     }
     auto barrier = [&] {
         SHMX_HIP(launch_sys_fence(s, sa.seen));
         SHMX_HIP(launch_signal(sa, s));
     };
-    const void *ins[kMaxFoldInputs];
     barrier();   // reduce-op.c:217
-    if (tgt != src && bytes <= oneshot_bytes()) {
-        for (int i = 0; i < P; ++i) ins[i] = hb[i] + soff;
-        SHMX_HIP(launch_fold(type, op, tgt, ins, P, n, s));
-        barrier();   // reduce-op.c:250
-        return SHMEMX_OK;
-    }
     const size_t g = sz >= 16 ? 1 : 16 / sz;
     size_t slice = (n + P - 1) / P;
     slice = (slice + g - 1) / g * g;

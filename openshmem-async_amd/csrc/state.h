@@ -115,12 +115,21 @@ char *ipc_scratch(size_t *bytes);
 // (logged under SHMEM_LOG_LEVELS=info; counted in shmemx_direct_stats).
 void fence_and_wait(hipStream_t s);
 // The device-side fence records and counters the SIGNAL barrier checks.
+struct SignalArgs;   // internal.h
 struct FenceRecords {
     unsigned int *seen;
     int nxcc;
     unsigned long long *stats;
+    unsigned int *gsync;   // the fused one-shot kernel's grid barrier (2 words)
 };
 FenceRecords fence_records();
+// SignalArgs for the members of a set over their mapped heap segments (the
+// signal counters at heap::signal_offset()); false if this PE has no heap
+// segment or a member's segment is not mapped.
+bool signal_args(int start, int step, int P, SignalArgs *sa);
+// A one-shot reduction as one fused launch (launch_signal_fold): count it in
+// shmemx_direct_stats.
+void count_fused_call();
 // Hand data between the members' GPUs: fence_and_wait, then the host barrier
 // over the set.
 // Optionally adds the time spent waiting for the stream (from since_us, a
@@ -144,6 +153,10 @@ int signal_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
 // After the stream has drained: 0, or 1 if a SIGNAL barrier timed out, 2 if
 // a fence before one missed an XCD.  (Clears it.)
 unsigned int signal_error();
+// The host-mapped error word the device barriers set, and their timeout in
+// s_memrealtime ticks ($SHMEMX_SIGNAL_TIMEOUT).
+unsigned int *signal_error_word();
+unsigned long long signal_timeout_ticks();
 // Every member's 8-byte value in set order: a collective over the active set
 // (collectives.cpp; RCCL all-gather / grouped p2p, or the node block's
 // descriptors on the IPC transport).  Validates the set like a call would.

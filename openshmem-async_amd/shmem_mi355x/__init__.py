@@ -350,14 +350,16 @@ DIRECT_PHASES = ("entry_wait_us", "entry_barrier_us", "fold_us", "fold_barrier_u
 
 
 FENCE_STATS = ("fences_host", "fence_refills_host", "fences_device", "fences_device_incomplete")
+DIRECT_COUNTS = ("fused_calls",)
 
 
 def direct_stats(reset: bool = True) -> dict:
     """shmemx_direct_stats: DIRECT calls since the last reset, the host-side
     microseconds summed over them per phase, and the system-fence coverage
     counters (fences checked on the host / refilled because a fence missed an
-    XCD; fences checked by the SIGNAL barrier / found incomplete)."""
-    names = DIRECT_PHASES + FENCE_STATS
+    XCD; fences checked by the SIGNAL barrier / found incomplete), and the
+    one-shot calls that ran as one fused launch."""
+    names = DIRECT_PHASES + FENCE_STATS + DIRECT_COUNTS
     buf = (ctypes.c_double * (1 + len(names)))()
     k = lib().shmemx_direct_stats(buf, len(buf), 1 if reset else 0)
     out = {"calls": buf[0]}

@@ -319,29 +319,31 @@ elif scenario == "signal":
             if e.code != 3:
                 fails.append(f"signal with a torch target: error {e.code}, want ENOTSUP")
     # graph capture: the barriers' counters live on the device, so replays
-    # stay in step across PEs; each replay reduces fresh inputs
-    n = 50000
+    # stay in step across PEs; each replay reduces fresh inputs.  50000
+    # doubles take the two-shot schedule, 20000 the fused one-shot launch
+    # (its grid barrier resets itself, so replays need no host step).
     stream = torch.cuda.Stream()
-    torch.cuda.synchronize()
-    shm.reduce_on_stream("double", "sum", HEAP_TGT, HEAP_SRC, n, 0, 0, npes, "signal",
-                         stream.cuda_stream)          # warm: maps and votes
-    torch.cuda.synchronize()
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph, stream=stream):
+    for n in (50000, 20000):
+        torch.cuda.synchronize()
         shm.reduce_on_stream("double", "sum", HEAP_TGT, HEAP_SRC, n, 0, 0, npes, "signal",
-                             stream.cuda_stream)
-    for rep_i in range(5):
-        seed += 1
-        srcs = oracle.sources("double", 1, npes, n, base_seed=seed)
-        shm.memcpy(HEAP_SRC, np.ascontiguousarray(srcs[pe]), n * 8)
+                             stream.cuda_stream)          # warm: maps and votes
         torch.cuda.synchronize()
-        graph.replay()
-        torch.cuda.synchronize()
-        ncases += 1
-        want = oracle.reduce_sim("double", "sum", srcs, 0, 0, npes)[0]
-        if not same_bits(read(HEAP_TGT, "double", n), want):
-            fails.append(f"graph replay {rep_i}: wrong result")
-    del graph
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=stream):
+            shm.reduce_on_stream("double", "sum", HEAP_TGT, HEAP_SRC, n, 0, 0, npes, "signal",
+                                 stream.cuda_stream)
+        for rep_i in range(5):
+            seed += 1
+            srcs = oracle.sources("double", 1, npes, n, base_seed=seed)
+            shm.memcpy(HEAP_SRC, np.ascontiguousarray(srcs[pe]), n * 8)
+            torch.cuda.synchronize()
+            graph.replay()
+            torch.cuda.synchronize()
+            ncases += 1
+            want = oracle.reduce_sim("double", "sum", srcs, 0, 0, npes)[0]
+            if not same_bits(read(HEAP_TGT, "double", n), want):
+                fails.append(f"graph replay {rep_i} n={n}: wrong result")
+        del graph
 elif scenario == "hostheap":
     # $SHMEMX_HEAP_MEMORY=host: shmem_malloc returns page-locked host memory,
     # as the reference's heap is; the host writes the symmetric objects and
@@ -718,6 +720,10 @@ stats = shm.direct_stats(reset=False)
 fences = {k: stats[k] for k in shm.FENCE_STATS}
 if fences["fence_refills_host"] or fences["fences_device_incomplete"]:
     fails.append(f"system fences missed an XCD: {fences}")
+# small heap calls ran as one fused launch (DIRECT's and SIGNAL's one shot)
+fences["fused_calls"] = stats["fused_calls"]
+if scenario in ("full", "signal") and npes > 1 and not stats["fused_calls"]:
+    fails.append("no one-shot call ran as a fused launch")
 shm.free(HEAP_TGT)
 shm.free(HEAP_SRC)
 shm.finalize()

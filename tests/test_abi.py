@@ -176,7 +176,7 @@ def test_direct_stats_without_calls(shm):
     needs a device."""
     st = shm.direct_stats(reset=True)
     assert st["calls"] == 0
-    assert set(st) == {"calls", *shm.DIRECT_PHASES, *shm.FENCE_STATS}
+    assert set(st) == {"calls", *shm.DIRECT_PHASES, *shm.FENCE_STATS, *shm.DIRECT_COUNTS}
     assert all(v == 0 for v in st.values())
 
 
