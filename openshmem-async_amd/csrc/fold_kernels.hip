@@ -619,47 +619,55 @@ __device__ void peer_handshake(const SignalArgs &a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope
 }
 
-// Grid arrival (thread 0 of each block).  Returns true in the last block to
-// arrive, which runs `last` and then releases the others (if `wait`).
-template <typename F>
-__device__ __forceinline__ void grid_arrive(unsigned int *gsync, bool wait, F last) {
-    const unsigned int gen0 = __hip_atomic_load(gsync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned int old =
-        __hip_atomic_fetch_add(gsync, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == gridDim.x - 1) {
-        last();
-        __hip_atomic_store(gsync, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(gsync + 1, gen0 + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else if (wait) {
-        while (__hip_atomic_load(gsync + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == gen0)
-            __builtin_amdgcn_s_sleep(1);
-    }
-}
-
 template <typename T, int OP>
 __global__ __launch_bounds__(kBlock) void signal_fold_kernel(SignalFoldArgs a) {
+    unsigned int *const count = a.gsync, *const gen = a.gsync + 1;
+    __shared__ int s_last;
     if (threadIdx.x == 0) {
-        // entry: this block's XCD writes back its L2 and drops stale peer
-        // lines, and says which XCD it was
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");   // system scope
+        // entry: record this block's XCD, then write back the XCD's L2 and
+        // drop stale peer lines (the fence also orders the record), arrive
         const unsigned int xcc = (unsigned int)__builtin_amdgcn_s_getreg(kXccIdReg) & 15u;
         __hip_atomic_store(a.sig.seen + blockIdx.x, kFenceSeen | xcc, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-        grid_arrive(a.gsync, true, [&] {
-            unsigned int mask = 0;
-            for (unsigned int b = 0; b < gridDim.x; ++b) {
-                const unsigned int r =
-                    __hip_atomic_load(a.sig.seen + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (r & kFenceSeen) mask |= 1u << (r & 15u);
-                __hip_atomic_store(a.sig.seen + b, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");   // system scope
+        const unsigned int gen0 = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned int old = __hip_atomic_fetch_add(count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == gridDim.x - 1;
+        if (!s_last) {
+            // relaxed polls (an acquire load would invalidate the L2 on every
+            // poll), one acquire once the generation moved
+            while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen0)
+                __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        } else {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+        if (s_last) s_last = 1 + (int)gen0;   // carry gen0 to the checking wave
+    }
+    __syncthreads();
+    if (s_last && threadIdx.x < 64) {
+        // the last block's first wave: every block's XCD record at once (lane
+        // b reads block b's), then lane 0 does the entry handshake
+        const int lane = threadIdx.x;
+        unsigned int rec = 0;
+        if (lane < (int)gridDim.x) {
+            rec = __hip_atomic_load(a.sig.seen + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.sig.seen + lane, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        int covered = 0;
+#pragma unroll
+        for (unsigned int x = 0; x < 16; ++x) covered += __ballot(rec == (kFenceSeen | x)) != 0 ? 1 : 0;
+        if (lane == 0) {
             atomicAdd(a.sig.fence_stats, 1ull);
-            if (__builtin_popcount(mask) < a.sig.nxcc) {
+            if (covered < a.sig.nxcc) {
                 atomicAdd(a.sig.fence_stats + 1, 1ull);
                 __hip_atomic_store(a.sig.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
             peer_handshake(a.sig);   // reduce-op.c:217
-        });
+            __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(gen, (unsigned int)(s_last - 1) + 1u, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     __syncthreads();
     const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x, nthr = (size_t)gridDim.x * kBlock;
@@ -671,7 +679,11 @@ __global__ __launch_bounds__(kBlock) void signal_fold_kernel(SignalFoldArgs a) {
     }
     __syncthreads();
     // exit: the last block to finish reading tells the peers (reduce-op.c:250)
-    if (threadIdx.x == 0) grid_arrive(a.gsync, false, [&] { peer_handshake(a.sig); });
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+        __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        peer_handshake(a.sig);
+    }
 }
 
 template <typename T, int OP>

@@ -30,7 +30,9 @@
 //   gather                  the other P-1 slices from the peers' targets
 //   barrier                 nobody reads my source or target any more
 // One shot (arrays up to $SHMEMX_DIRECT_ONESHOT_KB, target != source):
-//   barrier; fold all of every source -> my target; barrier.
+//   barrier; fold all of every source -> my target; barrier — as ONE fused
+//   launch (launch_signal_fold: the fence, both handshakes and the fold in
+//   one kernel, with a self-resetting grid barrier).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
