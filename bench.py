@@ -405,7 +405,7 @@ def crossover_extra(world, sp, stream, barrier, max_over_ranks):
     target in the symmetric heap (so DIRECT and SIGNAL can run too): GiB/s of
     the whole job (N * n * 8 B / max-over-ranks time).  The data `auto`'s
     per-size choice between RCCL and the IPC pulls is to be set from."""
-    sizes = [1 << 12, 1 << 16, 1 << 20, 1 << 24]
+    sizes = [1, 1 << 9, 1 << 12, 1 << 16, 1 << 20, 1 << 24]
     nbytes = sizes[-1] * 8
     hs, ht = malloc_pair(nbytes)
     out = {}
