@@ -408,12 +408,12 @@ def crossover_extra(world, sp, stream, barrier, max_over_ranks):
     sizes = [1, 1 << 9, 1 << 12, 1 << 16, 1 << 20, 1 << 24]
     nbytes = sizes[-1] * 8
     hs, ht = malloc_pair(nbytes)
-    out = {}
+    out = {"GiBps": {}, "us_per_call": {}}
     try:
         if not (hs and ht):
             return "shmem_malloc failed"
         for algo in ("rccl", "allreduce", "a2a", "direct", "signal"):
-            row = {}
+            row, row_us = {}, {}
             for n in sizes:
                 def step(n=n, algo=algo):
                     shm.reduce_on_stream("double", "sum", ht, hs, n, 0, 0, world, algo, sp)
@@ -423,10 +423,12 @@ def crossover_extra(world, sp, stream, barrier, max_over_ranks):
                     k = 20 if n <= 1 << 20 else 10
                     w, _ = time_region(step, k, stream, barrier)
                     w = max_over_ranks(w)
-                    row[str(n)] = round(world * n * 8 * k / w / GiB, 2)
+                    row[str(n)] = round(world * n * 8 * k / w / GiB, 4)
+                    row_us[str(n)] = round(w / k * 1e6, 1)
                 except shm.ShmemError as e:
-                    row[str(n)] = str(e)
-            out[algo] = row
+                    row[str(n)] = row_us[str(n)] = str(e)
+            out["GiBps"][algo] = row
+            out["us_per_call"][algo] = row_us
     finally:
         if ht:
             shm.free(ht)
@@ -737,7 +739,7 @@ def main():
         guarded("signal_heap", lambda: direct_extra(world, n, src, sp, stream, barrier,
                                                     max_over_ranks, max(3, a.steps // 4), "signal"))
         guarded("heap_latency", lambda: heap_latency_extras(world, barrier, max_over_ranks))
-        guarded("algo_crossover_GiBps", lambda: crossover_extra(world, sp, stream, barrier,
+        guarded("algo_crossover", lambda: crossover_extra(world, sp, stream, barrier,
                                                                 max_over_ranks))
 
     timer.cancel()
