@@ -316,9 +316,8 @@ namespace {
 // DIRECT's one shot as one fused launch (launch_signal_fold): every member's
 // source (heap or staged scratch, per the descriptors) and every member's
 // heap segment (the signal counters) mapped, then the launch and one wait.
-int direct_fused(int type, int op, char *tgt, const char *src, size_t n, int start, int step, int P,
+int direct_fused(int type, int op, char *tgt, size_t n, int start, int step, int P,
                  const std::vector<node::Desc> &desc, bool stage_tgt, hipStream_t s) {
-    (void)src;
     std::vector<std::pair<node::Region, int>> regs;
     for (int i = 0; i < P; ++i) {
         regs.emplace_back(static_cast<node::Region>(desc[i].src.region), start + i * step);
@@ -402,11 +401,11 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     // a chunk's copy-out overwrites source elements of the next chunk
     // bit 2: "I can take the fused one-shot launch" (I have the signal
     // counters, at the top of my heap segment)
-    d.count = (stage_src || stage_tgt ? 1 : 0) | (partial && tgt > src ? 2 : 0) |
-              (one_shot && heap::signal_area() ? 4 : 0);
-    node::put_desc(d);
     // One chunk (n <= cmax, known alike everywhere): stage it right away.
     const bool single = n <= cmax;
+    d.count = (stage_src || stage_tgt ? 1 : 0) | (partial && tgt > src ? 2 : 0) |
+              (one_shot && single && heap::signal_area() ? 4 : 0);
+    node::put_desc(d);
     if (single && stage_src)
         SHMX_HIP(hipMemcpyAsync(g_scratch.base, src, bytes, hipMemcpyDeviceToDevice, s));
     g_calls += 1;
@@ -426,7 +425,7 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
         read_descs();
         bool fuse = true;
         for (int i = 0; i < P; ++i) fuse &= (desc[i].count & 4) != 0;
-        if (fuse) return direct_fused(type, op, tgt, src, n, start, step, P, desc, stage_tgt, s);
+        if (fuse) return direct_fused(type, op, tgt, n, start, step, P, desc, stage_tgt, s);
         // my source (and its staging) is complete; reduce-op.c:217
         node_sync(start, step, P, s, &g_phase_us[kEntryWait], &g_phase_us[kEntryBarrier]);
     } else {
