@@ -137,6 +137,50 @@ __global__ __launch_bounds__(B) void rdonly(f64x2 *out, Ins in, int P) {
         if (acc[u].x == -1.0) st(out + v0 + u * B, acc[u]);
 }
 
+// round-2b variants for the P = 8, 16 Mi case (77 % of peak):
+//   pol<U,L,S>  rt's loop, load / store cache policy chosen (1 = nt)
+//   seq<U,R>    rt's loop, but each block walks R consecutive chunks, so it
+//               streams R*B*U*16 contiguous bytes per input (DRAM row reuse)
+template <int U, int L, int S>
+__global__ __launch_bounds__(B) void pol(f64x2 *out, Ins in, int P) {
+    const size_t v0 = (size_t)blockIdx.x * B * U + threadIdx.x;
+    auto l = [](const f64x2 *q) { if constexpr (L) return __builtin_nontemporal_load(q); else return *q; };
+    f64x2 acc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u] = l(in.p[0] + v0 + u * B);
+    for (int k = 1; k < P; ++k) {
+        f64x2 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = l(in.p[k] + v0 + u * B);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u] += x[u];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        if constexpr (S) __builtin_nontemporal_store(acc[u], out + v0 + u * B);
+        else out[v0 + u * B] = acc[u];
+    }
+}
+
+template <int U, int R>
+__global__ __launch_bounds__(B) void seq(f64x2 *out, Ins in, int P) {
+    for (int r = 0; r < R; ++r) {
+        const size_t v0 = ((size_t)blockIdx.x * R + r) * B * U + threadIdx.x;
+        f64x2 acc[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u] = ld(in.p[0] + v0 + u * B);
+        for (int k = 1; k < P; ++k) {
+            f64x2 x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) x[u] = ld(in.p[k] + v0 + u * B);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc[u] += x[u];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) st(out + v0 + u * B, acc[u]);
+    }
+}
+
 __global__ void flush(f64x2 *p, size_t n, double v) {
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
         p[i] = f64x2{v, v};
@@ -177,13 +221,24 @@ int main(int argc, char **argv) {
     const size_t sn = (size_t(1) << 30) / 16;
     CK(hipMalloc(&scratch, sn * 16));
     CK(hipDeviceSynchronize());
+    const bool round2b = getenv("FOLDN_2B") != nullptr;
     std::vector<Var> vars = {{"rt_u4", rt<4>, 4, 0}, {"rt_u2", rt<2>, 2, 0},
                              {"pipe_u4", pipe<4>, 4, 0}, {"pipe_u2", pipe<2>, 2, 0},
                              {"rdonly_u4", rdonly<4>, 4, 0}};
-    add_static<3>(vars);
-    add_static<4>(vars);
-    add_static<6>(vars);
-    add_static<8>(vars);
+    if (round2b) {
+        // U is the block's footprint divisor below (grid = nvec / (B*U)); seq
+        // counts its R chunks in it
+        vars = {{"rt_u4", rt<4>, 4, 0},          {"rt_u8", rt<8>, 8, 0},
+                {"pol_u4_L0S1", pol<4, 0, 1>, 4, 0}, {"pol_u4_L1S0", pol<4, 1, 0>, 4, 0},
+                {"pol_u4_L0S0", pol<4, 0, 0>, 4, 0}, {"seq_u4_r2", seq<4, 2>, 8, 0},
+                {"seq_u4_r4", seq<4, 4>, 16, 0},     {"seq_u4_r16", seq<4, 16>, 64, 0},
+                {"rdonly_u4", rdonly<4>, 4, 0}};
+    } else {
+        add_static<3>(vars);
+        add_static<4>(vars);
+        add_static<6>(vars);
+        add_static<8>(vars);
+    }
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -191,6 +246,7 @@ int main(int argc, char **argv) {
     printf("# n=%zu per input, %s; GB/s = (P+1)*n*8 / launch time (median of rounds)\n", n,
            cold ? "cold (1 GiB scratch rewritten before each launch)" : "warm (back to back)");
     for (int P : {3, 4, 6, 8}) {
+        if (round2b && P != 4 && P != 8) continue;
         Ins in{};
         for (int k = 0; k < P; ++k) in.p[k] = bufs[k];
         std::vector<std::vector<float>> t(vars.size());
