@@ -214,12 +214,16 @@ enum {
  *           barriers around and between (the reference's two plus one).
  *           Any set of <= 16 PEs, any op, PE_start bits on every PE.
  *           Operands outside the symmetric heap are staged through an IPC
- *           scratch region.  Host-synchronous.
+ *           scratch region.  Host-synchronous.  Arrays up to 256 KiB
+ *           ($SHMEMX_DIRECT_ONESHOT_KB) take one shot: every PE folds the
+ *           whole array, as one fused launch (fence, device barriers and
+ *           fold in one kernel) when every member has a heap segment.
  *   SIGNAL  DIRECT's pulls with device-side barriers (per-peer counters in
  *           each PE's heap segment, polled over xGMI): no host wait,
  *           stream-ordered, capturable.  Source and target must both be in
  *           the symmetric heap on every member (ENOTSUP otherwise); calls on
- *           one PE must not overlap in time.  A peer that never arrives
+ *           one PE must not overlap in time.  The one shot is one fused
+ *           launch.  A peer that never arrives
  *           times out after $SHMEMX_SIGNAL_TIMEOUT s (default 20); the next
  *           blocking call then aborts with a FATAL line.
  * With $SHMEMX_TRANSPORT=ipc there is no RCCL communicator: AUTO means

@@ -636,8 +636,15 @@ __global__ __launch_bounds__(kBlock) void signal_fold_kernel(SignalFoldArgs a) {
         if (!s_last) {
             // relaxed polls (an acquire load would invalidate the L2 on every
             // poll), one acquire once the generation moved
-            while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen0)
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen0) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > a.sig.timeout_ticks) {
+                    // only if launches overlapped on this GPU (they must not)
+                    __hip_atomic_store(a.sig.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(2);
+            }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         } else {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
