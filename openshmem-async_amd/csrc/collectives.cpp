@@ -310,8 +310,10 @@ int exchange_u64(int start, int logstride, int size, unsigned long long mine,
     SetInfo si;
     if (int rc = set_info(start, logstride, size, si)) return rc;
     all.assign(si.P, mine);
-    if (collective(si) && !g_state.comm) {
-        // IPC transport: the values travel in the node block's descriptors
+    if (collective(si) && (!g_state.comm || node::up())) {
+        // the values travel in the node block's descriptors (host only: two
+        // host barriers, where an RCCL all-gather costs a stream round trip);
+        // RCCL only when the PEs share no node block
         node::Desc d;
         d.aux = mine;
         node::put_desc(d);
