@@ -593,7 +593,13 @@ static int reduce_exchange(int type, int op, char *tgt, const char *src, int nre
             for (int i = 0; i < P; ++i) ins[i] = (i == m) ? src + m * cb : ws + i * cb;
             fold_chain(type, op, tgt + m * cb, ins.data(), P, (size_t)my_cnt, s);
         }
-        // 3. shard all-gather
+        // 3. shard all-gather: RCCL's own all-gather (in place) when the set
+        // is the whole job and every shard is full, grouped p2p otherwise
+        const bool world = start == 0 && step == 1 && P == g_state.npes;
+        if (world && n == (long long)P * p.chunk) {
+            SHMX_NCCL(ncclAllGather(tgt + m * cb, tgt, cb, ncclUint8, g_state.comm, s));
+            return SHMEMX_OK;
+        }
         SHMX_NCCL(ncclGroupStart());
         for (int i = 0; i < P; ++i) {
             if (i == m) continue;

@@ -393,6 +393,12 @@ elif scenario == "rccl":
         run_case("double", "sum", n, (0, 0, npes), "auto", "device", seed)   # all-reduce, then RS+AG+tail
     seed += 1
     run_case("long", "sum", (6 << 20) + 5, (0, 0, npes), "rccl", "device", seed)
+    # A2A with every shard full on the whole job: its all-gather is RCCL's
+    # own (in place), not grouped p2p
+    for t, op in (("long", "xor"), ("float", "min"), ("short", "and"), ("double", "sum")):
+        for mode in ("device", "inplace"):
+            seed += 1
+            run_case(t, op, 24576, (0, 0, npes), "a2a", mode, seed)
     for st in active_sets():
         size = st[2]
         for mode in ("heap", "device", "host"):
