@@ -611,15 +611,20 @@ static int reduce_exchange(int type, int op, char *tgt, const char *src, int nre
         return SHMEMX_OK;
     }
 
-    // GATHER: every source to every member, then the reference's own order on
+    // GATHER: every source to every member (RCCL's all-gather on the whole
+    // job, grouped p2p on a partial set), then the reference's own order on
     // each PE: r = src_me; r = op(r, src_p) for p ascending, p != me.
-    SHMX_NCCL(ncclGroupStart());
-    for (int i = 0; i < P; ++i) {
-        if (i == m) continue;
-        SHMX_NCCL(ncclSend(src, bytes, ncclUint8, peer(i), g_state.comm, s));
-        SHMX_NCCL(ncclRecv(ws + (size_t)i * bytes, bytes, ncclUint8, peer(i), g_state.comm, s));
+    if (start == 0 && step == 1 && P == g_state.npes) {
+        SHMX_NCCL(ncclAllGather(src, ws, bytes, ncclUint8, g_state.comm, s));
+    } else {
+        SHMX_NCCL(ncclGroupStart());
+        for (int i = 0; i < P; ++i) {
+            if (i == m) continue;
+            SHMX_NCCL(ncclSend(src, bytes, ncclUint8, peer(i), g_state.comm, s));
+            SHMX_NCCL(ncclRecv(ws + (size_t)i * bytes, bytes, ncclUint8, peer(i), g_state.comm, s));
+        }
+        SHMX_NCCL(ncclGroupEnd());
     }
-    SHMX_NCCL(ncclGroupEnd());
     {
         std::vector<const void *> ins;
         ins.reserve(P);
