@@ -644,6 +644,20 @@ elif scenario == "mirrored":
         if not same_bits(np.frombuffer(f.read(), dtype=np.float64), want[:nb // 8]):
             fails.append("mirrored: write(2) after shmemx_mirror_acquire wrote wrong bytes")
     ncases += 1
+    # and read(2) straight into a source: acquired for writing first, then
+    # the reduction sees the bytes the system call stored
+    m = 50000
+    srcs = oracle.sources("long", 1, npes, m, base_seed=0x717)
+    with tempfile.TemporaryFile() as f:
+        f.write(np.ascontiguousarray(srcs[pe]).tobytes())
+        f.seek(0)
+        shm.mirror_acquire(HEAP_SRC, m * 8, for_write=True)
+        got_n = os.readv(f.fileno(), [(ctypes.c_char * (m * 8)).from_address(HEAP_SRC)])
+    shm.to_all("long", "xor", HEAP_TGT, HEAP_SRC, m, 0, 0, npes)
+    ncases += 1
+    if got_n != m * 8 or not same_bits(host_view(HEAP_TGT, np.int64, m).copy(),
+                                       oracle.reduce_sim("long", "xor", srcs, 0, 0, npes)[0]):
+        fails.append(f"mirrored: read(2) into an acquired source ({got_n} bytes) then xor: wrong result")
     # SIGNAL (device barriers) on the view addresses: the twins are symmetric
     seed += 1
     srcs = oracle.sources("float", 1, npes, 70001, base_seed=seed)
