@@ -59,6 +59,29 @@ for n in [int(a) for a in sys.argv[1:]] or [4 << 20, 32 << 20]:
     got = tgt.copy()
     row["host_read2_ms"] = ms(t0)
     assert np.array_equal(got, vals)
+    # steady state, as a reference program iterates: the host rewrites the
+    # source, calls, reads the target back; per-phase medians of 5 rounds
+    phases = {"host_write": [], "call": [], "host_read": []}
+    for k in range(5):
+        vals2 = vals + k
+        t0 = time.perf_counter()
+        src[:] = vals2
+        phases["host_write"].append(ms(t0))
+        t0 = time.perf_counter()
+        shm.to_all("double", "sum", t_p, s_p, n, 0, 0, 1)
+        phases["call"].append(ms(t0))
+        t0 = time.perf_counter()
+        got = tgt.copy()
+        phases["host_read"].append(ms(t0))
+        assert np.array_equal(got, vals2)
+    row["steady_ms"] = {k: sorted(v)[2] for k, v in phases.items()}
+    row["steady_call_GiBps"] = round(n * 8 / (row["steady_ms"]["call"] * 1e-3) / 2**30, 1)
+    # the same round trip on plain numpy arrays (the host-array path)
+    h_s, h_t = vals.copy(), np.empty_like(vals)
+    shm.to_all("double", "sum", h_t, h_s, n, 0, 0, 1)
+    t0 = time.perf_counter()
+    shm.to_all("double", "sum", h_t, h_s, n, 0, 0, 1)
+    row["numpy_arrays_call_ms"] = ms(t0)
     # the same call on plain device arrays, for the floor
     d_s = torch.from_numpy(vals).cuda()
     d_t = torch.empty_like(d_s)
