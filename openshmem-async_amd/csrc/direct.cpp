@@ -25,7 +25,11 @@
 //
 // Synchronisation is the reference's: a barrier before the peers' sources
 // are read (reduce-op.c:217) and one after the targets are final (:250),
-// plus one between the two phases; host barriers over the node block.
+// plus one between the two phases; host barriers over the node block.  The
+// one shot (small arrays, every member folds the whole array) runs as ONE
+// fused launch when every member can take it (launch_signal_fold: the
+// fence, both barriers as device handshakes and the fold in one kernel),
+// after a fence-free host barrier that exchanges the descriptors.
 // Operands outside the symmetric heap (or a source that partially overlaps
 // its target) are staged through a per-PE scratch region, also IPC-mapped,
 // in chunks of half its size ($SHMEMX_DIRECT_SCRATCH_MB, default 512; every
