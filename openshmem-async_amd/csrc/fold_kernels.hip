@@ -622,6 +622,9 @@ __device__ void peer_handshake(const SignalArgs &a) {
 template <typename T, int OP>
 __global__ __launch_bounds__(kBlock) void signal_fold_kernel(SignalFoldArgs a) {
     unsigned int *const count = a.gsync, *const gen = a.gsync + 1;
+    // up to 4 elements per lane of one block: the last block to arrive folds
+    // alone, and no block waits for a release or arrives at the exit
+    const bool tiny = a.n <= (size_t)4 * kBlock;
     __shared__ int s_last;
     if (threadIdx.x == 0) {
         // entry: record this block's XCD, then write back the XCD's L2 and
@@ -633,7 +636,7 @@ __global__ __launch_bounds__(kBlock) void signal_fold_kernel(SignalFoldArgs a) {
         const unsigned int gen0 = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned int old = __hip_atomic_fetch_add(count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_last = old == gridDim.x - 1;
-        if (!s_last) {
+        if (!s_last && !tiny) {
             // relaxed polls (an acquire load would invalidate the L2 on every
             // poll), one acquire once the generation moved
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -646,12 +649,15 @@ __global__ __launch_bounds__(kBlock) void signal_fold_kernel(SignalFoldArgs a) {
                 __builtin_amdgcn_s_sleep(2);
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        } else {
+        } else if (s_last) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
         if (s_last) s_last = 1 + (int)gen0;   // carry gen0 to the checking wave
     }
     __syncthreads();
+    // a tiny array is folded by the last block alone: the others have fenced
+    // and arrived, and leave
+    if (tiny && !s_last) return;
     if (s_last && threadIdx.x < 64) {
         // the last block's first wave: every block's XCD record at once (lane
         // b reads block b's), then lane 0 does the entry handshake
@@ -677,8 +683,18 @@ __global__ __launch_bounds__(kBlock) void signal_fold_kernel(SignalFoldArgs a) {
         }
     }
     __syncthreads();
-    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x, nthr = (size_t)gridDim.x * kBlock;
     T *out = static_cast<T *>(a.out);
+    if (tiny) {
+        for (size_t i = threadIdx.x; i < a.n; i += kBlock) {
+            T acc = static_cast<const T *>(a.ins[0])[i];
+            for (int k = 1; k < a.nins; ++k) acc = Op<T, OP>::ap(acc, static_cast<const T *>(a.ins[k])[i]);
+            out[i] = acc;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) peer_handshake(a.sig);   // reduce-op.c:250
+        return;
+    }
+    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x, nthr = (size_t)gridDim.x * kBlock;
     for (size_t i = tid; i < a.n; i += nthr) {
         T acc = static_cast<const T *>(a.ins[0])[i];
         for (int k = 1; k < a.nins; ++k) acc = Op<T, OP>::ap(acc, static_cast<const T *>(a.ins[k])[i]);
