@@ -191,3 +191,17 @@ def test_typed_stream_forms_for_all_44(shm):
                          capture_output=True, text=True).stdout
     decls = re.findall(r"(\w+)\s+shmemx_\w+_to_all_on_stream\s*\(", pre)
     assert len(decls) == 44 and set(decls) == {"int"}
+
+
+def test_fortran_constants_match_the_c_header():
+    """include/shmem_reduce_mi355x.fh holds the reference's Fortran values
+    (src/shmem.fh:63-82): default INTEGER words, twice the C header's long
+    counts on LP64; SHMEM_SYNC_VALUE is the same -1."""
+    inc = os.path.join(REPO, "include")
+    c = dict(re.findall(r"#define\s+(SHMEM_\w+)\s+\(?(-?\d+)L\)?", open(os.path.join(inc, "shmem_reduce_mi355x.h")).read()))
+    f = dict(re.findall(r"parameter\s*\(\s*(SHMEM_\w+)\s*=\s*(-?\d+)\s*\)", open(os.path.join(inc, "shmem_reduce_mi355x.fh")).read()))
+    assert set(f) == {"SHMEM_REDUCE_SYNC_SIZE", "SHMEM_REDUCE_MIN_WRKDATA_SIZE", "SHMEM_BCAST_SYNC_SIZE",
+                      "SHMEM_BARRIER_SYNC_SIZE", "SHMEM_COLLECT_SYNC_SIZE", "SHMEM_SYNC_VALUE"}
+    for name, v in f.items():
+        want = int(c[name]) if name == "SHMEM_SYNC_VALUE" else 2 * int(c[name])
+        assert int(v) == want, (name, v, c[name])
