@@ -626,6 +626,7 @@ __global__ __launch_bounds__(kBlock) void signal_fold_kernel(SignalFoldArgs a) {
     // alone, and no block waits for a release or arrives at the exit
     const bool tiny = a.n <= (size_t)4 * kBlock;
     __shared__ int s_last;
+    __shared__ unsigned int s_gen0;
     if (threadIdx.x == 0) {
         // entry: record this block's XCD, then write back the XCD's L2 and
         // drop stale peer lines (the fence also orders the record), arrive
@@ -652,7 +653,7 @@ __global__ __launch_bounds__(kBlock) void signal_fold_kernel(SignalFoldArgs a) {
         } else if (s_last) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         }
-        if (s_last) s_last = 1 + (int)gen0;   // carry gen0 to the checking wave
+        s_gen0 = gen0;   // for the checking wave
     }
     __syncthreads();
     // a tiny array is folded by the last block alone: the others have fenced
@@ -678,8 +679,7 @@ __global__ __launch_bounds__(kBlock) void signal_fold_kernel(SignalFoldArgs a) {
             }
             peer_handshake(a.sig);   // reduce-op.c:217
             __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(gen, (unsigned int)(s_last - 1) + 1u, __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(gen, s_gen0 + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     __syncthreads();
