@@ -136,7 +136,98 @@ SHMX_HD ld80 round_pack(bool neg, int E, u128 m, bool sticky) {
     return make(neg, 0, sig);  // denormal or zero
 }
 
+// Fast path of add for the common case: both operands normal (exponent
+// 1..0x7FFE, integer bit set) and a normal result.  64-bit words instead of
+// the general path's 128-bit shifts: the significand of |b| aligned to |a|'s
+// is split into the word beside a's (bh) and the word of bits shifted out
+// below it (bl), plus one sticky bit (d == 65).  Returns false, without
+// touching r, whenever the general path is needed (specials, denormals,
+// over/underflow).
+SHMX_HD bool add_fast(const ld80 &a, const ld80 &b, ld80 &r) {
+    unsigned ea = exp_of(a), eb = exp_of(b);
+    if (ea - 1u >= 0x7FFEu || eb - 1u >= 0x7FFEu || !(a.sig & b.sig & kInt)) return false;
+    bool sa = sign_of(a), sb = sign_of(b);
+    uint64_t ma = a.sig, mb = b.sig;
+    if (ea < eb || (ea == eb && ma < mb)) {  // |a| >= |b| from here on
+        const unsigned te = ea; ea = eb; eb = te;
+        const uint64_t tm = ma; ma = mb; mb = tm;
+        const bool ts = sa; sa = sb; sb = ts;
+    }
+    const unsigned d = ea - eb;
+    if (d >= 66) {  // |b| < a quarter ulp of |a|: a itself, either sign
+        r = make(sa, ea, ma);
+        return true;
+    }
+    uint64_t bh, bl;
+    bool st = false;
+    if (d == 0) {
+        bh = mb;
+        bl = 0;
+    } else if (d < 64) {
+        bh = mb >> d;
+        bl = mb << (64 - d);
+    } else {
+        bh = 0;
+        bl = d == 64 ? mb : mb >> 1;
+        st = d == 65 && (mb & 1);
+    }
+    uint64_t sig, rest;
+    unsigned e = ea;
+    if (sa == sb) {
+        const uint64_t sum = ma + bh;
+        if (sum < ma) {  // carry: one more bit above
+            sig = (sum >> 1) | kInt;
+            rest = (sum << 63) | (bl >> 1);
+            st = st || (bl & 1);
+            ++e;
+        } else {
+            sig = sum;
+            rest = bl;
+        }
+    } else {
+        // (ma:0) - (bh:bl) - sticky: the value lies in (r, r + 1) when sticky
+        uint64_t lo = 0 - bl;
+        uint64_t hi = ma - bh - (bl != 0 ? 1 : 0);
+        if (st) {
+            hi -= lo == 0 ? 1 : 0;
+            lo -= 1;
+        }
+        if (hi == 0 && lo == 0 && !st) {  // exact cancellation: +0
+            r = make(false, 0, 0);
+            return true;
+        }
+        if (hi == 0) {  // only when d <= 1: exact, nothing below lo
+            const int l = clz64(lo);
+            if ((int)e - 64 - l < 1) return false;
+            r = make(sa, e - 64 - (unsigned)l, lo << l);
+            return true;
+        }
+        const int l = clz64(hi);
+        if (l) {
+            sig = (hi << l) | (lo >> (64 - l));
+            rest = lo << l;
+            if ((int)e - l < 1) return false;
+            e -= (unsigned)l;
+        } else {
+            sig = hi;
+            rest = lo;
+        }
+    }
+    // round to nearest even on the guard bit (rest's top), sticky below it
+    if ((rest >> 63) && (st || (rest << 1) != 0 || (sig & 1))) {
+        if (++sig == 0) {
+            sig = kInt;
+            ++e;
+        }
+    }
+    if (e > 0x7FFEu) return false;  // overflow: the general path returns inf
+    r = make(sa, e, sig);
+    return true;
+}
+
 SHMX_HD ld80 add(const ld80 &a, const ld80 &b) {
+    ld80 fast;
+    if (add_fast(a, b, fast)) return fast;
     if (unsupported(a) || unsupported(b)) return indefinite();
     if (is_nan(a) || is_nan(b)) return nan_result(a, b);
     const bool sa = sign_of(a), sb = sign_of(b);
@@ -185,7 +276,33 @@ SHMX_HD ld80 add(const ld80 &a, const ld80 &b) {
     return round_pack(neg, Ea + (L - 126), r << (127 - L), sticky);
 }
 
+// Fast path of mul: both operands normal and a normal result (64x64 ->
+// 128-bit product, one normalising shift, one rounding).
+SHMX_HD bool mul_fast(const ld80 &a, const ld80 &b, ld80 &r) {
+    const unsigned ea = exp_of(a), eb = exp_of(b);
+    if (ea - 1u >= 0x7FFEu || eb - 1u >= 0x7FFEu || !(a.sig & b.sig & kInt)) return false;
+    const u128 p = ((u128)a.sig) * b.sig;  // leading bit at 126 or 127
+    uint64_t hi = (uint64_t)(p >> 64), lo = (uint64_t)p;
+    int e = (int)ea + (int)eb - kBias + 1;
+    if (!(hi >> 63)) {
+        hi = (hi << 1) | (lo >> 63);
+        lo <<= 1;
+        --e;
+    }
+    if ((lo >> 63) && ((lo << 1) != 0 || (hi & 1))) {
+        if (++hi == 0) {
+            hi = kInt;
+            ++e;
+        }
+    }
+    if (e < 1 || e > 0x7FFE) return false;
+    r = make(sign_of(a) != sign_of(b), (unsigned)e, hi);
+    return true;
+}
+
 SHMX_HD ld80 mul(const ld80 &a, const ld80 &b) {
+    ld80 fast;
+    if (mul_fast(a, b, fast)) return fast;
     if (unsupported(a) || unsupported(b)) return indefinite();
     if (is_nan(a) || is_nan(b)) return nan_result(a, b);
     const bool neg = sign_of(a) != sign_of(b);

@@ -68,6 +68,15 @@ int main(int argc, char **argv) {
         const int ca = (int)(rng() % 8), cb = (i & 3) == 0 ? ca : (int)(rng() % 8);
         ld80 a = random_value(ca), b = random_value(cb);
         if (ca == 1 && cb == 1 && (i & 1)) b.se = (uint16_t)(a.se ^ 0x8000);  // near-cancel
+        if (i % 7 == 3) {
+            // both normal, exponents 0..70 apart: every alignment the fast
+            // add takes (64-bit words, the d = 64/65 sticky cases, d >= 66)
+            a = random_value(0);
+            const int ea = a.se & 0x7FFF, d = (int)(rng() % 71);
+            const int eb = ea - d >= 1 ? ea - d : ea + d;
+            b = enc(rng() & 1, (unsigned)(eb > 0x7FFE ? 0x7FFE : eb), rng() | (1ull << 63));
+            if (rng() & 1) b.sig = a.sig ^ (rng() & 7);   // nearly equal significands
+        }
         volatile long double x = to_ld(a), y = to_ld(b);
         const long double s = x + y, p = x * y;
         const bool lt = x < y, gt = x > y;

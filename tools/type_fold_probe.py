@@ -68,6 +68,43 @@ def main():
         gbs = 3 * BYTES / t_med / 1e9
         rows.append((t, op, t_med * 1e6, gbs))
         print(f"{t:>10} {op:>4}  {t_med * 1e6:8.1f} us  {gbs:7.1f} GB/s  {gbs / 8000:5.1%} of 8 TB/s", flush=True)
+    # the P-input fold (A2A / DIRECT / GATHER's fold step) at P = 8, 64 MiB
+    # per input, for the types whose op is the most arithmetic per byte
+    P, IB = 8, 64 << 20
+    ins = [torch.empty(IB, dtype=torch.uint8, device="cuda") for _ in range(P)]
+    out = torch.empty(IB, dtype=torch.uint8, device="cuda")
+    for (t, op) in (("double", "sum"), ("longdouble", "sum"), ("longdouble", "prod"),
+                    ("longdouble", "max"), ("complexd", "prod"), ("complexf", "prod"), ("short", "sum")):
+        sz = SIZES[t]
+        n = IB // sz
+        for x in ins:
+            if t == "longdouble":
+                v = torch.zeros(n, 2, dtype=torch.int64, device="cuda")
+                v[:, 0] = -0x8000000000000000
+                v[:, 1] = 0x3FFF
+                x.view(torch.int64).copy_(v.view(-1))
+            elif t in ("double", "complexd"):
+                x.view(torch.float64).uniform_(1.0, 1.0001, generator=g)
+            elif t == "complexf":
+                x.view(torch.float32).uniform_(1.0, 1.0001, generator=g)
+            else:
+                x.random_(0, 256, generator=g)
+        torch.cuda.synchronize()
+        for _ in range(3):
+            shm.fold_n(t, op, out, ins, n, sp)
+        times = []
+        for _ in range(10):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            shm.fold_n(t, op, out, ins, n, sp)
+            e1.record(stream)
+            e1.synchronize()
+            times.append(e0.elapsed_time(e1) * 1e-3)
+        times.sort()
+        t_med = times[len(times) // 2]
+        gbs = (P + 1) * IB / t_med / 1e9
+        print(f"P={P} {t:>10} {op:>4}  {t_med * 1e6:8.1f} us  {gbs:7.1f} GB/s  {gbs / 8000:5.1%} of 8 TB/s",
+              flush=True)
     shm.finalize()
 
 
