@@ -250,6 +250,28 @@ __global__ __launch_bounds__(kBlock) void fold_kernel(FoldArgs args) {
 #pragma unroll
                     for (int u = 0; u < UNROLL; ++u)
                         acc[u] = apply16<T, OP>(acc[u], x[k - 1][u]);
+            } else if (std::is_same<T, ld80>::value && nins >= 3) {
+                // soft-float ops are long: input k + 1's loads are issued
+                // before input k is folded, so the arithmetic overlaps them
+                // (P = 8 long double sum 115 -> 107 us)
+                auto in_k = [&](int k) {
+                    return reinterpret_cast<const u32x4 *>(static_cast<const T *>(args.ins[k]) + args.head);
+                };
+                u32x4 cur[UNROLL];
+#pragma unroll
+                for (int u = 0; u < UNROLL; ++u) cur[u] = ld16<NT>(in_k(1) + v0 + u * kBlock);
+                for (int k = 2; k < nins; ++k) {
+                    u32x4 nxt[UNROLL];
+#pragma unroll
+                    for (int u = 0; u < UNROLL; ++u) nxt[u] = ld16<NT>(in_k(k) + v0 + u * kBlock);
+#pragma unroll
+                    for (int u = 0; u < UNROLL; ++u) {
+                        acc[u] = apply16<T, OP>(acc[u], cur[u]);
+                        cur[u] = nxt[u];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < UNROLL; ++u) acc[u] = apply16<T, OP>(acc[u], cur[u]);
             } else {
                 for (int k = 1; k < nins; ++k) {
                     const u32x4 *ink = reinterpret_cast<const u32x4 *>(
