@@ -181,6 +181,45 @@ __global__ __launch_bounds__(B) void seq(f64x2 *out, Ins in, int P) {
     }
 }
 
+// round-2c variants for the same case: block size, and a persistent
+// grid-stride grid of G blocks (G from the grid the host passes)
+template <int U, int BS>
+__global__ __launch_bounds__(BS) void rtb(f64x2 *out, Ins in, int P) {
+    const size_t v0 = (size_t)blockIdx.x * BS * U + threadIdx.x;
+    f64x2 acc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u] = ld(in.p[0] + v0 + u * BS);
+    for (int k = 1; k < P; ++k) {
+        f64x2 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = ld(in.p[k] + v0 + u * BS);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u] += x[u];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) st(out + v0 + u * BS, acc[u]);
+}
+
+__device__ size_t g_nchunks;   // set by the host before the rtg launches
+template <int U>
+__global__ __launch_bounds__(B) void rtg(f64x2 *out, Ins in, int P) {
+    for (size_t c = blockIdx.x; c < g_nchunks; c += gridDim.x) {
+        const size_t v0 = c * B * U + threadIdx.x;
+        f64x2 acc[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u] = ld(in.p[0] + v0 + u * B);
+        for (int k = 1; k < P; ++k) {
+            f64x2 x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) x[u] = ld(in.p[k] + v0 + u * B);
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc[u] += x[u];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) st(out + v0 + u * B, acc[u]);
+    }
+}
+
 __global__ void flush(f64x2 *p, size_t n, double v) {
     for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
         p[i] = f64x2{v, v};
@@ -191,7 +230,9 @@ struct Var {
     const char *name;
     Kern k;
     int U;
-    int P;   // 0 = any
+    int P;        // 0 = any
+    int bs = 256;  // block size
+    int grid = 0;  // 0: one chunk per block; else a persistent grid of this many
 };
 
 template <int P>
@@ -222,10 +263,17 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&scratch, sn * 16));
     CK(hipDeviceSynchronize());
     const bool round2b = getenv("FOLDN_2B") != nullptr;
+    const bool round2c = getenv("FOLDN_2C") != nullptr;
     std::vector<Var> vars = {{"rt_u4", rt<4>, 4, 0}, {"rt_u2", rt<2>, 2, 0},
                              {"pipe_u4", pipe<4>, 4, 0}, {"pipe_u2", pipe<2>, 2, 0},
                              {"rdonly_u4", rdonly<4>, 4, 0}};
-    if (round2b) {
+    if (round2c) {
+        vars = {{"rt_u4", rt<4>, 4, 0},
+                {"b256_u2", rtb<2, 256>, 2, 0, 256},   {"b512_u1", rtb<1, 512>, 1, 0, 512},
+                {"b512_u2", rtb<2, 512>, 2, 0, 512},   {"b512_u4", rtb<4, 512>, 4, 0, 512},
+                {"b1024_u1", rtb<1, 1024>, 1, 0, 1024}, {"b1024_u2", rtb<2, 1024>, 2, 0, 1024},
+                {"g512_u4", rtg<4>, 4, 0, 256, 512},   {"rdonly_u4", rdonly<4>, 4, 0}};
+    } else if (round2b) {
         // U is the block's footprint divisor below (grid = nvec / (B*U)); seq
         // counts its R chunks in it
         vars = {{"rt_u4", rt<4>, 4, 0},          {"rt_u8", rt<8>, 8, 0},
@@ -245,8 +293,9 @@ int main(int argc, char **argv) {
     printf("# skew %ld (%s)\n", skew, skew < 0 ? "separate allocations" : "one block, inputs k*(n*8+skew) apart");
     printf("# n=%zu per input, %s; GB/s = (P+1)*n*8 / launch time (median of rounds)\n", n,
            cold ? "cold (1 GiB scratch rewritten before each launch)" : "warm (back to back)");
-    for (int P : {3, 4, 6, 8}) {
-        if (round2b && P != 4 && P != 8) continue;
+    for (int P : {2, 3, 4, 6, 8}) {
+        if (P == 2 && !round2c) continue;
+        if ((round2b || round2c) && P != 2 && P != 4 && P != 8) continue;
         Ins in{};
         for (int k = 0; k < P; ++k) in.p[k] = bufs[k];
         std::vector<std::vector<float>> t(vars.size());
@@ -254,13 +303,15 @@ int main(int argc, char **argv) {
             for (size_t vi = 0; vi < vars.size(); ++vi) {
                 const Var &v = vars[vi];
                 if (v.P && v.P != P) continue;
-                const dim3 grid((unsigned)(nvec / ((size_t)B * v.U)));
+                const size_t nch = nvec / ((size_t)v.bs * v.U);
+                CK(hipMemcpyToSymbol(HIP_SYMBOL(g_nchunks), &nch, sizeof nch));
+                const dim3 grid((unsigned)(v.grid ? v.grid : nch));
                 float total = 0;
                 const int reps = cold ? 5 : 10;
                 for (int r = 0; r < reps + 1; ++r) {
                     if (cold) hipLaunchKernelGGL(flush, dim3(8192), dim3(256), 0, 0, scratch, sn, (double)r);
                     CK(hipEventRecord(e0, 0));
-                    hipLaunchKernelGGL(v.k, grid, dim3(B), 0, 0, bufs[MAXP], in, P);
+                    hipLaunchKernelGGL(v.k, grid, dim3(v.bs), 0, 0, bufs[MAXP], in, P);
                     CK(hipEventRecord(e1, 0));
                     CK(hipEventSynchronize(e1));
                     float ms;
@@ -275,7 +326,9 @@ int main(int argc, char **argv) {
             const Var &v = vars[vi];
             if (v.P && v.P != P) continue;
             CK(hipMemset(bufs[MAXP], 0, n * 8));
-            hipLaunchKernelGGL(v.k, dim3((unsigned)(nvec / ((size_t)B * v.U))), dim3(B), 0, 0,
+            const size_t nch = nvec / ((size_t)v.bs * v.U);
+            CK(hipMemcpyToSymbol(HIP_SYMBOL(g_nchunks), &nch, sizeof nch));
+            hipLaunchKernelGGL(v.k, dim3((unsigned)(v.grid ? v.grid : nch)), dim3(v.bs), 0, 0,
                                bufs[MAXP], in, P);
             double h[4];
             CK(hipMemcpy(h, reinterpret_cast<double *>(bufs[MAXP]) + n - 4, sizeof h, hipMemcpyDeviceToHost));
