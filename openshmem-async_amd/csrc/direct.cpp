@@ -263,6 +263,14 @@ void node_done(int start, int step, int P, hipStream_t s, double *stream_us, dou
 
 void count_fused_call() { g_fused_calls += 1; }
 
+bool fused_oneshot_enabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("SHMEMX_FUSED_ONESHOT");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 bool signal_args(int start, int step, int P, SignalArgs *sa) {
     unsigned long long *mine = heap::signal_area();
     if (!mine || P > kMaxFoldInputs) return false;
@@ -427,7 +435,7 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     // One chunk (n <= cmax, known alike everywhere): stage it right away.
     const bool single = n <= cmax;
     d.count = (stage_src || stage_tgt ? 1 : 0) | (partial && tgt > src ? 2 : 0) |
-              (one_shot && single && heap::signal_area() ? 4 : 0);
+              (one_shot && single && fused_oneshot_enabled() && heap::signal_area() ? 4 : 0);
     node::put_desc(d);
     if (single && stage_src)
         SHMX_HIP(hipMemcpyAsync(g_scratch.base, src, bytes, hipMemcpyDeviceToDevice, s));

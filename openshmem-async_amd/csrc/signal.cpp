@@ -113,7 +113,7 @@ int signal_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     std::vector<char *> hb(P);
     for (int i = 0; i < P; ++i) hb[i] = node::peer_base(node::kHeap, start + i * step);
     const void *ins[kMaxFoldInputs];
-    if (tgt != src && bytes <= oneshot_bytes()) {
+    if (tgt != src && bytes <= oneshot_bytes() && fused_oneshot_enabled()) {
         // barrier, fold of every whole source, barrier: one fused launch
         SignalFoldArgs fa{};
         fa.sig = sa;
@@ -131,6 +131,12 @@ int signal_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
         SHMX_HIP(launch_signal(sa, s));
     };
     barrier();   // reduce-op.c:217
+    if (tgt != src && bytes <= oneshot_bytes()) {   // the one shot, unfused
+        for (int i = 0; i < P; ++i) ins[i] = hb[i] + soff;
+        SHMX_HIP(launch_fold(type, op, tgt, ins, P, n, s));
+        barrier();   // reduce-op.c:250
+        return SHMEMX_OK;
+    }
     const size_t g = sz >= 16 ? 1 : 16 / sz;
     size_t slice = (n + P - 1) / P;
     slice = (slice + g - 1) / g * g;

@@ -743,7 +743,7 @@ if fences["fence_refills_host"] or fences["fences_device_incomplete"]:
 # small heap calls ran as one fused launch (DIRECT's and SIGNAL's one shot)
 fences["fused_calls"] = stats["fused_calls"]
 if (scenario in ("full", "signal") and npes > 1 and os.environ.get("SHMEMX_DIRECT_ONESHOT_KB") != "0"
-        and not stats["fused_calls"]):
+        and os.environ.get("SHMEMX_FUSED_ONESHOT") != "0" and not stats["fused_calls"]):
     fails.append("no one-shot call ran as a fused launch")
 shm.free(HEAP_TGT)
 shm.free(HEAP_SRC)

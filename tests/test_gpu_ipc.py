@@ -244,6 +244,20 @@ def test_ipc_signal_device_barriers(tmp_path, npes):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("scenario", ["full", "signal"])
+def test_ipc_one_shot_unfused(tmp_path, scenario):
+    """$SHMEMX_FUSED_ONESHOT=0: DIRECT's and SIGNAL's one shot on their
+    multi-launch schedules (fence + barrier launches around a plain fold),
+    the path the fused launch replaced, still bit-exact on every pair."""
+    reports = run_pes(tmp_path, 3, scenario, {"SHMEMX_FUSED_ONESHOT": "0"})
+    for r in reports:
+        assert r["ncases"] > 0
+        assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
+        assert r["fences"]["fused_calls"] == 0
+    fences_checked(reports, device=scenario == "signal")
+
+
+@pytest.mark.gpu
 def test_ipc_signal_missing_peer_times_out(tmp_path):
     """A peer that never reaches a SIGNAL barrier: the waiting PE's device
     barrier gives up after $SHMEMX_SIGNAL_TIMEOUT and the blocking call aborts
