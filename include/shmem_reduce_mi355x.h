@@ -358,7 +358,8 @@ int shmemx_mirror_stats(unsigned long long *out, int nout, int reset);
  * data to the peers): [7] fences checked on the host, [8] of them run again
  * because a block did not reach some XCD, [9] fences checked by the SIGNAL
  * device barrier, [10] of them incomplete (the call fails); [11] one-shot
- * calls (DIRECT or SIGNAL) that ran as one fused launch.  Fills at most
+ * calls (DIRECT or SIGNAL) that ran as one fused launch, [12] two-shot calls
+ * that did ($SHMEMX_FUSED_TWOSHOT_KB, default 4096).  Fills at most
  * nout values and returns how many; reset != 0 zeroes the counters. */
 int shmemx_direct_stats(double *out, int nout, int reset);
 

@@ -29,7 +29,10 @@
 // one shot (small arrays, every member folds the whole array) runs as ONE
 // fused launch when every member can take it (launch_signal_fold: the
 // fence, both barriers as device handshakes and the fold in one kernel),
-// after a fence-free host barrier that exchanges the descriptors.
+// after a fence-free host barrier that exchanges the descriptors; so does
+// the two shot up to $SHMEMX_FUSED_TWOSHOT_KB (default 4 MiB) when every
+// member's source and target are in its heap segment (three device
+// handshakes and two grid barriers in the kernel, one host wait).
 // Operands outside the symmetric heap (or a source that partially overlaps
 // its target) are staged through a per-PE scratch region, also IPC-mapped,
 // in chunks of half its size ($SHMEMX_DIRECT_SCRATCH_MB, default 512; every
@@ -56,6 +59,7 @@ namespace {
 
 constexpr size_t kDefaultScratchBytes = size_t(512) << 20;
 constexpr size_t kDefaultOneShotBytes = size_t(256) << 10;
+constexpr size_t kDefaultFusedTwoShotBytes = size_t(4) << 20;
 
 // Arrays up to this size take the one-shot path ($SHMEMX_DIRECT_ONESHOT_KB).
 size_t oneshot_bytes() {
@@ -115,6 +119,7 @@ enum Phase { kEntryWait, kEntryBarrier, kFold, kFoldBarrier, kGather, kExitBarri
 double g_phase_us[kNumPhases];
 double g_calls;
 double g_fused_calls;   // one-shot calls that ran as one fused launch (DIRECT and SIGNAL)
+double g_fused2_calls;  // two-shot calls that ran as one fused launch
 
 double now_us() {
     return std::chrono::duration<double, std::micro>(
@@ -262,6 +267,7 @@ void node_done(int start, int step, int P, hipStream_t s, double *stream_us, dou
 }
 
 void count_fused_call() { g_fused_calls += 1; }
+void count_fused_twoshot_call() { g_fused2_calls += 1; }
 
 bool fused_oneshot_enabled() {
     static const bool on = [] {
@@ -269,6 +275,14 @@ bool fused_oneshot_enabled() {
         return !(e && e[0] == '0');
     }();
     return on;
+}
+
+size_t fused_twoshot_bytes() {
+    static const size_t b = [] {
+        const char *e = std::getenv("SHMEMX_FUSED_TWOSHOT_KB");
+        return e ? size_t(std::atol(e)) << 10 : kDefaultFusedTwoShotBytes;
+    }();
+    return b;
 }
 
 bool signal_args(int start, int step, int P, SignalArgs *sa) {
@@ -297,8 +311,9 @@ bool signal_args(int start, int step, int P, SignalArgs *sa) {
 
 int direct_stats(double *out, int nout, bool reset) {
     // [calls, 6 phase times, host fences, host refills, device fence
-    // checks, device fences that missed an XCD, fused one-shot calls]
-    double all[1 + kNumPhases + 5] = {g_calls};
+    // checks, device fences that missed an XCD, fused one-shot calls, fused
+    // two-shot calls]
+    double all[1 + kNumPhases + 6] = {g_calls};
     for (int i = 0; i < kNumPhases; ++i) all[1 + i] = g_phase_us[i];
     unsigned long long dev[2] = {0, 0};
     if (g_fence.dev_stats) {
@@ -310,13 +325,14 @@ int direct_stats(double *out, int nout, bool reset) {
     all[3 + kNumPhases] = (double)dev[0];
     all[4 + kNumPhases] = (double)dev[1];
     all[5 + kNumPhases] = g_fused_calls;
+    all[6 + kNumPhases] = g_fused2_calls;
     const int k = std::min(nout, (int)(sizeof all / sizeof all[0]));
     for (int i = 0; i < k; ++i) out[i] = all[i];
     if (reset) {
         g_calls = 0;
         for (double &v : g_phase_us) v = 0;
         g_fence.host_checks = g_fence.host_refills = 0;
-        g_fused_calls = 0;
+        g_fused_calls = g_fused2_calls = 0;
         if (g_fence.dev_stats) SHMX_HIP(hipMemset(g_fence.dev_stats, 0, sizeof dev));
     }
     return k;
@@ -383,6 +399,53 @@ int direct_fused(int type, int op, char *tgt, size_t n, int start, int step, int
     return SHMEMX_OK;
 }
 
+// DIRECT's two shot as one fused launch (launch_signal_fold, two_shot): every
+// member's source and target in its heap segment, one chunk.  Slice fold,
+// device handshake, gather of the peers' slices, device handshake, in the
+// same kernel; then one wait.
+int direct_fused2(int type, int op, char *tgt, size_t n, int start, int step, int P, int m,
+                  const std::vector<node::Desc> &desc, hipStream_t s) {
+    std::vector<std::pair<node::Region, int>> regs;
+    for (int i = 0; i < P; ++i) regs.emplace_back(node::kHeap, start + i * step);
+    if (!map_regions(regs, start, step, P)) {
+        trace(LOG_REDUCTION, "DIRECT: a member could not map a peer heap (%s)", node::last_ipc_error());
+        return set_error(SHMEMX_ENOTSUP);
+    }
+    SignalFoldArgs fa{};
+    if (!signal_args(start, step, P, &fa.sig)) fatal("DIRECT", "a mapped peer heap went missing");
+    fa.gsync = fence_records().gsync;
+    const size_t sz = type_size(type);
+    const size_t g = sz >= 16 ? 1 : 16 / sz;
+    size_t slice = (n + P - 1) / P;
+    slice = (slice + g - 1) / g * g;
+    auto lo_of = [&](int i) { return std::min(n, (size_t)i * slice); };
+    auto hi_of = [&](int i) { return std::min(n, (size_t)(i + 1) * slice); };
+    fa.out = tgt;
+    for (int i = 0; i < P; ++i) fa.ins[i] = node::peer_base(node::kHeap, start + i * step) + desc[i].src.off;
+    fa.nins = P;
+    fa.n = n;
+    fa.two_shot = 1;
+    fa.lo = lo_of(m);
+    fa.hi = hi_of(m);
+    for (int i = 0; i < P; ++i) {
+        if (i == m || hi_of(i) <= lo_of(i)) continue;
+        fa.gsrc[fa.nseg] = node::peer_base(node::kHeap, start + i * step) + desc[i].tgt.off + lo_of(i) * sz;
+        fa.gdst[fa.nseg] = tgt + lo_of(i) * sz;
+        fa.glen[fa.nseg++] = (hi_of(i) - lo_of(i)) * sz;
+    }
+    const double t0 = now_us();
+    SHMX_HIP(launch_signal_fold(type, op, fa, s));   // reduce-op.c:217-250
+    SHMX_HIP(hipStreamSynchronize(s));
+    g_phase_us[kFold] += now_us() - t0;
+    count_fused_twoshot_call();
+    switch (signal_error()) {
+    case 0: break;
+    case 2: fatal("DIRECT reduction", "a system fence before a device barrier missed an XCD");
+    default: fatal("DIRECT reduction", "a member never reached the device barrier");
+    }
+    return SHMEMX_OK;
+}
+
 }  // namespace
 
 int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int start,
@@ -433,9 +496,13 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     // bit 2: "I can take the fused one-shot launch" (I have the signal
     // counters, at the top of my heap segment)
     // One chunk (n <= cmax, known alike everywhere): stage it right away.
+    // bit 3: "I can take the fused two-shot launch" (source and target in my
+    // heap segment, one chunk)
     const bool single = n <= cmax;
+    const bool twoshot_size = !own_order && !one_shot && bytes <= fused_twoshot_bytes();
     d.count = (stage_src || stage_tgt ? 1 : 0) | (partial && tgt > src ? 2 : 0) |
-              (one_shot && single && fused_oneshot_enabled() && heap::signal_area() ? 4 : 0);
+              (one_shot && single && fused_oneshot_enabled() && heap::signal_area() ? 4 : 0) |
+              (twoshot_size && single && !stage_src && !stage_tgt && heap::signal_area() ? 8 : 0);
     node::put_desc(d);
     if (single && stage_src)
         SHMX_HIP(hipMemcpyAsync(g_scratch.base, src, bytes, hipMemcpyDeviceToDevice, s));
@@ -444,19 +511,21 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     auto read_descs = [&] {
         for (int i = 0; i < P; ++i) desc[i] = i == m ? d : node::get_desc(pe_of(i));
     };
-    if (one_shot) {
+    if (one_shot || twoshot_size) {
         // The descriptors first, with no fence: when every member can, the
         // whole call is one fused launch (system fence on every XCD, device
-        // barrier, fold, device barrier — launch_signal_fold) and one wait,
-        // instead of two fenced host syncs around the fold.  All members see
-        // the same descriptors, so all take the same path.
+        // barriers, fold (and gather), device barrier — launch_signal_fold)
+        // and one wait, instead of fenced host syncs around each kernel.  All
+        // members see the same descriptors, so all take the same path.
         const double t0 = now_us();
         node::barrier(start, step, P);
         g_phase_us[kEntryBarrier] += now_us() - t0;
         read_descs();
+        const int bit = one_shot ? 4 : 8;
         bool fuse = true;
-        for (int i = 0; i < P; ++i) fuse &= (desc[i].count & 4) != 0;
-        if (fuse) return direct_fused(type, op, tgt, n, start, step, P, desc, stage_tgt, s);
+        for (int i = 0; i < P; ++i) fuse &= (desc[i].count & bit) != 0;
+        if (fuse && one_shot) return direct_fused(type, op, tgt, n, start, step, P, desc, stage_tgt, s);
+        if (fuse) return direct_fused2(type, op, tgt, n, start, step, P, m, desc, s);
         // my source (and its staging) is complete; reduce-op.c:217
         node_sync(start, step, P, s, &g_phase_us[kEntryWait], &g_phase_us[kEntryBarrier]);
     } else {

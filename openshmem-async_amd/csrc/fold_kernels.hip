@@ -731,9 +731,227 @@ __global__ __launch_bounds__(kBlock) void signal_fold_kernel(SignalFoldArgs a) {
     }
 }
 
+// ------------------------------------------------ fused two-shot (SIGNAL)
+// The peers' operands are read over xGMI, where a load's latency (µs) rather
+// than HBM bounds a 64-block grid: every lane issues its U 16-B loads from
+// each of the nins inputs (uniform predicates, unrolled) before folding any,
+// so a block keeps U x nins x 4 KiB in flight per step; U = 16 / MAXIN (4
+// vectors per input up to 4 inputs, 2 up to 8, 1 up to 16: 16 vectors in
+// registers either way).
+template <typename T, int OP, int MAXIN>
+__device__ __forceinline__ void fold_vecs(const SignalFoldArgs &a, u32x4 *out, size_t nvec, size_t tid,
+                                          size_t nthr) {
+    constexpr int U = kMaxFoldInputs / MAXIN;
+    const size_t step = nthr * U;
+    auto in = [&](int k) {
+        return reinterpret_cast<const u32x4 *>(static_cast<const T *>(a.ins[k]) + a.lo);
+    };
+    size_t v = (tid / kBlock) * kBlock * U + tid % kBlock;   // U vectors of a block are kBlock apart
+    for (; v + (size_t)(U - 1) * kBlock < nvec; v += step) {
+        u32x4 x[MAXIN][U];
+#pragma unroll
+        for (int k = 0; k < MAXIN; ++k)
+            if (k < a.nins)
+#pragma unroll
+                for (int u = 0; u < U; ++u) x[k][u] = __builtin_nontemporal_load(in(k) + v + u * kBlock);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            u32x4 acc = x[0][u];
+#pragma unroll
+            for (int k = 1; k < MAXIN; ++k)
+                if (k < a.nins) acc = apply16<T, OP>(acc, x[k][u]);
+            out[v + u * kBlock] = acc;
+        }
+    }
+    for (int u = 0; u < U; ++u) {   // the last partial step
+        const size_t w = v + (size_t)u * kBlock;
+        if (w >= nvec) break;
+        u32x4 acc = __builtin_nontemporal_load(in(0) + w);
+        for (int k = 1; k < a.nins; ++k) acc = apply16<T, OP>(acc, __builtin_nontemporal_load(in(k) + w));
+        out[w] = acc;
+    }
+}
+
+template <typename T, int OP>
+__device__ __forceinline__ void fold_span(const SignalFoldArgs &a, size_t tid, size_t nthr) {
+    constexpr int E = 16 / sizeof(T);
+    const size_t lo = a.lo, n = a.hi - a.lo;
+    T *const out = static_cast<T *>(a.out) + lo;
+    bool vec = (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+    for (int k = 0; k < a.nins; ++k)
+        vec &= (reinterpret_cast<uintptr_t>(static_cast<const T *>(a.ins[k]) + lo) & 15) == 0;
+    const size_t nvec = vec ? n / E : 0;
+    u32x4 *const vout = reinterpret_cast<u32x4 *>(out);
+    // soft x87 and the complex products (Annex G recovery branch) unrolled
+    // 16 vectors deep would spill: one vector of one input at a time
+    constexpr bool heavy = std::is_same<T, ld80>::value ||
+                           ((std::is_same<T, cplxd>::value || std::is_same<T, cplxf>::value) &&
+                            OP == SHMEMX_OP_PROD);
+    if constexpr (heavy) {
+        for (size_t v = tid; v < nvec; v += nthr) {
+            u32x4 acc = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(
+                                                       static_cast<const T *>(a.ins[0]) + lo) + v);
+            for (int k = 1; k < a.nins; ++k)
+                acc = apply16<T, OP>(acc, __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(
+                                                  static_cast<const T *>(a.ins[k]) + lo) + v));
+            vout[v] = acc;
+        }
+    } else if (a.nins <= 4) {
+        fold_vecs<T, OP, 4>(a, vout, nvec, tid, nthr);
+    } else if (a.nins <= 8) {
+        fold_vecs<T, OP, 8>(a, vout, nvec, tid, nthr);
+    } else {
+        fold_vecs<T, OP, 16>(a, vout, nvec, tid, nthr);
+    }
+    for (size_t i = nvec * E + tid; i < n; i += nthr) {
+        T acc = static_cast<const T *>(a.ins[0])[lo + i];
+        for (int k = 1; k < a.nins; ++k) acc = Op<T, OP>::ap(acc, static_cast<const T *>(a.ins[k])[lo + i]);
+        out[i] = acc;
+    }
+}
+
+// The all-gather of the two-shot: every segment's loads of a step issued
+// before any store, so all peers' links are busy at once (U vectors per
+// segment per lane, as fold_vecs).
+template <int MAXSEG>
+__device__ __forceinline__ void gather_vecs(const SignalFoldArgs &a, size_t nvec, size_t tid, size_t nthr) {
+    constexpr int U = kMaxFoldInputs / MAXSEG;
+    for (size_t v = (tid / kBlock) * kBlock * U + tid % kBlock; v < nvec; v += nthr * U) {
+        u32x4 x[MAXSEG][U];
+#pragma unroll
+        for (int k = 0; k < MAXSEG; ++k)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (k < a.nseg && v + u * kBlock < a.glen[k] / 16)
+                    x[k][u] = __builtin_nontemporal_load(static_cast<const u32x4 *>(a.gsrc[k]) + v + u * kBlock);
+#pragma unroll
+        for (int k = 0; k < MAXSEG; ++k)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (k < a.nseg && v + u * kBlock < a.glen[k] / 16)
+                    static_cast<u32x4 *>(a.gdst[k])[v + u * kBlock] = x[k][u];
+    }
+}
+
+__device__ __forceinline__ void gather_span(const SignalFoldArgs &a, size_t tid, size_t nthr) {
+    bool vec = true;
+    size_t most = 0;
+    for (int k = 0; k < a.nseg; ++k) {
+        vec &= ((reinterpret_cast<uintptr_t>(a.gsrc[k]) | reinterpret_cast<uintptr_t>(a.gdst[k])) & 15) == 0;
+        most = a.glen[k] > most ? a.glen[k] : most;
+    }
+    if (!vec) {
+        for (int k = 0; k < a.nseg; ++k)
+            for (size_t i = tid; i < a.glen[k]; i += nthr)
+                static_cast<unsigned char *>(a.gdst[k])[i] = static_cast<const unsigned char *>(a.gsrc[k])[i];
+        return;
+    }
+    if (a.nseg <= 4) gather_vecs<4>(a, most / 16, tid, nthr);
+    else if (a.nseg <= 8) gather_vecs<8>(a, most / 16, tid, nthr);
+    else gather_vecs<16>(a, most / 16, tid, nthr);
+    for (int k = 0; k < a.nseg; ++k)
+        for (size_t i = a.glen[k] / 16 * 16 + tid; i < a.glen[k]; i += nthr)
+            static_cast<unsigned char *>(a.gdst[k])[i] = static_cast<const unsigned char *>(a.gsrc[k])[i];
+}
+
+// Grid barrier + peer handshake inside the kernel: every block writes back
+// its XCD's L2 (its own stores become visible over xGMI) and arrives; the
+// last one does the handshake and releases the generation gen_now + 1; every
+// block then drops stale lines of the peers' memory (system acquire) before
+// it reads what the peers wrote.
+__device__ void grid_handshake(const SignalFoldArgs &a, unsigned int gen_now) {
+    unsigned int *const count = a.gsync, *const gen = a.gsync + 1;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope
+        if (__hip_atomic_fetch_add(count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+            peer_handshake(a.sig);
+            __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(gen, gen_now + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen_now) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > a.sig.timeout_ticks) {
+                    __hip_atomic_store(a.sig.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope
+    }
+    __syncthreads();
+}
+
+template <typename T, int OP>
+__global__ __launch_bounds__(kBlock) void signal_fold2_kernel(SignalFoldArgs a) {
+    unsigned int *const count = a.gsync, *const gen = a.gsync + 1;
+    __shared__ int s_last;
+    __shared__ unsigned int s_gen0;
+    if (threadIdx.x == 0) {
+        // entry, as the one shot: record the XCD, fence, arrive
+        const unsigned int xcc = (unsigned int)__builtin_amdgcn_s_getreg(kXccIdReg) & 15u;
+        __hip_atomic_store(a.sig.seen + blockIdx.x, kFenceSeen | xcc, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");   // system scope
+        const unsigned int gen0 = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned int old = __hip_atomic_fetch_add(count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == gridDim.x - 1;
+        if (!s_last) {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gen0) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > a.sig.timeout_ticks) {
+                    __hip_atomic_store(a.sig.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        s_gen0 = gen0;
+    }
+    __syncthreads();
+    if (s_last && threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        unsigned int rec = 0;
+        if (lane < (int)gridDim.x) {
+            rec = __hip_atomic_load(a.sig.seen + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(a.sig.seen + lane, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        int covered = 0;
+#pragma unroll
+        for (unsigned int x = 0; x < 16; ++x) covered += __ballot(rec == (kFenceSeen | x)) != 0 ? 1 : 0;
+        if (lane == 0) {
+            atomicAdd(a.sig.fence_stats, 1ull);
+            if (covered < a.sig.nxcc) {
+                atomicAdd(a.sig.fence_stats + 1, 1ull);
+                __hip_atomic_store(a.sig.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            peer_handshake(a.sig);   // reduce-op.c:217: every source is final
+            __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(gen, s_gen0 + 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x, nthr = (size_t)gridDim.x * kBlock;
+    fold_span<T, OP>(a, tid, nthr);     // my slice from every member's source
+    grid_handshake(a, s_gen0 + 1u);     // every member's slice is final
+    gather_span(a, tid, nthr);          // the other slices from the peers' targets
+    __syncthreads();
+    // exit: the last block to finish reading tells the peers (reduce-op.c:250)
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+        __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        peer_handshake(a.sig);
+    }
+}
+
 template <typename T, int OP>
 hipError_t sf_launch(const SignalFoldArgs &a, hipStream_t s) {
-    hipLaunchKernelGGL((signal_fold_kernel<T, OP>), dim3(kFenceBlocks), dim3(kBlock), 0, s, a);
+    if (a.two_shot)
+        hipLaunchKernelGGL((signal_fold2_kernel<T, OP>), dim3(kFenceBlocks), dim3(kBlock), 0, s, a);
+    else
+        hipLaunchKernelGGL((signal_fold_kernel<T, OP>), dim3(kFenceBlocks), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
 
@@ -775,6 +993,11 @@ hipError_t launch_signal_fold(int type, int op, const SignalFoldArgs &a, hipStre
         if (!a.ins[k]) return hipErrorInvalidValue;
     for (int i = 0; i < a.sig.P; ++i)
         if (a.sig.pe[i] != a.sig.me && !a.sig.peer[i]) return hipErrorInvalidValue;
+    if (a.two_shot) {
+        if (a.lo > a.hi || a.hi > a.n || a.nseg < 0 || a.nseg > kMaxFoldInputs) return hipErrorInvalidValue;
+        for (int k = 0; k < a.nseg; ++k)
+            if (a.glen[k] && (!a.gsrc[k] || !a.gdst[k])) return hipErrorInvalidValue;
+    }
     switch (type) {
     case SHMEMX_TYPE_SHORT: return sf_ops<short>(op, a, stream);
     case SHMEMX_TYPE_INT: return sf_ops<int>(op, a, stream);

@@ -83,6 +83,15 @@ hipError_t launch_signal(const SignalArgs &a, hipStream_t stream);
 // at the first launch and left zero (an arrival counter, a generation).
 // sig.seen must hold kFenceBlocks words.  Launches on one GPU must not
 // overlap (stream order, or one stream).
+//
+// Two-shot (two_shot != 0: SIGNAL's and DIRECT's two-shot schedule for
+// mid-size arrays, as ONE launch): after the entry handshake every block
+// folds its share of elements [lo, hi) only (out, ins indexed alike), then
+// every block writes back its XCD's L2 and arrives; the last block does the
+// mid handshake with the peers (every member's slice is final) and releases
+// the grid; every block drops stale peer lines (system acquire) and copies
+// the nseg byte ranges gsrc[k] -> gdst[k] (the peers' result slices); the
+// last block to finish does the exit handshake.
 struct SignalFoldArgs {
     SignalArgs sig;
     unsigned int *gsync;
@@ -90,6 +99,12 @@ struct SignalFoldArgs {
     const void *ins[kMaxFoldInputs];
     int nins;
     size_t n;
+    int two_shot;
+    size_t lo, hi;
+    int nseg;
+    const void *gsrc[kMaxFoldInputs];
+    void *gdst[kMaxFoldInputs];
+    size_t glen[kMaxFoldInputs];   // bytes
 };
 hipError_t launch_signal_fold(int type, int op, const SignalFoldArgs &a, hipStream_t stream);
 

@@ -29,6 +29,9 @@
 //   barrier                 every slice is final
 //   gather                  the other P-1 slices from the peers' targets
 //   barrier                 nobody reads my source or target any more
+// — as ONE fused launch up to $SHMEMX_FUSED_TWOSHOT_KB (default 4 MiB):
+// launch_signal_fold with two_shot, three handshakes and two grid barriers
+// inside one 64-block kernel, instead of seven launches.
 // One shot (arrays up to $SHMEMX_DIRECT_ONESHOT_KB, target != source):
 //   barrier; fold all of every source -> my target; barrier — as ONE fused
 //   launch (launch_signal_fold: the fence, both handshakes and the fold in
@@ -130,8 +133,8 @@ int signal_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
         SHMX_HIP(launch_sys_fence(s, sa.seen));
         SHMX_HIP(launch_signal(sa, s));
     };
-    barrier();   // reduce-op.c:217
     if (tgt != src && bytes <= oneshot_bytes()) {   // the one shot, unfused
+        barrier();   // reduce-op.c:217
         for (int i = 0; i < P; ++i) ins[i] = hb[i] + soff;
         SHMX_HIP(launch_fold(type, op, tgt, ins, P, n, s));
         barrier();   // reduce-op.c:250
@@ -142,6 +145,29 @@ int signal_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     slice = (slice + g - 1) / g * g;
     auto lo_of = [&](int i) { return std::min(n, (size_t)i * slice); };
     auto hi_of = [&](int i) { return std::min(n, (size_t)(i + 1) * slice); };
+    if (bytes <= fused_twoshot_bytes()) {
+        // barrier, slice fold, barrier, gather, barrier: one fused launch
+        SignalFoldArgs fa{};
+        fa.sig = sa;
+        fa.gsync = fence_records().gsync;
+        fa.out = tgt;
+        for (int i = 0; i < P; ++i) fa.ins[i] = hb[i] + soff;
+        fa.nins = P;
+        fa.n = n;
+        fa.two_shot = 1;
+        fa.lo = lo_of(m);
+        fa.hi = hi_of(m);
+        for (int i = 0; i < P; ++i) {
+            if (i == m || hi_of(i) <= lo_of(i)) continue;
+            fa.gsrc[fa.nseg] = hb[i] + toff + lo_of(i) * sz;
+            fa.gdst[fa.nseg] = tgt + lo_of(i) * sz;
+            fa.glen[fa.nseg++] = (hi_of(i) - lo_of(i)) * sz;
+        }
+        SHMX_HIP(launch_signal_fold(type, op, fa, s));   // reduce-op.c:217-250
+        count_fused_twoshot_call();
+        return SHMEMX_OK;
+    }
+    barrier();   // reduce-op.c:217
     if (hi_of(m) > lo_of(m)) {
         for (int i = 0; i < P; ++i) ins[i] = hb[i] + soff + lo_of(m) * sz;
         SHMX_HIP(launch_fold(type, op, tgt + lo_of(m) * sz, ins, P, hi_of(m) - lo_of(m), s));

@@ -130,9 +130,15 @@ bool signal_args(int start, int step, int P, SignalArgs *sa);
 // A one-shot reduction as one fused launch (launch_signal_fold): count it in
 // shmemx_direct_stats.
 void count_fused_call();
+// A two-shot reduction as one fused launch (launch_signal_fold, two_shot):
+// counted apart in shmemx_direct_stats.
+void count_fused_twoshot_call();
 // $SHMEMX_FUSED_ONESHOT=0 turns the fused one-shot launch off (DIRECT's and
 // SIGNAL's one shot then take their multi-launch schedules); default on.
 bool fused_oneshot_enabled();
+// Two-shot calls up to this many bytes run as one fused launch
+// ($SHMEMX_FUSED_TWOSHOT_KB, default 4 MiB; 0 turns it off).
+size_t fused_twoshot_bytes();
 // Hand data between the members' GPUs: fence_and_wait, then the host barrier
 // over the set.
 // Optionally adds the time spent waiting for the stream (from since_us, a

@@ -350,7 +350,7 @@ DIRECT_PHASES = ("entry_wait_us", "entry_barrier_us", "fold_us", "fold_barrier_u
 
 
 FENCE_STATS = ("fences_host", "fence_refills_host", "fences_device", "fences_device_incomplete")
-DIRECT_COUNTS = ("fused_calls",)
+DIRECT_COUNTS = ("fused_calls", "fused_twoshot_calls")
 
 
 def direct_stats(reset: bool = True) -> dict:

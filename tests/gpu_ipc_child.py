@@ -243,7 +243,8 @@ if scenario == "full":
             for algo in ("direct", "gather"):
                 seed += 1
                 run_case(t, op, 4103, (0, 0, npes), algo, mode, seed)
-    for n in (0, 1, 2, 63, 65, 1 << 20):
+    # 100003 doubles: the fused two-shot launch; 1 Mi: the multi-launch two shot
+    for n in (0, 1, 2, 63, 65, 100003, 1 << 20):
         seed += 1
         run_case("double", "sum", n, (0, 0, npes), "auto", "heap", seed)
     # put through heap_ptr, then a barrier: PE q's slot p holds p + 1
@@ -745,6 +746,12 @@ fences["fused_calls"] = stats["fused_calls"]
 if (scenario in ("full", "signal") and npes > 1 and os.environ.get("SHMEMX_DIRECT_ONESHOT_KB") != "0"
         and os.environ.get("SHMEMX_FUSED_ONESHOT") != "0" and not stats["fused_calls"]):
     fails.append("no one-shot call ran as a fused launch")
+# and mid-size heap calls (100003 doubles; SIGNAL's 70001-element cases) as one
+# fused two-shot launch
+fences["fused_twoshot_calls"] = stats["fused_twoshot_calls"]
+if (scenario in ("full", "signal") and npes > 1 and os.environ.get("SHMEMX_FUSED_TWOSHOT_KB") != "0"
+        and not stats["fused_twoshot_calls"]):
+    fails.append("no two-shot call ran as a fused launch")
 shm.free(HEAP_TGT)
 shm.free(HEAP_SRC)
 shm.finalize()

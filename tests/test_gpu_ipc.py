@@ -246,14 +246,15 @@ def test_ipc_signal_device_barriers(tmp_path, npes):
 @pytest.mark.gpu
 @pytest.mark.parametrize("scenario", ["full", "signal"])
 def test_ipc_one_shot_unfused(tmp_path, scenario):
-    """$SHMEMX_FUSED_ONESHOT=0: DIRECT's and SIGNAL's one shot on their
-    multi-launch schedules (fence + barrier launches around a plain fold),
-    the path the fused launch replaced, still bit-exact on every pair."""
-    reports = run_pes(tmp_path, 3, scenario, {"SHMEMX_FUSED_ONESHOT": "0"})
+    """$SHMEMX_FUSED_ONESHOT=0 and $SHMEMX_FUSED_TWOSHOT_KB=0: DIRECT's and
+    SIGNAL's one shot and two shot on their multi-launch schedules (fence +
+    barrier launches around a plain fold and gather), the paths the fused
+    launches replaced, still bit-exact on every pair."""
+    reports = run_pes(tmp_path, 3, scenario, {"SHMEMX_FUSED_ONESHOT": "0", "SHMEMX_FUSED_TWOSHOT_KB": "0"})
     for r in reports:
         assert r["ncases"] > 0
         assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
-        assert r["fences"]["fused_calls"] == 0
+        assert r["fences"]["fused_calls"] == 0 and r["fences"]["fused_twoshot_calls"] == 0
     fences_checked(reports, device=scenario == "signal")
 
 
