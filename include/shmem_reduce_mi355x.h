@@ -281,6 +281,14 @@ int shmemx_fold_on_stream(int type, int op, void *acc, const void *in,
 int shmemx_fold_n_on_stream(int type, int op, void *out,
                             const void *const *ins, int nins, size_t nelems,
                             void *stream);
+/* The same fold for inputs that live in other GPUs' HBM (IPC-mapped peer
+ * memory, as DIRECT and SIGNAL read it): every lane issues its loads of all
+ * inputs before folding any, so every peer's xGMI link carries traffic at
+ * once (the kernel above folds input k before loading input k + 1, which
+ * keeps all waves behind one link at a time).  Same results, bit for bit. */
+int shmemx_fold_n_peers_on_stream(int type, int op, void *out,
+                                  const void *const *ins, int nins, size_t nelems,
+                                  void *stream);
 
 /* DIRECT's all-gather step as one launch: nseg (<= 16) byte ranges
  * srcs[i] -> dsts[i] copied concurrently (blockIdx.y = segment), so reads

@@ -581,7 +581,7 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
                 if (!own_order || i != m) ins[k2++] = at(sbase[i], desc[i].src, c0);
             char *out = stage_tgt ? scratch_tgt : tgt + c0 * sz;
             const double tf = now_us();
-            fold_chain(type, op, out, ins.data(), P, cnt, s);
+            fold_chain(type, op, out, ins.data(), P, cnt, s, true);
             // reduce-op.c:250: no member reads my source any more
             node_done(start, step, P, s, &g_phase_us[kFold], &g_phase_us[kExitBarrier], tf);
             if (stage_tgt)
@@ -599,7 +599,7 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
         if (hi > lo) {
             for (int i = 0; i < P; ++i) ins[i] = at(sbase[i], desc[i].src, c0 + lo);
             char *out = at(tbase[m], desc[m].tgt, c0 + lo);
-            SHMX_HIP(launch_fold(type, op, out, ins.data(), P, hi - lo, s));
+            SHMX_HIP(launch_fold_peers(type, op, out, ins.data(), P, hi - lo, s));
         }
         // every member's slice is final
         node_sync(start, step, P, s, &g_phase_us[kFold], &g_phase_us[kFoldBarrier], tf);

@@ -193,6 +193,7 @@ struct FoldArgs {
     size_t head;   // scalar elements before the first 16-B aligned vector
     size_t nvec;   // 16-B vectors in the aligned body
     size_t tail;   // scalar elements after it
+    int peers;     // the inputs are other GPUs' HBM (launch_fold_peers)
 };
 
 constexpr int kBlock = 256;  // 4 waves of 64
@@ -304,6 +305,77 @@ __global__ __launch_bounds__(kBlock) void fold_kernel(FoldArgs args) {
 // 16-B vectors per lane per input for the runtime-nins kernel.
 constexpr int kUnrollN = 4;
 
+// The P-input fold over inputs that live in the peers' HBM (DIRECT's and
+// SIGNAL's fold phase).  The runtime-nins kernel above issues input k + 1's
+// loads only after folding input k; with every input on another GPU, every
+// resident wave would then wait on the same peer's link at the same time
+// (all blocks start at input 0 together and stay in step behind that one
+// link), so only one of the P - 1 links would carry traffic at a time.  Here
+// every lane issues its U vectors of ALL inputs before folding any (uniform
+// predicates, unrolled), so each wave has loads in flight on every link; U =
+// 16 / MAXIN keeps 16 vectors in registers (4 per input up to 4 inputs, 2 up
+// to 8, 1 up to 16).  The fold order is unchanged: input 0, then 1, ...
+template <typename T, int OP, int MAXIN, int NT>
+__global__ __launch_bounds__(kBlock) void fold_peers_kernel(FoldArgs args) {
+    constexpr int E = 16 / sizeof(T);
+    constexpr int U = kMaxFoldInputs / MAXIN;
+    const int nins = args.nins;
+    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t nthr = (size_t)gridDim.x * kBlock;
+    {
+        T *out = static_cast<T *>(args.out);
+        const size_t body_end = args.head + args.nvec * E;
+        const size_t nscalar = args.head + args.tail;
+        for (size_t s = tid; s < nscalar; s += nthr) {
+            const size_t i = s < args.head ? s : body_end + (s - args.head);
+            T acc = static_cast<const T *>(args.ins[0])[i];
+            for (int k = 1; k < nins; ++k) acc = Op<T, OP>::ap(acc, static_cast<const T *>(args.ins[k])[i]);
+            out[i] = acc;
+        }
+    }
+    if (args.nvec == 0) return;
+    auto in = [&](int k) {
+        return reinterpret_cast<const u32x4 *>(static_cast<const T *>(args.ins[k]) + args.head);
+    };
+    u32x4 *out = reinterpret_cast<u32x4 *>(static_cast<T *>(args.out) + args.head);
+    const size_t nvec = args.nvec;
+    const size_t step = (size_t)gridDim.x * kBlock * U;
+    for (size_t base = (size_t)blockIdx.x * kBlock * U; base < nvec; base += step) {
+        const size_t v0 = base + threadIdx.x;
+        if (base + (size_t)kBlock * U <= nvec) {
+            u32x4 x[MAXIN][U];
+#pragma unroll
+            for (int k = 0; k < MAXIN; ++k)
+                if (k < nins)
+#pragma unroll
+                    for (int u = 0; u < U; ++u) x[k][u] = ld16<NT>(in(k) + v0 + u * kBlock);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                u32x4 acc = x[0][u];
+#pragma unroll
+                for (int k = 1; k < MAXIN; ++k)
+                    if (k < nins) acc = apply16<T, OP>(acc, x[k][u]);
+                st16<NT>(out + v0 + u * kBlock, acc);
+            }
+        } else {
+            for (int u = 0; u < U; ++u) {
+                const size_t v = v0 + (size_t)u * kBlock;
+                if (v >= nvec) break;
+                u32x4 acc = ld16<NT>(in(0) + v);
+                for (int k = 1; k < nins; ++k) acc = apply16<T, OP>(acc, ld16<NT>(in(k) + v));
+                st16<NT>(out + v, acc);
+            }
+        }
+    }
+}
+
+// long double and the complex products: soft-float / Annex G code unrolled
+// 16 vectors deep would spill; they keep the runtime-nins kernel.
+template <typename T, int OP>
+constexpr bool kHeavyOp = std::is_same<T, ld80>::value ||
+                          ((std::is_same<T, cplxd>::value || std::is_same<T, cplxf>::value) &&
+                           OP == SHMEMX_OP_PROD);
+
 static size_t grid_for(const FoldArgs &a, int unroll) {
     const FoldTuning &tune = fold_tuning();
     size_t work_blocks;
@@ -339,6 +411,16 @@ hipError_t launch_typed(const FoldArgs &a, hipStream_t stream) {
             else
                 hipLaunchKernelGGL((fold_kernel<T, OP, 2, 4, NT>), grid, dim3(kBlock), 0, stream, a);
         }
+    } else if (a.peers && !kHeavyOp<T, OP> && (NT == 0 || NT == 3)) {
+        if (a.nins <= 4)
+            hipLaunchKernelGGL((fold_peers_kernel<T, OP, 4, NT>), dim3((unsigned)grid_for(a, 4)),
+                               dim3(kBlock), 0, stream, a);
+        else if (a.nins <= 8)
+            hipLaunchKernelGGL((fold_peers_kernel<T, OP, 8, NT>), dim3((unsigned)grid_for(a, 2)),
+                               dim3(kBlock), 0, stream, a);
+        else
+            hipLaunchKernelGGL((fold_peers_kernel<T, OP, 16, NT>), dim3((unsigned)grid_for(a, 1)),
+                               dim3(kBlock), 0, stream, a);
     } else {
         hipLaunchKernelGGL((fold_kernel<T, OP, 0, kUnrollN, NT>), dim3((unsigned)grid_for(a, kUnrollN)),
                            dim3(kBlock), 0, stream, a);
@@ -362,6 +444,7 @@ hipError_t launch_nt(const FoldArgs &a, hipStream_t stream) {
     if constexpr (std::is_same<T, ld80>::value) {  // fewer soft-float variants
         return mode ? launch_typed<T, OP, 3>(a, stream) : launch_typed<T, OP, 0>(a, stream);
     } else {
+        if (a.peers) return mode ? launch_typed<T, OP, 3>(a, stream) : launch_typed<T, OP, 0>(a, stream);
         switch (mode & 3) {
         case 0: return launch_typed<T, OP, 0>(a, stream);
         case 1: return launch_typed<T, OP, 1>(a, stream);
@@ -503,11 +586,33 @@ hipError_t launch_fold(int type, int op, void *out, const void *const *ins,
     return dispatch(type, op, a, ptrs, nins + 1, n, stream);
 }
 
+hipError_t launch_fold_peers(int type, int op, void *out, const void *const *ins, int nins, size_t n,
+                             hipStream_t stream) {
+    if (!op_on_device(type, op) || nins < 1 || nins > kMaxFoldInputs || !out)
+        return hipErrorInvalidValue;
+    if (n == 0) return hipSuccess;
+    FoldArgs a{};
+    a.out = out;
+    a.nins = nins;
+    a.peers = 1;
+    const void *ptrs[kMaxFoldInputs + 1];
+    ptrs[0] = out;
+    for (int k = 0; k < nins; ++k) {
+        if (!ins[k]) return hipErrorInvalidValue;
+        a.ins[k] = ins[k];
+        ptrs[k + 1] = ins[k];
+    }
+    return dispatch(type, op, a, ptrs, nins + 1, n, stream);
+}
+
 // ------------------------------------------------------------ gather copy
 // DIRECT's all-gather phase: up to kMaxFoldInputs byte ranges (each a slice
 // of a peer's result, read over xGMI) copied into this PE's target by ONE
-// launch, blockIdx.y = segment, so the reads from all peers are in flight at
-// once (one copy per peer would serialise the links).
+// launch, so the reads from all peers are in flight at once (one copy per
+// peer would serialise the links).  Consecutive blocks take consecutive
+// segments (segment = blockIdx.x mod nseg): workgroups are dispatched in
+// block order, and with the segment as the slow index (blockIdx.y) the first
+// ~2048 resident blocks would all read the same peer, one link at a time.
 namespace {
 
 struct CopySeg {
@@ -517,14 +622,16 @@ struct CopySeg {
 };
 struct GatherArgs {
     CopySeg seg[kMaxFoldInputs];
+    int nseg;
 };
 
 constexpr int kGatherUnroll = 4;
 
 __global__ __launch_bounds__(kBlock) void gather_kernel(GatherArgs a) {
-    const CopySeg sg = a.seg[blockIdx.y];
-    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    const size_t nthr = (size_t)gridDim.x * kBlock;
+    const CopySeg sg = a.seg[blockIdx.x % a.nseg];
+    const size_t bx = blockIdx.x / a.nseg, nbx = gridDim.x / a.nseg;
+    const size_t tid = bx * kBlock + threadIdx.x;
+    const size_t nthr = nbx * kBlock;
     const uintptr_t d = reinterpret_cast<uintptr_t>(sg.dst);
     const uintptr_t s = reinterpret_cast<uintptr_t>(sg.src);
     size_t head = (16 - (d & 15)) & 15;
@@ -540,7 +647,7 @@ __global__ __launch_bounds__(kBlock) void gather_kernel(GatherArgs a) {
     const u32x4 *in = reinterpret_cast<const u32x4 *>(sg.src + head);
     u32x4 *out = reinterpret_cast<u32x4 *>(sg.dst + head);
     const size_t step = nthr * kGatherUnroll;
-    size_t v = (size_t)blockIdx.x * kBlock * kGatherUnroll + threadIdx.x;
+    size_t v = bx * kBlock * kGatherUnroll + threadIdx.x;
     for (; v + (size_t)(kGatherUnroll - 1) * kBlock < nvec; v += step) {
         u32x4 x[kGatherUnroll];
 #pragma unroll
@@ -784,10 +891,7 @@ __device__ __forceinline__ void fold_span(const SignalFoldArgs &a, size_t tid, s
     u32x4 *const vout = reinterpret_cast<u32x4 *>(out);
     // soft x87 and the complex products (Annex G recovery branch) unrolled
     // 16 vectors deep would spill: one vector of one input at a time
-    constexpr bool heavy = std::is_same<T, ld80>::value ||
-                           ((std::is_same<T, cplxd>::value || std::is_same<T, cplxf>::value) &&
-                            OP == SHMEMX_OP_PROD);
-    if constexpr (heavy) {
+    if constexpr (kHeavyOp<T, OP>) {
         for (size_t v = tid; v < nvec; v += nthr) {
             u32x4 acc = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(
                                                        static_cast<const T *>(a.ins[0]) + lo) + v);
@@ -1043,7 +1147,8 @@ hipError_t launch_gather(const void *const *srcs, void *const *dsts, const size_
     size_t bx = (most / 16 + (size_t)kBlock * kGatherUnroll - 1) / ((size_t)kBlock * kGatherUnroll);
     if (bx < 1) bx = 1;
     if (bx > 65535) bx = 65535;
-    hipLaunchKernelGGL(gather_kernel, dim3((unsigned)bx, (unsigned)k), dim3(kBlock), 0, stream, a);
+    a.nseg = k;
+    hipLaunchKernelGGL(gather_kernel, dim3((unsigned)(bx * k)), dim3(kBlock), 0, stream, a);
     return hipGetLastError();
 }
 

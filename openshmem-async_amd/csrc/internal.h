@@ -27,6 +27,12 @@ bool op_on_device(int type, int op);   // this build has a HIP kernel for it
 hipError_t launch_fold(int type, int op, void *out, const void *const *ins,
                        int nins, size_t n, hipStream_t stream);
 
+// launch_fold for inputs in other GPUs' HBM (DIRECT and SIGNAL): every lane
+// issues its loads of all inputs before folding any, so every peer's link is
+// busy at once; same results as launch_fold.
+hipError_t launch_fold_peers(int type, int op, void *out, const void *const *ins, int nins, size_t n,
+                             hipStream_t stream);
+
 // Copy nseg (<= kMaxFoldInputs) byte ranges srcs[i] -> dsts[i] in one launch
 // (DIRECT all-gather: the peers' result slices, read concurrently).
 hipError_t launch_gather(const void *const *srcs, void *const *dsts, const size_t *bytes, int nseg,

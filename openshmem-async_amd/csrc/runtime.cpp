@@ -455,17 +455,18 @@ static long long count_of(long long n, long long chunk, int i) {
 }
 
 void fold_chain(int type, int op, void *out, const void **ins, int nins, size_t n,
-                hipStream_t s) {
+                hipStream_t s, bool peers) {
     // Left fold in groups of kMaxFoldInputs: out = fold(ins[0..15]);
     // out = fold(out, ins[16..30]); ... (same order as one long fold).
+    auto fold = peers ? launch_fold_peers : launch_fold;
     int done = std::min(nins, kMaxFoldInputs);
-    SHMX_HIP(launch_fold(type, op, out, ins, done, n, s));
+    SHMX_HIP(fold(type, op, out, ins, done, n, s));
     while (done < nins) {
         const void *grp[kMaxFoldInputs];
         grp[0] = out;
         int k = 1;
         while (k < kMaxFoldInputs && done < nins) grp[k++] = ins[done++];
-        SHMX_HIP(launch_fold(type, op, out, grp, k, n, s));
+        SHMX_HIP(fold(type, op, out, grp, k, n, s));
     }
 }
 
@@ -909,8 +910,9 @@ int shmemx_fold_on_stream(int type, int op, void *acc, const void *in,
     return SHMEMX_OK;
 }
 
-int shmemx_fold_n_on_stream(int type, int op, void *out, const void *const *ins,
-                            int nins, size_t nelems, void *stream) {
+static int fold_n(int type, int op, void *out, const void *const *ins, int nins, size_t nelems,
+                  void *stream, bool peers) {
+    auto launch = peers ? launch_fold_peers : launch_fold;
     t_last_error = SHMEMX_OK;
     if (!op_on_device(type, op)) return set_error(op_valid(type, op) ? SHMEMX_ENOTSUP : SHMEMX_EINVAL);
     if (nins < 1 || !ins) return set_error(SHMEMX_EINVAL);
@@ -920,15 +922,25 @@ int shmemx_fold_n_on_stream(int type, int op, void *out, const void *const *ins,
         if (!ins[k]) return set_error(SHMEMX_EINVAL);
     int done = std::min(nins, kMaxFoldInputs);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (launch_fold(type, op, out, ins, done, nelems, s) != hipSuccess) return set_error(SHMEMX_EDEVICE);
+    if (launch(type, op, out, ins, done, nelems, s) != hipSuccess) return set_error(SHMEMX_EDEVICE);
     while (done < nins) {
         const void *grp[kMaxFoldInputs];
         grp[0] = out;
         int k = 1;
         while (k < kMaxFoldInputs && done < nins) grp[k++] = ins[done++];
-        if (launch_fold(type, op, out, grp, k, nelems, s) != hipSuccess) return set_error(SHMEMX_EDEVICE);
+        if (launch(type, op, out, grp, k, nelems, s) != hipSuccess) return set_error(SHMEMX_EDEVICE);
     }
     return SHMEMX_OK;
+}
+
+int shmemx_fold_n_on_stream(int type, int op, void *out, const void *const *ins,
+                            int nins, size_t nelems, void *stream) {
+    return fold_n(type, op, out, ins, nins, nelems, stream, false);
+}
+
+int shmemx_fold_n_peers_on_stream(int type, int op, void *out, const void *const *ins,
+                                  int nins, size_t nelems, void *stream) {
+    return fold_n(type, op, out, ins, nins, nelems, stream, true);
 }
 
 int shmemx_gather_on_stream(const void *const *srcs, void *const *dsts, const size_t *bytes,

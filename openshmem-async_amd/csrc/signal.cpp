@@ -136,7 +136,7 @@ int signal_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     if (tgt != src && bytes <= oneshot_bytes()) {   // the one shot, unfused
         barrier();   // reduce-op.c:217
         for (int i = 0; i < P; ++i) ins[i] = hb[i] + soff;
-        SHMX_HIP(launch_fold(type, op, tgt, ins, P, n, s));
+        SHMX_HIP(launch_fold_peers(type, op, tgt, ins, P, n, s));
         barrier();   // reduce-op.c:250
         return SHMEMX_OK;
     }
@@ -170,7 +170,7 @@ int signal_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     barrier();   // reduce-op.c:217
     if (hi_of(m) > lo_of(m)) {
         for (int i = 0; i < P; ++i) ins[i] = hb[i] + soff + lo_of(m) * sz;
-        SHMX_HIP(launch_fold(type, op, tgt + lo_of(m) * sz, ins, P, hi_of(m) - lo_of(m), s));
+        SHMX_HIP(launch_fold_peers(type, op, tgt + lo_of(m) * sz, ins, P, hi_of(m) - lo_of(m), s));
     }
     barrier();   // every member's slice is final
     const void *from[kMaxFoldInputs];

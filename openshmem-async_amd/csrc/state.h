@@ -101,8 +101,10 @@ bool device_accessible(const void *ptr);
 bool host_pinned(const void *ptr);
 void *grow(void *&buf, size_t &have, size_t need);   // grow-only device buffer
 bool stream_capturing(hipStream_t s);
-// out = left fold of ins[0..nins) in groups of kMaxFoldInputs (any nins)
-void fold_chain(int type, int op, void *out, const void **ins, int nins, size_t n, hipStream_t s);
+// out = left fold of ins[0..nins) in groups of kMaxFoldInputs (any nins);
+// peers: the inputs are in other GPUs' HBM (launch_fold_peers)
+void fold_chain(int type, int op, void *out, const void **ins, int nins, size_t n, hipStream_t s,
+                bool peers = false);
 // DIRECT algorithm (direct.cpp); own_order: every PE folds in its own
 // reference order (GATHER semantics on the IPC transport)
 int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int start,

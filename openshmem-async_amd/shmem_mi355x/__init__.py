@@ -80,6 +80,8 @@ def lib() -> ctypes.CDLL:
     L.shmemx_fold_on_stream.restype = i
     L.shmemx_fold_n_on_stream.argtypes = [i, i, vp, ctypes.POINTER(vp), i, sz, vp]
     L.shmemx_fold_n_on_stream.restype = i
+    L.shmemx_fold_n_peers_on_stream.argtypes = [i, i, vp, ctypes.POINTER(vp), i, sz, vp]
+    L.shmemx_fold_n_peers_on_stream.restype = i
     L.shmemx_gather_on_stream.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp),
                                           ctypes.POINTER(sz), i, vp]
     L.shmemx_gather_on_stream.restype = i
@@ -258,11 +260,13 @@ def fold(type_name: str, op: str, acc, inp, nelems: int, stream: int = 0) -> Non
     _check(rc, f"shmemx_fold_on_stream({type_name},{op})")
 
 
-def fold_n(type_name: str, op: str, out, ins, nelems: int, stream: int = 0) -> None:
+def fold_n(type_name: str, op: str, out, ins, nelems: int, stream: int = 0, peers: bool = False) -> None:
+    """shmemx_fold_n_on_stream, or with peers=True shmemx_fold_n_peers_on_stream
+    (every input's loads in flight before any op: the peers' HBM over xGMI)."""
     arr = (ctypes.c_void_p * len(ins))(*[addr(x) for x in ins])
-    rc = lib().shmemx_fold_n_on_stream(TYPES[type_name], OPS[op], addr(out), arr, len(ins),
-                                       nelems, stream or None)
-    _check(rc, f"shmemx_fold_n_on_stream({type_name},{op})")
+    fn = lib().shmemx_fold_n_peers_on_stream if peers else lib().shmemx_fold_n_on_stream
+    rc = fn(TYPES[type_name], OPS[op], addr(out), arr, len(ins), nelems, stream or None)
+    _check(rc, f"shmemx_fold_n{'_peers' if peers else ''}_on_stream({type_name},{op})")
 
 
 def gather(srcs, dsts, nbytes, stream: int = 0) -> None:

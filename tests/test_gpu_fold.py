@@ -240,11 +240,14 @@ def test_longdouble_x87_encodings(cuda, shm, oracle):
             assert same_bits(got, want), (op, order)
 
 
-def test_fold_fuzz_against_oracle(cuda, shm, oracle):
+@pytest.mark.parametrize("peers", [False, True])
+def test_fold_fuzz_against_oracle(cuda, shm, oracle, peers):
     """400 random cases: type, op, 1..20 inputs, 0..70 000 elements, random
-    element offsets per array (same or different alignment mod 16), kind."""
+    element offsets per array (same or different alignment mod 16), kind.
+    peers: the same through shmemx_fold_n_peers_on_stream (DIRECT's and
+    SIGNAL's fold, all inputs' loads in flight), which must agree bit for bit."""
     import torch
-    rng = np.random.default_rng(20251015)
+    rng = np.random.default_rng(20251015 + peers)
     pairs = DEVICE_PAIRS
     for case in range(400):
         t, op = pairs[rng.integers(len(pairs))]
@@ -265,7 +268,7 @@ def test_fold_fuzz_against_oracle(cuda, shm, oracle):
         outbuf = to_dev(torch, np.zeros(n + 8, dtype=dt))
         out = outbuf[offs[0] * isz:(offs[0] + n) * isz] if dt == np.longdouble \
             else outbuf[offs[0]:offs[0] + n]
-        shm.fold_n(t, op, out, ins, n)
+        shm.fold_n(t, op, out, ins, n, peers=peers)
         torch.cuda.synchronize()
         got = from_dev(outbuf, dt)
         assert same_bits(got[offs[0]:offs[0] + n], want), (case, t, op, P, n, list(offs))
