@@ -748,6 +748,28 @@ __device__ void peer_handshake(const SignalArgs &a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope
 }
 
+// One element of the one-shot fold: the peers' values are remote loads
+// (µs each over xGMI), so all nins of them are issued before the first op
+// instead of one load's latency per input; heavy ops keep the loop.
+template <typename T, int OP>
+__device__ __forceinline__ T fold_elem(const SignalFoldArgs &a, size_t i) {
+    if constexpr (kHeavyOp<T, OP>) {
+        T acc = static_cast<const T *>(a.ins[0])[i];
+        for (int k = 1; k < a.nins; ++k) acc = Op<T, OP>::ap(acc, static_cast<const T *>(a.ins[k])[i]);
+        return acc;
+    } else {
+        T x[kMaxFoldInputs];
+#pragma unroll
+        for (int k = 0; k < kMaxFoldInputs; ++k)
+            if (k < a.nins) x[k] = static_cast<const T *>(a.ins[k])[i];
+        T acc = x[0];
+#pragma unroll
+        for (int k = 1; k < kMaxFoldInputs; ++k)
+            if (k < a.nins) acc = Op<T, OP>::ap(acc, x[k]);
+        return acc;
+    }
+}
+
 template <typename T, int OP>
 __global__ __launch_bounds__(kBlock) void signal_fold_kernel(SignalFoldArgs a) {
     unsigned int *const count = a.gsync, *const gen = a.gsync + 1;
@@ -814,21 +836,13 @@ __global__ __launch_bounds__(kBlock) void signal_fold_kernel(SignalFoldArgs a) {
     __syncthreads();
     T *out = static_cast<T *>(a.out);
     if (tiny) {
-        for (size_t i = threadIdx.x; i < a.n; i += kBlock) {
-            T acc = static_cast<const T *>(a.ins[0])[i];
-            for (int k = 1; k < a.nins; ++k) acc = Op<T, OP>::ap(acc, static_cast<const T *>(a.ins[k])[i]);
-            out[i] = acc;
-        }
+        for (size_t i = threadIdx.x; i < a.n; i += kBlock) out[i] = fold_elem<T, OP>(a, i);
         __syncthreads();
         if (threadIdx.x == 0) peer_handshake(a.sig);   // reduce-op.c:250
         return;
     }
     const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x, nthr = (size_t)gridDim.x * kBlock;
-    for (size_t i = tid; i < a.n; i += nthr) {
-        T acc = static_cast<const T *>(a.ins[0])[i];
-        for (int k = 1; k < a.nins; ++k) acc = Op<T, OP>::ap(acc, static_cast<const T *>(a.ins[k])[i]);
-        out[i] = acc;
-    }
+    for (size_t i = tid; i < a.n; i += nthr) out[i] = fold_elem<T, OP>(a, i);
     __syncthreads();
     // exit: the last block to finish reading tells the peers (reduce-op.c:250)
     if (threadIdx.x == 0 &&

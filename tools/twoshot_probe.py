@@ -44,8 +44,9 @@ def main():
     big = 16 << 20
     hs, ht = shm.malloc(big), shm.malloc(big)
     res = {"fused_twoshot_kb": os.environ.get("SHMEMX_FUSED_TWOSHOT_KB", "default"), "npes": world}
-    for kib in (512, 1024, 2048, 4096, 8192, 16384):
-        n = kib * 1024 // 8
+    sizes = [float(x) for x in os.environ.get("PROBE_KIB", "512,1024,2048,4096,8192,16384").split(",")]
+    for kib in sizes:
+        n = max(1, int(kib * 1024) // 8)
         g = torch.Generator(device="cuda")
         srcs = []
         for p in range(world):
@@ -62,14 +63,14 @@ def main():
                 shm.reduce_on_stream("double", "sum", ht, hs, n, 0, 0, world, algo)
                 torch.cuda.synchronize()
             shm.direct_stats(reset=True)
-            row[algo] = per_call(call, 100 if kib <= 4096 else 30)
+            row[algo] = per_call(call, 200 if kib <= 256 else 100 if kib <= 4096 else 30)
             st = shm.direct_stats(reset=True)
             row[algo + "_fused2"] = int(st.get("fused_twoshot_calls", 0))
             got = torch.empty(n, dtype=torch.float64, device="cuda")
             shm.memcpy(got, ht, n * 8)
             torch.cuda.synchronize()
             row[algo + "_exact"] = bool(torch.equal(got.view(torch.int64), want.view(torch.int64)))
-        res[f"{kib}KiB"] = row
+        res[f"{kib:g}KiB"] = row
     if rank == 0:
         print(res, flush=True)
     shm.free(ht)
