@@ -609,10 +609,12 @@ hipError_t launch_fold_peers(int type, int op, void *out, const void *const *ins
 // DIRECT's all-gather phase: up to kMaxFoldInputs byte ranges (each a slice
 // of a peer's result, read over xGMI) copied into this PE's target by ONE
 // launch, so the reads from all peers are in flight at once (one copy per
-// peer would serialise the links).  Consecutive blocks take consecutive
-// segments (segment = blockIdx.x mod nseg): workgroups are dispatched in
-// block order, and with the segment as the slow index (blockIdx.y) the first
-// ~2048 resident blocks would all read the same peer, one link at a time.
+// peer would serialise the links).  Consecutive blocks take the segments in
+// turn: workgroups are dispatched in block order, and with the segment as
+// the slow index (blockIdx.y) the first ~2048 resident blocks would all read
+// the same peer, one link at a time.  On local HBM (one GPU) this costs 4 %
+// against the y-major order (80.5 vs 77.4 us, 7 x 32 MiB), and runs of 16
+// blocks per segment cost 15 % (89.3 us): profiles/r02c_pmc_kernels.json.
 namespace {
 
 struct CopySeg {
@@ -626,10 +628,15 @@ struct GatherArgs {
 };
 
 constexpr int kGatherUnroll = 4;
+constexpr unsigned kGatherRun = 1;   // consecutive blocks on one segment
 
 __global__ __launch_bounds__(kBlock) void gather_kernel(GatherArgs a) {
-    const CopySeg sg = a.seg[blockIdx.x % a.nseg];
-    const size_t bx = blockIdx.x / a.nseg, nbx = gridDim.x / a.nseg;
+    // runs of kGatherRun consecutive blocks per segment, the runs dealt out
+    // to the segments in turn
+    const unsigned run = blockIdx.x / kGatherRun;
+    const CopySeg sg = a.seg[run % a.nseg];
+    const size_t bx = (size_t)(run / a.nseg) * kGatherRun + blockIdx.x % kGatherRun;
+    const size_t nbx = gridDim.x / a.nseg;
     const size_t tid = bx * kBlock + threadIdx.x;
     const size_t nthr = nbx * kBlock;
     const uintptr_t d = reinterpret_cast<uintptr_t>(sg.dst);
@@ -1161,6 +1168,7 @@ hipError_t launch_gather(const void *const *srcs, void *const *dsts, const size_
     size_t bx = (most / 16 + (size_t)kBlock * kGatherUnroll - 1) / ((size_t)kBlock * kGatherUnroll);
     if (bx < 1) bx = 1;
     if (bx > 65535) bx = 65535;
+    bx = (bx + kGatherRun - 1) / kGatherRun * kGatherRun;   // whole runs per segment
     a.nseg = k;
     hipLaunchKernelGGL(gather_kernel, dim3((unsigned)(bx * k)), dim3(kBlock), 0, stream, a);
     return hipGetLastError();

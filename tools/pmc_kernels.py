@@ -6,6 +6,8 @@ FETCH_SIZE and WRITE_SIZE in separate --pmc runs; tools/gpu_pmc_all.sh):
   fold2_long_{and,or,xor}   2 inputs, 64 Mi longs (configs[3]'s fold)
   foldP4_double_sum  P-input fold, P = 4, 16 Mi doubles per input
   foldP8_double_sum  P = 8, 16 Mi - 2048 doubles per input (distinct grid)
+  foldP{4,8}_peers_double_sum  the same folds through fold_peers_kernel
+                     (shmemx_fold_n_peers_on_stream: DIRECT's and SIGNAL's fold)
   foldP8_shard       P = 8 over one 4 Mi-double A2A shard per input, inputs
                      contiguous in one block (the A2A workspace layout)
   gather7            gather_kernel, 7 segments of 4 Mi doubles (DIRECT's
@@ -83,6 +85,13 @@ timed("foldP4_double_sum", lambda: shm.fold_n("double", "sum", out, ins[:4], n, 
 m = n - 2048
 timed("foldP8_double_sum", lambda: shm.fold_n("double", "sum", out, ins, m, s.cuda_stream),
       9 * 8 * m, blocks(m // 2))
+# the peers kernel (DIRECT's and SIGNAL's fold: every input's loads in flight)
+timed("foldP4_peers_double_sum", lambda: shm.fold_n("double", "sum", out, ins[:4], n, s.cuda_stream,
+                                                    peers=True),
+      5 * 8 * n, blocks(n // 2))
+timed("foldP8_peers_double_sum", lambda: shm.fold_n("double", "sum", out, ins, m, s.cuda_stream,
+                                                    peers=True),
+      9 * 8 * m, blocks(m // 2, 2))
 del ins, out
 
 n = 4 * Mi
