@@ -405,7 +405,7 @@ def crossover_extra(world, sp, stream, barrier, max_over_ranks):
     target in the symmetric heap (so DIRECT and SIGNAL can run too): GiB/s of
     the whole job (N * n * 8 B / max-over-ranks time).  The data `auto`'s
     per-size choice between RCCL and the IPC pulls is to be set from."""
-    sizes = [1, 1 << 9, 1 << 12, 1 << 16, 1 << 20, 1 << 24]
+    sizes = [1, 1 << 9, 1 << 12, 1 << 16, 1 << 18, 1 << 20, 1 << 24]
     nbytes = sizes[-1] * 8
     hs, ht = malloc_pair(nbytes)
     out = {"GiBps": {}, "us_per_call": {}}
@@ -429,6 +429,58 @@ def crossover_extra(world, sp, stream, barrier, max_over_ranks):
                     row[str(n)] = row_us[str(n)] = str(e)
             out["GiBps"][algo] = row
             out["us_per_call"][algo] = row_us
+    finally:
+        if ht:
+            shm.free(ht)
+        if hs:
+            shm.free(hs)
+    return out
+
+
+def subset_extra(world, rank, sp, stream, barrier, max_over_ranks):
+    """double sum on partial active sets (N >= 4): the first half of the PEs
+    (PE_start 0, stride 1) and every other PE (PE_start 0, logPE_stride 1),
+    heap operands, per algorithm, microseconds per call (max over ranks;
+    non-members skip the call, as OpenSHMEM's do).  `auto` sends these through
+    grouped-p2p A2A on the RCCL transport; this is the data to revisit it."""
+    if world < 4:
+        return "needs N >= 4"
+    sizes = [1 << 9, 1 << 16, 1 << 20]
+    hs, ht = malloc_pair(sizes[-1] * 8)
+    out = {}
+    try:
+        if not (hs and ht):
+            return "shmem_malloc failed"
+        for name, (start, logstride, size) in (("first_half", (0, 0, world // 2)),
+                                               ("every_other", (0, 1, world // 2))):
+            member = rank >= start and (rank - start) % (1 << logstride) == 0 and \
+                (rank - start) >> logstride < size
+            table = {}
+            for algo in ("a2a", "direct", "signal"):
+                row = {}
+                for n in sizes:
+                    failed = []
+
+                    def step(n=n, algo=algo):
+                        # never raises: a member's error must not leave the
+                        # others waiting in time_region's barrier
+                        if member and not failed:
+                            try:
+                                shm.reduce_on_stream("double", "sum", ht, hs, n, start, logstride, size,
+                                                     algo, sp)
+                            except shm.ShmemError as e:
+                                failed.append(str(e))
+                    for _ in range(3):
+                        step()
+                    k = 20 if n <= 1 << 16 else 10
+                    w, _ = time_region(step, k, stream, barrier)
+                    w = max_over_ranks(w)
+                    if max_over_ranks(1.0 if failed else 0.0):
+                        row[str(n)] = failed[0] if failed else "error on another member"
+                    else:
+                        row[str(n)] = round(w / k * 1e6, 1)
+                table[algo] = row
+            out[f"{name}_us_per_call"] = table
     finally:
         if ht:
             shm.free(ht)
@@ -741,6 +793,7 @@ def main():
         guarded("heap_latency", lambda: heap_latency_extras(world, barrier, max_over_ranks))
         guarded("algo_crossover", lambda: crossover_extra(world, sp, stream, barrier,
                                                                 max_over_ranks))
+        guarded("partial_sets", lambda: subset_extra(world, rank, sp, stream, barrier, max_over_ranks))
 
     timer.cancel()
     faulthandler.cancel_dump_traceback_later()

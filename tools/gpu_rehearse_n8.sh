@@ -1,7 +1,8 @@
 # The driver's N = 4 and N = 8 bench command rehearsed on the one GPU
 # (numbers never reported: 8 processes share one GPU): IPC transport with
 # every extra, then the default RCCL transport through the RCCL test double
-# (headline only; its rates are the double's host-memory shim).
+# (headline only at 8 ranks, every extra at 4; its rates are the double's
+# host-memory shim).
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 export SHMEMX_SHARE_GPU=1 GPU_MAX_HW_QUEUES=2
@@ -17,5 +18,12 @@ timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 
   --master-port 29531 bench.py --gpus 8 --steps 3 --warmup 1 --extras 0 \
   > gpurun_out/rehearse_rccl_n8.json 2> gpurun_out/rehearse_rccl_n8.err
 rc=$?; echo "rccl double n=8 rc=$rc"; grep '"metric"' gpurun_out/rehearse_rccl_n8.json | tail -1 | cut -c1-600
-[ $rc -eq 0 ] || tail -20 gpurun_out/rehearse_rccl_n8.err
+[ $rc -eq 0 ] || { tail -20 gpurun_out/rehearse_rccl_n8.err; exit $rc; }
+# every extra on the RCCL transport at 4 ranks (smaller nreduce: the double
+# moves data through host memory)
+timeout -k 10 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 \
+  --master-port 29532 bench.py --gpus 4 --steps 3 --warmup 1 --nreduce 1048576 \
+  > gpurun_out/rehearse_rccl_n4_extras.json 2> gpurun_out/rehearse_rccl_n4_extras.err
+rc=$?; echo "rccl double n=4 extras rc=$rc"
+[ $rc -eq 0 ] || tail -20 gpurun_out/rehearse_rccl_n4_extras.err
 exit $rc
