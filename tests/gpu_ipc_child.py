@@ -116,13 +116,15 @@ def run_case(t, op, n, st, algo, mode, seed):
         src_p = HEAP_SRC
         if mode == "heap":
             tgt_p = HEAP_TGT
+        elif mode == "heapoff":   # heap operands off 16-B alignment, differently
+            src_p, tgt_p = HEAP_SRC + sz, HEAP_TGT + 3 * sz
         elif mode == "inplace":
             tgt_p = src_p
         else:  # "overlap": target = source + 3 elements (partial overlap)
             tgt_p = src_p + 3 * sz
         if n:
             shm.memcpy(src_p, mine, mine.nbytes)
-        if mode == "heap" and n:
+        if mode in ("heap", "heapoff") and n:
             shm.memcpy(tgt_p, np.full(mine.nbytes, 0xAB, np.uint8), mine.nbytes)
         shm.reduce_on_stream(t, op, tgt_p, src_p, n, *st, algo)
         torch.cuda.synchronize()
@@ -247,6 +249,11 @@ if scenario == "full":
     for n in (0, 1, 2, 63, 65, 100003, 1 << 20):
         seed += 1
         run_case("double", "sum", n, (0, 0, npes), "auto", "heap", seed)
+    # heap operands off 16-B alignment through the fused one- and two-shot
+    for t, op in (("double", "sum"), ("short", "max"), ("int", "prod")):
+        for n in (1013, 100003):
+            seed += 1
+            run_case(t, op, n, (0, 0, npes), "direct", "heapoff", seed)
     # put through heap_ptr, then a barrier: PE q's slot p holds p + 1
     slots = np.zeros(npes, np.int64)
     shm.memcpy(HEAP_TGT, slots, slots.nbytes)
@@ -307,6 +314,13 @@ elif scenario == "signal":
         for n in (4103, 300007):
             seed += 1
             run_case(t, op, n, (0, 0, npes), "signal", "inplace", seed)
+    # heap operands off 16-B alignment (source +1, target +3 elements): the
+    # fused launches' scalar fold and byte gather
+    for t, op in (("double", "sum"), ("short", "max"), ("float", "prod"), ("complexd", "prod"),
+                  ("longdouble", "sum")):
+        for n in (1013, 70001):
+            seed += 1
+            run_case(t, op, n, (0, 0, npes), "signal", "heapoff", seed)
     for n in (0, 1, 2, 63, 65, 1 << 20):
         seed += 1
         run_case("double", "sum", n, (0, 0, npes), "signal", "heap", seed)
