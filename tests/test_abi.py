@@ -205,3 +205,18 @@ def test_fortran_constants_match_the_c_header():
     for name, v in f.items():
         want = int(c[name]) if name == "SHMEM_SYNC_VALUE" else 2 * int(c[name])
         assert int(v) == want, (name, v, c[name])
+
+
+@pytest.mark.parametrize("peers", [False, True])
+def test_fold_n_argument_errors_without_a_device(shm, peers):
+    """shmemx_fold_n_on_stream / shmemx_fold_n_peers_on_stream reject bad
+    arguments before touching HIP: EINVAL for no inputs, a NULL input or a
+    pair the reference lacks; nothing to do for zero elements."""
+    import ctypes
+    fn = shm.lib().shmemx_fold_n_peers_on_stream if peers else shm.lib().shmemx_fold_n_on_stream
+    T, O = shm.TYPES, shm.OPS
+    ins = (ctypes.c_void_p * 2)(8, None)
+    assert fn(T["double"], O["sum"], 8, ins, 0, 16, None) == 1            # nins < 1
+    assert fn(T["double"], O["sum"], 8, ins, 2, 16, None) == 1            # NULL input
+    assert fn(T["double"], O["xor"], 8, ins, 1, 16, None) == 1            # not a reference pair
+    assert fn(T["double"], O["sum"], 8, ins, 2, 0, None) == 0             # zero elements
