@@ -470,9 +470,9 @@ elif scenario == "soak":
             n = min(n, 40000)
         st = rng.choice(sets)
         algo = rng.choice(algos)
-        mode = rng.choice(("heap", "device", "inplace", "overlap", "host"))
+        mode = rng.choice(("heap", "device", "inplace", "overlap", "host", "heapoff"))
         if algo == "signal":
-            mode = rng.choice(("heap", "inplace"))     # symmetric operands only
+            mode = rng.choice(("heap", "inplace", "heapoff"))     # symmetric operands only
         if (n + 3) * 16 > CAP:
             n = CAP // 16 - 3
         try:

@@ -3,7 +3,7 @@
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 ulimit -c 0
-for seed in 21 22; do
+for seed in ${SOAK_SEEDS:-21 22}; do
   SOAK_ITERS=1000 SOAK_SEED=$seed GPU_TEST_LOGDIR=gpurun_out/soak_logs_$seed timeout -k 10 560 \
     python -u -m pytest tests/test_gpu_ipc.py -k soak -x -v --timeout 540 --timeout-method thread \
     > gpurun_out/soak8_$seed.log 2>&1
