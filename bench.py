@@ -429,6 +429,33 @@ def crossover_extra(world, sp, stream, barrier, max_over_ranks):
                     row[str(n)] = row_us[str(n)] = str(e)
             out["GiBps"][algo] = row
             out["us_per_call"][algo] = row_us
+        # the fused two-shot launch against the multi-launch two shot at the
+        # same sizes (512 KiB, 2 MiB, 8 MiB per PE), to set
+        # $SHMEMX_FUSED_TWOSHOT_KB's default from (every rank sets the same
+        # limit before its calls)
+        prev = shm.set_fused_twoshot_kb(0)
+        try:
+            cmp = {}
+            for algo in ("direct", "signal"):
+                cmp[algo] = {}
+                for n in (1 << 16, 1 << 18, 1 << 20):
+                    cell = {}
+                    for label, kb in (("fused", 16384), ("unfused", 0)):
+                        shm.set_fused_twoshot_kb(kb)
+
+                        def step(n=n, algo=algo):
+                            shm.reduce_on_stream("double", "sum", ht, hs, n, 0, 0, world, algo, sp)
+                        try:
+                            for _ in range(3):
+                                step()
+                            w, _ = time_region(step, 10, stream, barrier)
+                            cell[label] = round(max_over_ranks(w) / 10 * 1e6, 1)
+                        except shm.ShmemError as e:
+                            cell[label] = str(e)
+                    cmp[algo][str(n)] = cell
+            out["twoshot_fused_vs_unfused_us"] = cmp
+        finally:
+            shm.set_fused_twoshot_kb(prev)
     finally:
         if ht:
             shm.free(ht)

@@ -304,6 +304,13 @@ int shmemx_gather_on_stream(const void *const *srcs, void *const *dsts,
  * vectors per lane per input of the 2-input fold (2, 4 or 8; default 4). */
 int shmemx_fold_set_tuning(int max_blocks, int nontemporal, int unroll);
 
+/* Largest DIRECT / SIGNAL two-shot call, in KiB, that runs as one fused
+ * launch (default $SHMEMX_FUSED_TWOSHOT_KB, else 4096; 0 = never).  Every
+ * member of a set must hold the same value when it calls (the members choose
+ * their schedules independently).  Returns the previous value, or -1 (and
+ * EINVAL) for kb < 0. */
+long shmemx_set_fused_twoshot_kb(long kb);
+
 /* How a call would be executed (pure host logic, no device needed). */
 typedef struct {
     int algo;          /* resolved SHMEMX_ALGO_* (never AUTO)               */

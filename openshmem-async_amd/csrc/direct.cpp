@@ -277,12 +277,20 @@ bool fused_oneshot_enabled() {
     return on;
 }
 
-size_t fused_twoshot_bytes() {
-    static const size_t b = [] {
-        const char *e = std::getenv("SHMEMX_FUSED_TWOSHOT_KB");
-        return e ? size_t(std::atol(e)) << 10 : kDefaultFusedTwoShotBytes;
-    }();
-    return b;
+namespace {
+long twoshot_kb_from_env() {
+    const char *e = std::getenv("SHMEMX_FUSED_TWOSHOT_KB");
+    return e ? std::max(0L, std::atol(e)) : (long)(kDefaultFusedTwoShotBytes >> 10);
+}
+long g_fused_twoshot_kb = twoshot_kb_from_env();
+}  // namespace
+
+size_t fused_twoshot_bytes() { return size_t(g_fused_twoshot_kb) << 10; }
+
+long set_fused_twoshot_kb(long kb) {
+    const long prev = g_fused_twoshot_kb;
+    g_fused_twoshot_kb = kb;
+    return prev;
 }
 
 bool signal_args(int start, int step, int P, SignalArgs *sa) {

@@ -962,6 +962,15 @@ int shmemx_reduce_plan(int type, int op, int nreduce, int PE_start,
     return make_plan(type, op, nreduce, PE_start, logPE_stride, PE_size, pe, npes, algo, plan);
 }
 
+long shmemx_set_fused_twoshot_kb(long kb) {
+    if (kb < 0) {
+        set_error(SHMEMX_EINVAL);
+        return -1;
+    }
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    return set_fused_twoshot_kb(kb);
+}
+
 int shmemx_fold_set_tuning(int max_blocks, int nontemporal, int unroll) {
     if (max_blocks < 0 || (unroll != 2 && unroll != 4 && unroll != 8)) return set_error(SHMEMX_EINVAL);
     FoldTuning &t = fold_tuning();

@@ -141,6 +141,7 @@ bool fused_oneshot_enabled();
 // Two-shot calls up to this many bytes run as one fused launch
 // ($SHMEMX_FUSED_TWOSHOT_KB, default 4 MiB; 0 turns it off).
 size_t fused_twoshot_bytes();
+long set_fused_twoshot_kb(long kb);   // shmemx_set_fused_twoshot_kb; returns the previous value
 // Hand data between the members' GPUs: fence_and_wait, then the host barrier
 // over the set.
 // Optionally adds the time spent waiting for the stream (from since_us, a

@@ -97,6 +97,8 @@ def lib() -> ctypes.CDLL:
     L.shmemx_set_algo.restype = i
     L.shmemx_fold_set_tuning.argtypes = [i, i, i]
     L.shmemx_fold_set_tuning.restype = i
+    L.shmemx_set_fused_twoshot_kb.argtypes = [ctypes.c_long]
+    L.shmemx_set_fused_twoshot_kb.restype = ctypes.c_long
     L.shmemx_type_size.argtypes = [i]
     L.shmemx_type_size.restype = sz
     L.shmemx_op_valid.argtypes = [i, i]
@@ -224,6 +226,16 @@ def n_pes() -> int:
 
 def get_stream() -> int:
     return lib().shmemx_get_stream() or 0
+
+
+def set_fused_twoshot_kb(kb: int) -> int:
+    """shmemx_set_fused_twoshot_kb: the largest DIRECT/SIGNAL two-shot call
+    (KiB) run as one fused launch; returns the previous limit.  Collective in
+    effect: every member must set the same value."""
+    prev = lib().shmemx_set_fused_twoshot_kb(kb)
+    if prev < 0:
+        raise ShmemError(1, "shmemx_set_fused_twoshot_kb")
+    return prev
 
 
 def set_algo(name: str) -> str:

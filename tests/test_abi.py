@@ -220,3 +220,17 @@ def test_fold_n_argument_errors_without_a_device(shm, peers):
     assert fn(T["double"], O["sum"], 8, ins, 2, 16, None) == 1            # NULL input
     assert fn(T["double"], O["xor"], 8, ins, 1, 16, None) == 1            # not a reference pair
     assert fn(T["double"], O["sum"], 8, ins, 2, 0, None) == 0             # zero elements
+
+
+def test_fused_twoshot_limit_setter(shm):
+    """shmemx_set_fused_twoshot_kb returns the previous limit (the 4 MiB
+    default unless $SHMEMX_FUSED_TWOSHOT_KB says otherwise) and refuses a
+    negative one."""
+    import os
+    default = int(os.environ.get("SHMEMX_FUSED_TWOSHOT_KB", "4096"))
+    prev = shm.set_fused_twoshot_kb(0)
+    assert prev == default
+    assert shm.set_fused_twoshot_kb(16384) == 0
+    with pytest.raises(shm.ShmemError):
+        shm.set_fused_twoshot_kb(-1)
+    assert shm.set_fused_twoshot_kb(prev) == 16384
