@@ -400,6 +400,51 @@ def direct_extra(world, n, src, sp, stream, barrier, max_over_ranks, steps, algo
             shm.free(hs)
 
 
+def coherence_extra(world, rank, sp, max_over_ranks, iters=20):
+    """Cross-GPU coherence check of the IPC pulls (N > 1): DIRECT and SIGNAL
+    on heap operands whose contents change on every call, at a fused one-shot
+    (1 KiB), a fused two-shot (1 MiB) and a multi-launch two-shot (16 MiB)
+    size.  Source values are small integers, (i mod 1024) + 7 * rank + 3 * it,
+    so every PE's sum is exact in any order and the whole target is compared
+    with it.  A stale line of a peer's previous source or target (an L2 that
+    was not written back or invalidated on some XCD) shows up as mismatched
+    elements.  Reports calls and the mismatches summed over elements, max
+    over ranks."""
+    sizes = [128, 1 << 17, 1 << 21]
+    hs, ht = malloc_pair(sizes[-1] * 8)
+    out = {}
+    try:
+        if not (hs and ht):
+            return "shmem_malloc failed"
+        for algo in ("direct", "signal"):
+            bad = calls = 0
+            err = None
+            for it in range(iters):
+                for n in sizes:
+                    base = torch.arange(n, device="cuda", dtype=torch.float64).remainder_(1024)
+                    shm.memcpy(hs, base + (7 * rank + 3 * it), n * 8)
+                    try:
+                        shm.reduce_on_stream("double", "sum", ht, hs, n, 0, 0, world, algo, sp)
+                    except shm.ShmemError as e:
+                        err = str(e)
+                        break
+                    torch.cuda.synchronize()
+                    got = torch.empty(n, device="cuda", dtype=torch.float64)
+                    shm.memcpy(got, ht, n * 8)
+                    want = base * world + (7 * world * (world - 1) // 2 + 3 * it * world)
+                    bad += int((got != want).sum().item())
+                    calls += 1
+                if err:
+                    break
+            out[algo] = err if err else {"calls": calls, "mismatched_elements": int(max_over_ranks(bad))}
+    finally:
+        if ht:
+            shm.free(ht)
+        if hs:
+            shm.free(hs)
+    return out
+
+
 def crossover_extra(world, sp, stream, barrier, max_over_ranks):
     """double sum over the full set, per algorithm and size, with source and
     target in the symmetric heap (so DIRECT and SIGNAL can run too): GiB/s of
@@ -817,6 +862,7 @@ def main():
                                                     max_over_ranks, max(3, a.steps // 4)))
         guarded("signal_heap", lambda: direct_extra(world, n, src, sp, stream, barrier,
                                                     max_over_ranks, max(3, a.steps // 4), "signal"))
+        guarded("coherence", lambda: coherence_extra(world, rank, sp, max_over_ranks))
         guarded("heap_latency", lambda: heap_latency_extras(world, barrier, max_over_ranks))
         guarded("algo_crossover", lambda: crossover_extra(world, sp, stream, barrier,
                                                                 max_over_ranks))
