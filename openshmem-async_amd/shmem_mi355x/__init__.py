@@ -436,14 +436,21 @@ _hip = None
 
 def memcpy(dst, src, nbytes: int) -> None:
     """hipMemcpy(kind = default) between any host/device addresses (heap
-    pointers are plain device addresses, not tensors)."""
+    pointers are plain device addresses, not tensors), complete on return.
+    A device-to-device hipMemcpy returns before the copy has run (it is only
+    ordered on the legacy default stream), so a reduction enqueued right
+    after it on a non-blocking stream (torch.cuda.Stream, the stream-ordered
+    API) could read the old bytes: the device is synchronised here."""
     global _hip
     if _hip is None:
         lib()   # torch's HIP runtime first
         _hip = ctypes.CDLL("libamdhip64.so.7")
         _hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
         _hip.hipMemcpy.restype = ctypes.c_int
+        _hip.hipDeviceSynchronize.restype = ctypes.c_int
     rc = _hip.hipMemcpy(addr(dst), addr(src), nbytes, 4)   # hipMemcpyDefault
+    if rc == 0:
+        rc = _hip.hipDeviceSynchronize()
     if rc != 0:
         raise ShmemError(6, f"hipMemcpy failed ({rc})")
 
