@@ -480,7 +480,11 @@ void *pshmem_realloc(void *ptr, size_t size) {
         const size_t keep = old_bytes < size ? old_bytes : size;
         void *dst = heap::device_operand(p, keep);
         const void *src = heap::device_operand(ptr, keep);
-        SHMX_HIP(hipMemcpy(dst, src, keep, hipMemcpyDefault));
+        // complete before the old block is freed (a device-to-device
+        // hipMemcpy would return before the copy ran); the library stream is
+        // ordered after the legacy default stream, so earlier writes land first
+        SHMX_HIP(hipMemcpyAsync(dst, src, keep, hipMemcpyDefault, g_state.stream));
+        SHMX_HIP(hipStreamSynchronize(g_state.stream));
         heap::device_wrote(p, keep);
         heap_free(ptr);
     }
