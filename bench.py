@@ -61,6 +61,9 @@ def parse():
     ap.add_argument("--extras", type=int, default=1, help="also time the other algorithms / API forms")
     ap.add_argument("--extras-timeout", type=float, default=300.0,
                     help="seconds the extras may take before the line is printed without the rest")
+    ap.add_argument("--extras-max-nreduce", type=int, default=256 * 1024 * 1024,
+                    help="cap on the extras' array sizes (elements; the tests' short N > 1 runs "
+                         "lower it; the driver's runs keep the full BASELINE.json sizes)")
     return ap.parse_args()
 
 
@@ -206,11 +209,11 @@ def host_e2e(n: int):
     return res
 
 
-def config_extras(world, stream, barrier, max_over_ranks):
+def config_extras(world, stream, barrier, max_over_ranks, cap=256 * 1024 * 1024):
     """BASELINE.json configs[3] and [4] as extra lines (not `value`):
     long and/or/xor over 64 Mi elements, and the float sum GiB/s-vs-size curve
-    for nreduce 4 Ki .. 256 Mi.  At N = 1 the step is the local fold (2
-    inputs), at N > 1 the full collective."""
+    for nreduce 4 Ki .. 256 Mi (both capped at `cap` elements).  At N = 1 the
+    step is the local fold (2 inputs), at N > 1 the full collective."""
     sp = stream.cuda_stream
     g = torch.Generator(device="cuda")
     g.manual_seed(0xC0F + int(os.environ.get("RANK", "0")))
@@ -253,11 +256,13 @@ def config_extras(world, stream, barrier, max_over_ranks):
         w = max_over_ranks(w)
         return round(world * n * elem * steps / w / GiB, 2)
 
+    nlong = min(64 * 1024 * 1024, cap)
     for op in ("and", "or", "xor"):
-        out[f"long_{op}_64Mi_GiBps"] = rate("long", op, 64 * 1024 * 1024, 8, 10)
+        key = "64Mi" if nlong == 64 * 1024 * 1024 else str(nlong)
+        out[f"long_{op}_{key}_GiBps"] = rate("long", op, nlong, 8, 10)
     cold, warm = {}, {}
     n = 4 * 1024
-    while n <= 256 * 1024 * 1024:
+    while n <= min(256 * 1024 * 1024, cap):
         steps = 20 if n >= 1 << 24 else 50
         cold[str(n)] = rate("float", "sum", n, 4, steps, cold=True)
         warm[str(n)] = rate("float", "sum", n, 4, steps)
@@ -445,20 +450,49 @@ def coherence_extra(world, rank, sp, max_over_ranks, iters=20):
     return out
 
 
-def crossover_extra(world, sp, stream, barrier, max_over_ranks):
+def exact_source(hs, n, rank):
+    """Fill heap block hs with (i mod 1024) + rank: small integers, so any
+    summation order gives the exact sum, and the target can be checked whole."""
+    base = torch.arange(n, device="cuda", dtype=torch.float64).remainder_(1024)
+    shm.memcpy(hs, base + rank, n * 8)
+    return base
+
+
+def exact_target_ok(ht, base, n, members):
+    """Is the target [0, n) at hs's exact sum over `members` (ranks)?"""
+    got = torch.empty(n, device="cuda", dtype=torch.float64)
+    shm.memcpy(got, ht, n * 8)
+    return bool(torch.equal(got, base * len(members) + float(sum(members))))
+
+
+# The size buckets and set shapes `auto` chooses among (bytes per PE), and
+# the algorithms the library's table ($SHMEMX_AUTO_FULL / _PARTIAL) may name:
+# SIGNAL is timed but never a table choice (it needs heap operands on every
+# PE; DIRECT takes any operand and runs the same fused launches on heap ones).
+AUTO_BUCKETS = {"8B": 1, "4KiB": 1 << 9, "512KiB": 1 << 16, "4MiB": 1 << 19, "128MiB": 1 << 24}
+AUTO_TABLE_ALGOS = {"full": ("allreduce", "rccl", "a2a", "direct", "gather"),
+                    "partial": ("a2a", "direct", "gather")}
+
+
+def crossover_extra(world, rank, sp, stream, barrier, max_over_ranks, cap=1 << 24):
     """double sum over the full set, per algorithm and size, with source and
     target in the symmetric heap (so DIRECT and SIGNAL can run too): GiB/s of
-    the whole job (N * n * 8 B / max-over-ranks time).  The data `auto`'s
-    per-size choice between RCCL and the IPC pulls is to be set from."""
-    sizes = [1, 1 << 9, 1 << 12, 1 << 16, 1 << 18, 1 << 20, 1 << 24]
+    the whole job (N * n * 8 B / max-over-ranks time), microseconds per call,
+    and whether every element of every PE's target was exact after the timed
+    calls.  The data `auto`'s per-size choice (auto_recommendation) is set
+    from."""
+    sizes = sorted(set([1, 1 << 9, 1 << 12, 1 << 16, 1 << 18, 1 << 19, 1 << 20, 1 << 24]))
+    sizes = [n for n in sizes if n <= cap] or [1]
     nbytes = sizes[-1] * 8
     hs, ht = malloc_pair(nbytes)
-    out = {"GiBps": {}, "us_per_call": {}}
+    out = {"GiBps": {}, "us_per_call": {}, "correct": {}}
     try:
         if not (hs and ht):
             return "shmem_malloc failed"
-        for algo in ("rccl", "allreduce", "a2a", "direct", "signal"):
-            row, row_us = {}, {}
+        base = exact_source(hs, sizes[-1], rank)
+        torch.cuda.synchronize()
+        for algo in ("rccl", "allreduce", "a2a", "direct", "signal", "gather"):
+            row, row_us, row_ok = {}, {}, {}
             for n in sizes:
                 def step(n=n, algo=algo):
                     shm.reduce_on_stream("double", "sum", ht, hs, n, 0, 0, world, algo, sp)
@@ -470,10 +504,13 @@ def crossover_extra(world, sp, stream, barrier, max_over_ranks):
                     w = max_over_ranks(w)
                     row[str(n)] = round(world * n * 8 * k / w / GiB, 4)
                     row_us[str(n)] = round(w / k * 1e6, 1)
+                    ok = exact_target_ok(ht, base[:n], n, range(world))
+                    row_ok[str(n)] = max_over_ranks(0.0 if ok else 1.0) == 0.0
                 except shm.ShmemError as e:
-                    row[str(n)] = row_us[str(n)] = str(e)
+                    row[str(n)] = row_us[str(n)] = row_ok[str(n)] = str(e)
             out["GiBps"][algo] = row
             out["us_per_call"][algo] = row_us
+            out["correct"][algo] = row_ok
         # the fused two-shot launch against the multi-launch two shot at the
         # same sizes (512 KiB, 2 MiB, 8 MiB per PE), to set
         # $SHMEMX_FUSED_TWOSHOT_KB's default from (every rank sets the same
@@ -483,7 +520,7 @@ def crossover_extra(world, sp, stream, barrier, max_over_ranks):
             cmp = {}
             for algo in ("direct", "signal"):
                 cmp[algo] = {}
-                for n in (1 << 16, 1 << 18, 1 << 20):
+                for n in [m for m in (1 << 16, 1 << 18, 1 << 20) if m <= cap]:
                     cell = {}
                     for label, kb in (("fused", 16384), ("unfused", 0)):
                         shm.set_fused_twoshot_kb(kb)
@@ -509,27 +546,30 @@ def crossover_extra(world, sp, stream, barrier, max_over_ranks):
     return out
 
 
-def subset_extra(world, rank, sp, stream, barrier, max_over_ranks):
+def subset_extra(world, rank, sp, stream, barrier, max_over_ranks, cap=1 << 24):
     """double sum on partial active sets (N >= 4): the first half of the PEs
     (PE_start 0, stride 1) and every other PE (PE_start 0, logPE_stride 1),
     heap operands, per algorithm, microseconds per call (max over ranks;
-    non-members skip the call, as OpenSHMEM's do).  `auto` sends these through
-    grouped-p2p A2A on the RCCL transport; this is the data to revisit it."""
+    non-members skip the call, as OpenSHMEM's do) and whether every member's
+    target was exact.  `auto` sends these through grouped-p2p A2A on the RCCL
+    transport by default; this is the data to revisit it (auto_recommendation)."""
     if world < 4:
         return "needs N >= 4"
-    sizes = [1 << 9, 1 << 16, 1 << 20]
+    sizes = [n for n in AUTO_BUCKETS.values() if n <= cap] or [1]
     hs, ht = malloc_pair(sizes[-1] * 8)
     out = {}
     try:
         if not (hs and ht):
             return "shmem_malloc failed"
+        base = exact_source(hs, sizes[-1], rank)
+        torch.cuda.synchronize()
         for name, (start, logstride, size) in (("first_half", (0, 0, world // 2)),
                                                ("every_other", (0, 1, world // 2))):
-            member = rank >= start and (rank - start) % (1 << logstride) == 0 and \
-                (rank - start) >> logstride < size
-            table = {}
-            for algo in ("a2a", "direct", "signal"):
-                row = {}
+            members = [start + (i << logstride) for i in range(size)]
+            member = rank in members
+            table, table_ok = {}, {}
+            for algo in ("a2a", "direct", "signal", "gather"):
+                row, row_ok = {}, {}
                 for n in sizes:
                     failed = []
 
@@ -548,16 +588,76 @@ def subset_extra(world, rank, sp, stream, barrier, max_over_ranks):
                     w, _ = time_region(step, k, stream, barrier)
                     w = max_over_ranks(w)
                     if max_over_ranks(1.0 if failed else 0.0):
-                        row[str(n)] = failed[0] if failed else "error on another member"
+                        row[str(n)] = row_ok[str(n)] = failed[0] if failed else "error on another member"
                     else:
                         row[str(n)] = round(w / k * 1e6, 1)
+                        ok = exact_target_ok(ht, base[:n], n, members) if member else True
+                        row_ok[str(n)] = max_over_ranks(0.0 if ok else 1.0) == 0.0
                 table[algo] = row
+                table_ok[algo] = row_ok
             out[f"{name}_us_per_call"] = table
+            out[f"{name}_correct"] = table_ok
     finally:
         if ht:
             shm.free(ht)
         if hs:
             shm.free(hs)
+    return out
+
+
+def auto_recommendation(crossover, partial):
+    """The fastest correct algorithm per size bucket and set shape, from the
+    crossover (full set) and partial_sets tables, as one compact object, plus
+    the $SHMEMX_AUTO_FULL / $SHMEMX_AUTO_PARTIAL values that make the
+    library's `auto` take it (runtime.cpp make_plan; "bytes:algo" cut
+    points, ascending; a cut between two buckets sits at their geometric
+    mean).  "fastest" names the fastest correct algorithm of all (SIGNAL
+    included); "table" the fastest the table may name."""
+    def best(us_row, ok_row, algos):
+        cands = [(us_row[a], a) for a in algos
+                 if isinstance(us_row.get(a), (int, float)) and ok_row.get(a) is True]
+        return min(cands)[1] if cands else None
+
+    shapes = {}
+    if isinstance(crossover, dict):
+        shapes["full"] = (crossover.get("us_per_call", {}), crossover.get("correct", {}))
+    if isinstance(partial, dict):
+        shapes["half"] = (partial.get("first_half_us_per_call", {}), partial.get("first_half_correct", {}))
+        shapes["strided"] = (partial.get("every_other_us_per_call", {}), partial.get("every_other_correct", {}))
+    out = {}
+    for shape, (us, ok) in shapes.items():
+        row = {}
+        for label, n in AUTO_BUCKETS.items():
+            us_n = {a: r.get(str(n)) for a, r in us.items()}
+            ok_n = {a: r.get(str(n)) for a, r in ok.items()}
+            kind = "full" if shape == "full" else "partial"
+            row[label] = {"fastest": best(us_n, ok_n, list(us_n)),
+                          "table": best(us_n, ok_n, AUTO_TABLE_ALGOS[kind]),
+                          "us": {a: v for a, v in us_n.items() if isinstance(v, (int, float))}}
+        out[shape] = row
+
+    def env_value(rows):
+        cuts, prev_n, prev_algo = [], None, None
+        for label, n in AUTO_BUCKETS.items():
+            algo = rows.get(label, {}).get("table")
+            if algo is None:
+                continue
+            if algo != prev_algo:
+                cut = 0 if prev_n is None else int(((prev_n * 8) * (n * 8)) ** 0.5)
+                cuts.append(f"{cut}:{algo}")
+                prev_algo = algo
+            prev_n = n
+        return ",".join(cuts)
+    env = {}
+    if "full" in out:
+        env["SHMEMX_AUTO_FULL"] = env_value(out["full"])
+    # one partial table for both partial shapes: the strided set's choice
+    # (every other PE crosses the most links), else the half set's
+    for shape in ("strided", "half"):
+        if shape in out and env_value(out[shape]):
+            env["SHMEMX_AUTO_PARTIAL"] = env_value(out[shape])
+            break
+    out["env"] = env
     return out
 
 
@@ -835,7 +935,8 @@ def main():
                         "us_per_call": round(e2 / k2 * 1e6, 2)}
             guarded("api_pe_size_1", api_pe_size_1)
             guarded("host_resident_e2e", lambda: host_e2e(n))
-            guarded("configs", lambda: config_extras(world, stream, barrier, max_over_ranks))
+            guarded("configs", lambda: config_extras(world, stream, barrier, max_over_ranks,
+                                                     a.extras_max_nreduce))
             guarded("latency", lambda: latency_extras(world, barrier, max_over_ranks))
     elif a.extras:
         for alt in ("rccl", "allreduce", "a2a", "gather"):
@@ -855,7 +956,8 @@ def main():
                 except shm.ShmemError as e:
                     return str(e)
             guarded(f"algo_{alt}_GiBps", alt_rate)
-        guarded("configs", lambda: config_extras(world, stream, barrier, max_over_ranks))
+        guarded("configs", lambda: config_extras(world, stream, barrier, max_over_ranks,
+                                                     a.extras_max_nreduce))
         guarded("latency", lambda: latency_extras(world, barrier, max_over_ranks))
         # last: the kernels that load from the peers' HBM through IPC mappings
         guarded("direct_heap", lambda: direct_extra(world, n, src, sp, stream, barrier,
@@ -864,9 +966,12 @@ def main():
                                                     max_over_ranks, max(3, a.steps // 4), "signal"))
         guarded("coherence", lambda: coherence_extra(world, rank, sp, max_over_ranks))
         guarded("heap_latency", lambda: heap_latency_extras(world, barrier, max_over_ranks))
-        guarded("algo_crossover", lambda: crossover_extra(world, sp, stream, barrier,
-                                                                max_over_ranks))
-        guarded("partial_sets", lambda: subset_extra(world, rank, sp, stream, barrier, max_over_ranks))
+        guarded("algo_crossover", lambda: crossover_extra(world, rank, sp, stream, barrier,
+                                                          max_over_ranks, a.extras_max_nreduce))
+        guarded("partial_sets", lambda: subset_extra(world, rank, sp, stream, barrier, max_over_ranks,
+                                                     a.extras_max_nreduce))
+        guarded("auto_recommendation", lambda: auto_recommendation(extras.get("algo_crossover"),
+                                                                   extras.get("partial_sets")))
 
     timer.cancel()
     faulthandler.cancel_dump_traceback_later()

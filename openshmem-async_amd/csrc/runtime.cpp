@@ -316,6 +316,61 @@ static long long allreduce_max_bytes() {
     return b;
 }
 
+// AUTO's per-size table, from the driver's multi-GPU bench
+// (extras.auto_recommendation.env): $SHMEMX_AUTO_FULL for the whole job,
+// $SHMEMX_AUTO_PARTIAL for partial and strided sets, each a list of
+// "bytes:algo" cut points in ascending order ("0:allreduce,3145728:rccl":
+// arrays of fewer than 3 MiB per PE take one all-reduce, larger ones
+// reduce-scatter + all-gather).  Names: allreduce, rccl, a2a, direct, gather.
+// A cut whose algorithm cannot serve a call (an RCCL algorithm for a pair
+// RCCL does not reduce as the reference does, DIRECT without the node block)
+// falls back to the built-in rule, so every PE still plans alike.  Unset or
+// unparsable: the built-in rule alone (the bad value is reported once).
+struct AutoCut {
+    long long bytes;
+    int algo;
+};
+
+static std::vector<AutoCut> parse_auto_table(const char *var) {
+    std::vector<AutoCut> cuts;
+    const char *e = std::getenv(var);
+    if (!e || !*e) return cuts;
+    std::string s(e);
+    size_t pos = 0;
+    long long last = -1;
+    while (pos <= s.size()) {
+        const size_t end = std::min(s.find(',', pos), s.size());
+        const std::string item = s.substr(pos, end - pos);
+        const size_t colon = item.find(':');
+        char *stop = nullptr;
+        const long long b = colon == std::string::npos ? -1 : std::strtoll(item.c_str(), &stop, 10);
+        const std::string name = colon == std::string::npos ? "" : item.substr(colon + 1);
+        const int a = parse_algo(name.c_str());
+        const bool named = name == "allreduce" || name == "rccl" || name == "a2a" || name == "direct" ||
+                           name == "gather";
+        if (b < 0 || stop != item.c_str() + colon || !named || b <= last) {
+            trace(LOG_INFO, "%s=\"%s\": unusable cut \"%s\"; the built-in rule applies", var, e,
+                  item.c_str());
+            return {};
+        }
+        cuts.push_back({b, a});
+        last = b;
+        pos = end + 1;
+    }
+    return cuts;
+}
+
+// The table's algorithm for an array of `bytes` per PE, or AUTO.
+static int auto_table_algo(bool world, long long bytes) {
+    static const std::vector<AutoCut> full = parse_auto_table("SHMEMX_AUTO_FULL");
+    static const std::vector<AutoCut> partial = parse_auto_table("SHMEMX_AUTO_PARTIAL");
+    const std::vector<AutoCut> &t = world ? full : partial;
+    int algo = SHMEMX_ALGO_AUTO;
+    for (const AutoCut &c : t)
+        if (bytes >= c.bytes) algo = c.algo;
+    return algo;
+}
+
 int make_plan(int type, int op, int nreduce, int start, int logstride,
                      int size, int pe, int npes, int algo, shmemx_plan_t *p) {
     std::memset(p, 0, sizeof *p);
@@ -334,6 +389,15 @@ int make_plan(int type, int op, int nreduce, int start, int logstride,
     const int sz = (int)type_size(type);
     const long long g = sz >= 16 ? 1 : 16 / sz;  // elements per 16-byte granule
     const bool world = start == 0 && (logstride == 0 || size == 1) && size == npes;
+    if (algo == SHMEMX_ALGO_AUTO && P > 1) {
+        const int t = auto_table_algo(world, n * sz);
+        const bool rccl_ok = world && rccl_native(type, op) && !g_state.ipc_only;
+        const bool pull_ok = node::up() && P <= kMaxFoldInputs;
+        if (((t == SHMEMX_ALGO_RCCL || t == SHMEMX_ALGO_ALLREDUCE) && rccl_ok) ||
+            (t == SHMEMX_ALGO_A2A && !g_state.ipc_only) || (t == SHMEMX_ALGO_DIRECT && pull_ok) ||
+            t == SHMEMX_ALGO_GATHER)
+            algo = t;
+    }
     if (algo == SHMEMX_ALGO_AUTO) {
         if (g_state.ipc_only) algo = SHMEMX_ALGO_DIRECT;
         else if (!(world && rccl_native(type, op))) algo = SHMEMX_ALGO_A2A;

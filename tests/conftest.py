@@ -32,12 +32,29 @@ def pytest_collection_modifyitems(session, config, items):
     (eight compute address spaces); a ninth — the runner, once an in-process
     GPU test has run — puts the hardware scheduler into time-slicing, and the
     8-PE tests then crawl (minutes per case).  The runner never touches the GPU
-    for the multi-process tests, so running them first keeps them at 8."""
-    first = [it for it in items if it.nodeid.startswith("tests/test_gpu_ipc.py")
-             or "test_gpu_ipc.py::" in it.nodeid]
-    if first:
-        rest = [it for it in items if it not in first]
-        items[:] = first + rest
+    for the multi-process tests, so running them first keeps them at 8.
+
+    Within that constraint the BASELINE.json config tests go first, so a run
+    cut short by -x still reaches every config: the multi-process ones
+    (configs[0] at 2 PEs, configs[2]/[4] at 8 PEs, configs[2]/[3] at 4 PEs),
+    then the bench's own N > 1 path, then the rest of the multi-process
+    tests, then the in-process config tests (configs[1] at full size and
+    the configs[3]/[4] shapes on one PE), then everything else."""
+    multi_process = ("test_gpu_ipc.py::", "test_gpu_bench_multi.py::")
+    config_tests = ("test_baseline_config0", "test_ipc_eight_pe_baseline_configs",
+                    "test_ipc_baseline_configs_full_size", "test_gpu_configs.py::",
+                    "test_fold_full_size_double_sum")
+
+    def rank(it):
+        multi = any(k in it.nodeid for k in multi_process)
+        config = any(k in it.nodeid for k in config_tests)
+        if multi:
+            if config:
+                return 0
+            return 1 if "test_gpu_bench_multi.py::" in it.nodeid else 2
+        return 3 if config else 4
+
+    items[:] = sorted(items, key=rank)   # stable: file order within a rank
 
 
 def _ensure_built():

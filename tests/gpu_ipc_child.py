@@ -42,6 +42,7 @@ shm.init()
 assert shm.my_pe() == pe and shm.n_pes() == npes
 fails = []
 ncases = 0
+extra = {}    # scenario-specific report fields
 
 
 def member(start, log, size):
@@ -481,6 +482,37 @@ elif scenario == "soak":
             continue                               # not a valid (set, algo) pair here
         seed += 1
         run_case(t, op, n, st, algo, mode, seed)
+elif scenario == "config0":
+    # BASELINE.json configs[0]: shmem_int_sum_to_all, nreduce = 1024, on 2 PEs
+    # (the reference's "oshrun loopback"), through the C entry point itself
+    # with the reference's pWrk and pSync arguments, on the HIP path.  Sources
+    # are the oracle's (SURVEY §8d seeds, kind 0), so the test runner can hold
+    # every PE's target against oracle_reduce_fork, the fork-per-PE run of the
+    # restated reduce-op.c (the GASNet smp model); here each target is also
+    # compared element for element with the oracle's simulation.
+    n = 1024
+    srcs = oracle.sources("int", 0, npes, n)
+    want = oracle.reduce_sim("int", "sum", srcs, 0, 0, npes)[pe]
+    modes = ("view", "host") if MIRRORED else ("heap", "device", "host")
+    extra["target_hash"] = {}
+    for mode in modes:
+        ncases += 1
+        pwrk = np.zeros(64, np.int32)                   # SHMEM_REDUCE_MIN_WRKDATA_SIZE
+        psync = np.full(128, -1, np.int64)              # SHMEM_REDUCE_SYNC_SIZE x SHMEM_SYNC_VALUE
+        src, _ = place(np.ascontiguousarray(srcs[pe]), mode, HEAP_SRC)
+        tgt, get = place(np.full(n, -7, np.int32), mode, HEAP_TGT)
+        shm.barrier_all()
+        print(f"config0 int sum n={n} mode={mode}", flush=True)
+        shm.to_all("int", "sum", tgt, src, n, 0, 0, npes, pwrk, psync)
+        torch.cuda.synchronize()
+        got = np.ascontiguousarray(get())
+        extra["target_hash"][mode] = oracle.value_hash("int", got)
+        if shm.last_error() or not same_bits(got, want):
+            fails.append(f"config0 mode={mode}: error {shm.last_error()} / wrong result")
+        if not np.all(psync == -1):
+            fails.append(f"config0 mode={mode}: pSync not left at SHMEM_SYNC_VALUE")
+        algo = shm.plan("int", "sum", n, 0, 0, npes, pe, npes, "auto").algo
+        extra.setdefault("algo", {})[mode] = algo
 elif scenario == "configs":
     # BASELINE.json configs at full size through the blocking drop-in entry
     # points, every PE a process: long and/or/xor over 64 Mi elements
@@ -770,4 +802,4 @@ shm.free(HEAP_TGT)
 shm.free(HEAP_SRC)
 shm.finalize()
 with open(out_path, "w") as f:
-    json.dump({"pe": pe, "fails": fails, "ncases": ncases, "fences": fences}, f)
+    json.dump(dict(extra, pe=pe, fails=fails, ncases=ncases, fences=fences), f)

@@ -1,0 +1,108 @@
+"""bench.py's N > 1 path, run the way the driver runs it
+(`python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`),
+with every rank on the box's one GPU: on the default RCCL transport through
+the RCCL test double (tests/native/fake_rccl.cpp), and on the IPC transport.
+
+This is the code the driver's 8-GPU scaling run executes: gloo bootstrap,
+the timed region with its barriers and max over ranks, the correctness guard
+on the whole target (tolerance check + shmemx_verify), every extra (other
+algorithms, config curves, latencies, DIRECT/SIGNAL over the peers' HBM, the
+coherence check, the crossover and partial-set tables, auto_recommendation).
+The numbers are a shared GPU's and are never reported; what is asserted is
+that the line comes out, says correct, and carries no error where the
+transport supports the algorithm.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+
+# algorithms that need an RCCL communicator: refused (ENOTSUP) on the IPC transport
+RCCL_ONLY = ("rccl", "allreduce", "a2a")
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def strings(x, path=""):
+    """(path, text) of every string leaf of a JSON value."""
+    if isinstance(x, dict):
+        for k, v in x.items():
+            yield from strings(v, f"{path}.{k}")
+    elif isinstance(x, list):
+        for i, v in enumerate(x):
+            yield from strings(v, f"{path}[{i}]")
+    elif isinstance(x, str):
+        yield path, x
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport,npes", [("rccl", 2), ("ipc", 2), ("rccl", 8), ("ipc", 8)])
+def test_bench_multi_rank_line(tmp_path, transport, npes):
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env.update(SHMEMX_SHARE_GPU="1", SHMEMX_BARRIER_TIMEOUT="120", PYTHONUNBUFFERED="1")
+    if transport == "ipc":
+        env["SHMEMX_TRANSPORT"] = "ipc"
+    else:
+        env.pop("SHMEMX_TRANSPORT", None)
+        env["FAKE_RCCL"] = os.path.join(HERE, "native", "libfake_rccl.so")
+    if npes > 4:
+        env["GPU_MAX_HW_QUEUES"] = "2"     # 8 processes' queues on one GPU (test_gpu_ipc.py)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={npes}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}",
+           os.path.join(REPO, "bench.py"), "--gpus", str(npes), "--steps", "3", "--warmup", "1",
+           "--nreduce", str(1 << 20), "--extras-max-nreduce", str(1 << 20), "--extras-timeout", "240"]
+    logdir = os.environ.get("GPU_TEST_LOGDIR")
+    err_path = (os.path.join(logdir, f"bench_multi_{transport}_{npes}.err") if logdir
+                else str(tmp_path / "bench.err"))
+    if logdir:
+        os.makedirs(logdir, exist_ok=True)
+    with open(err_path, "w") as err:
+        p = subprocess.run(cmd, env=env, cwd=REPO, stdout=subprocess.PIPE, stderr=err, text=True,
+                           timeout=420, start_new_session=True)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{"metric"')]
+    tail = open(err_path).read()[-3000:]
+    assert p.returncode == 0, f"exit {p.returncode}\n{p.stdout[-2000:]}\n{tail}"
+    assert len(lines) == 1, f"want one JSON line, got {len(lines)}\n{p.stdout[-2000:]}"
+    line = json.loads(lines[0])
+    assert line["correct"] is True
+    assert line["n_gpus"] == npes and line["steps"] == 3 and line["value"] > 0
+    assert line["roofline"]["bound"] == "xgmi" and line["cpu_baseline"] is None
+    extras = line["extras"]
+    assert "note" not in extras, extras.get("note")     # no watchdog, no fatal signal
+    for algo in ("direct", "signal"):
+        c = extras["coherence"][algo]
+        assert isinstance(c, dict) and c["calls"] == 60 and c["mismatched_elements"] == 0, c
+    for k in ("direct_heap", "signal_heap"):
+        assert isinstance(extras[k], dict) and extras[k]["correct"] is True, extras[k]
+    bad = []
+    for path, text in strings(extras):
+        if path.endswith("_note") or path.startswith(".auto_recommendation"):
+            continue     # labels and algorithm names, not outcomes
+        refused = "ENOTSUP" in text and transport == "ipc" and any(
+            f".{a}" in path or f"algo_{a}_" in path for a in RCCL_ONLY)
+        if not refused:
+            bad.append(f"{path}: {text[:160]}")
+    assert not bad, "\n".join(bad[:20])
+    # every timed crossover / partial-set call left exact targets
+    for algo, row in extras["algo_crossover"]["correct"].items():
+        for n, ok in row.items():
+            assert ok is True or (transport == "ipc" and algo in RCCL_ONLY), (algo, n, ok)
+    rec = extras["auto_recommendation"]
+    assert "full" in rec and rec["env"].get("SHMEMX_AUTO_FULL", "").startswith("0:"), rec
+    if npes >= 4:
+        p2 = extras["partial_sets"]
+        for shape in ("first_half_correct", "every_other_correct"):
+            for algo, row in p2[shape].items():
+                for n, ok in row.items():
+                    assert ok is True or (transport == "ipc" and algo in RCCL_ONLY), (shape, algo, n, ok)
+        assert rec["env"].get("SHMEMX_AUTO_PARTIAL", "").startswith("0:"), rec

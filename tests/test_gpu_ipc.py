@@ -110,6 +110,33 @@ def test_ipc_transport_all_pairs_sets_placements(tmp_path, npes, shots):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("transport,heap", [("ipc", "device"), ("ipc", "mirrored"), ("rccl", "device")])
+def test_baseline_config0_int_sum_1024_two_pes(tmp_path, transport, heap):
+    """BASELINE.json configs[0]: shmem_int_sum_to_all, nreduce = 1024, 2 PEs,
+    as 2 PE processes through the C entry point on the HIP path (DIRECT's
+    fused one shot on the IPC transport; RCCL's all-reduce on the RCCL
+    transport, with the RCCL test double), from heap, device and host arrays
+    and, on the mirrored heap, host-written view addresses.  Every PE's
+    target is held bit for bit against oracle_reduce_fork: the restated
+    reduce-op.c run as one forked process per PE over shared segments (the
+    GASNet smp loopback the reference's oshrun uses), on the same sources."""
+    import oracle
+    env = {"SHMEMX_TRANSPORT": transport, "SHMEMX_HEAP_MEMORY": heap}
+    if transport == "rccl":
+        env["FAKE_RCCL"] = os.path.join(HERE, "native", "libfake_rccl.so")
+    npes, n = 2, 1024
+    _, want = oracle.reduce_fork("int", "sum", npes, 0, 0, npes, n, kind=0, reps=1)
+    reports = run_pes(tmp_path, npes, "config0", env, timeout=300)
+    for r in reports:
+        assert not r["fails"], f"PE {r['pe']}: {r['fails']}"
+        modes = ("view", "host") if heap == "mirrored" else ("heap", "device", "host")
+        assert r["ncases"] == len(modes)
+        assert r["target_hash"] == {m: want[r["pe"]] for m in modes}, (r["target_hash"], want)
+        # the GPU path ran: DIRECT's pulls on the IPC transport, RCCL's all-reduce on RCCL
+        assert set(r["algo"].values()) == {"direct" if transport == "ipc" else "allreduce"}, r["algo"]
+
+
+@pytest.mark.gpu
 def test_ipc_eight_pe_baseline_configs(tmp_path):
     """BASELINE.json configs[2] (double sum, 32 Mi, 8 PEs) on DIRECT, SIGNAL
     and own-order GATHER, and configs[4] (float sum sweep 4 Ki .. 256 Mi, 8
