@@ -330,8 +330,11 @@ int shmemx_reduce_plan(int type, int op, int nreduce, int PE_start,
  * mapped on this PE for PE `pe`'s copy — a device pointer a HIP kernel here
  * can load from / store to over xGMI (the shmem_ptr idea, querying/ptr.c).
  * NULL if `addr` is not in the heap segment or the peer is not mapped.  For a
- * mirrored heap's host-view address: `addr` itself for this PE, the peers'
- * HBM copies (device addresses) for the others. */
+ * mirrored heap's host-view address: `addr` itself for this PE, NULL for the
+ * others (a store into a peer's HBM would go behind that peer's host view);
+ * device-side puts take the twin (shmemx_mirror_device_ptr), whose peer
+ * addresses this returns, and the receiver calls shmemx_mirror_invalidate on
+ * the range after the barrier that orders the puts. */
 void *shmemx_heap_ptr(const void *addr, int pe);
 
 /* Mirrored heap (the default; $SHMEMX_HEAP_MEMORY=mirrored): the symmetric
@@ -355,9 +358,16 @@ void *shmemx_heap_ptr(const void *addr, int pe);
  *                             given a view address (write(2) of a result,
  *                             read(2) into a source) fails with EFAULT on a
  *                             block the library has not opened;
- *   shmemx_mirror_stats       out[0..4] = write faults, read faults, blocks
+ *   shmemx_mirror_stats       out[0..5] = write faults, read faults, blocks
  *                             copied to HBM, blocks copied back, blocks marked
- *                             device-newer; returns how many were filled. */
+ *                             device-newer, faults that waited for a
+ *                             collective being enqueued on their block;
+ *                             returns how many were filled.
+ * A host access to a block a collective is writing waits for it (from any
+ * thread), then reads the result; a fetch waits only for the streams that
+ * wrote the view (the caller's stream of a stream-ordered call, not the whole
+ * device), and its HIP work runs on a service thread, never in the SIGSEGV
+ * handler ("Mirrored heap"). */
 void *shmemx_mirror_device_ptr(const void *addr);
 int shmemx_mirror_sync(const void *addr, size_t bytes);
 int shmemx_mirror_invalidate(const void *addr, size_t bytes);

@@ -164,15 +164,14 @@ int broadcast_impl(size_t esize, void *target, const void *source, size_t nelems
     if (!bytes || !collective(si)) return SHMEMX_OK;  // the root's target is never written
     if ((si.m == root_idx && !source) || (si.m != root_idx && !target)) return set_error(SHMEMX_EINVAL);
     hipStream_t s = g_state.stream;
-    // mirrored heap: operands in the host view run on their HBM twins
-    void *const user_target = target;
+    // mirrored heap: operands in the host view run on their HBM twins (a
+    // non-root's target is DEVICE_NEWER from here, heap.h DeviceWrite)
     if (si.m == root_idx) source = heap::device_operand(source, bytes);
-    else target = heap::device_operand(target, bytes);
+    heap::DeviceWrite tw(si.m == root_idx ? nullptr : target, bytes, s);
+    if (si.m != root_idx) target = tw.ptr();
     if (!g_state.comm) {   // IPC transport
-        const int rc = ipc_broadcast(static_cast<char *>(target), static_cast<const char *>(source),
-                                     bytes, root_idx, si.start, si.step, si.P, si.m, s);
-        if (rc == SHMEMX_OK && si.m != root_idx) heap::device_wrote(user_target, bytes);
-        return rc;
+        return ipc_broadcast(static_cast<char *>(target), static_cast<const char *>(source),
+                             bytes, root_idx, si.start, si.step, si.P, si.m, s);
     }
     const int root = si.peer(root_idx);
     const bool is_root = si.m == root_idx;
@@ -199,7 +198,6 @@ int broadcast_impl(size_t esize, void *target, const void *source, size_t nelems
         SHMX_NCCL(ncclGroupEnd());
     }
     finish(out, s);
-    if (!is_root) heap::device_wrote(user_target, bytes);
     return SHMEMX_OK;
 }
 
@@ -222,7 +220,7 @@ int collect_impl(size_t esize, void *target, const void *source, size_t nelems, 
         size_t total = 0;
         const int rc = ipc_collect(static_cast<char *>(target), static_cast<const char *>(source), esize,
                                    nelems, si.start, si.step, si.P, si.m, &total, s);
-        if (rc == SHMEMX_OK && target) heap::device_wrote(user_target, total);
+        if (rc == SHMEMX_OK && target) heap::device_wrote(user_target, total, s);
         trace(LOG_COLLECT, "%s over IPC: %zu bytes mine, %zu in all, set (%d,%d,%d)",
               fixed ? "fcollect" : "collect", nelems * esize, total, start, logstride, size);
         return rc;
@@ -278,7 +276,7 @@ int collect_impl(size_t esize, void *target, const void *source, size_t nelems, 
         }
     }
     finish(out, s);
-    heap::device_wrote(user_target, total);
+    heap::device_wrote(user_target, total, s);
     return SHMEMX_OK;
 }
 
@@ -478,14 +476,16 @@ void *pshmem_realloc(void *ptr, size_t size) {
         // the old contents move on the device (a mirrored heap's host stores
         // go up first, and the new block's host view is refreshed from HBM)
         const size_t keep = old_bytes < size ? old_bytes : size;
-        void *dst = heap::device_operand(p, keep);
         const void *src = heap::device_operand(ptr, keep);
-        // complete before the old block is freed (a device-to-device
-        // hipMemcpy would return before the copy ran); the library stream is
-        // ordered after the legacy default stream, so earlier writes land first
-        SHMX_HIP(hipMemcpyAsync(dst, src, keep, hipMemcpyDefault, g_state.stream));
-        SHMX_HIP(hipStreamSynchronize(g_state.stream));
-        heap::device_wrote(p, keep);
+        {
+            heap::DeviceWrite dst(p, keep, g_state.stream);
+            // complete before the old block is freed (a device-to-device
+            // hipMemcpy would return before the copy ran); the library stream
+            // is ordered after the legacy default stream, so earlier writes
+            // land first
+            SHMX_HIP(hipMemcpyAsync(dst.ptr(), src, keep, hipMemcpyDefault, g_state.stream));
+            SHMX_HIP(hipStreamSynchronize(g_state.stream));
+        }
         heap_free(ptr);
     }
     pshmem_barrier_all();

@@ -511,6 +511,11 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     d.count = (stage_src || stage_tgt ? 1 : 0) | (partial && tgt > src ? 2 : 0) |
               (one_shot && single && fused_oneshot_enabled() && heap::signal_area() ? 4 : 0) |
               (twoshot_size && single && !stage_src && !stage_tgt && heap::signal_area() ? 8 : 0);
+    // aux: the size limits this PE decided with ($SHMEMX_DIRECT_ONESHOT_KB,
+    // $SHMEMX_FUSED_TWOSHOT_KB / shmemx_set_fused_twoshot_kb), in KiB.  They
+    // pick the schedule (one shot or two, fused or not) and with it the
+    // number of barriers, so members that disagree on them must not start it.
+    if (!own_order) d.aux = (uint64_t)(oneshot_bytes() >> 10) << 32 | (uint64_t)(fused_twoshot_bytes() >> 10);
     node::put_desc(d);
     if (single && stage_src)
         SHMX_HIP(hipMemcpyAsync(g_scratch.base, src, bytes, hipMemcpyDeviceToDevice, s));
@@ -519,21 +524,36 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     auto read_descs = [&] {
         for (int i = 0; i < P; ++i) desc[i] = i == m ? d : node::get_desc(pe_of(i));
     };
-    if (one_shot || twoshot_size) {
-        // The descriptors first, with no fence: when every member can, the
-        // whole call is one fused launch (system fence on every XCD, device
-        // barriers, fold (and gather), device barrier — launch_signal_fold)
-        // and one wait, instead of fenced host syncs around each kernel.  All
-        // members see the same descriptors, so all take the same path.
+    if (!own_order) {
+        // The descriptors first, with no fence, on every call whatever its
+        // size (so the barrier sequence never depends on a local setting).
+        // Every member then sees the same descriptors and takes the same
+        // path: a collective ENOTSUP if the members' size limits differ;
+        // when every member can, the whole call is one fused launch (system
+        // fence on every XCD, device barriers, fold (and gather), device
+        // barrier — launch_signal_fold) and one wait, instead of fenced host
+        // syncs around each kernel.
         const double t0 = now_us();
         node::barrier(start, step, P);
         g_phase_us[kEntryBarrier] += now_us() - t0;
         read_descs();
-        const int bit = one_shot ? 4 : 8;
-        bool fuse = true;
-        for (int i = 0; i < P; ++i) fuse &= (desc[i].count & bit) != 0;
-        if (fuse && one_shot) return direct_fused(type, op, tgt, n, start, step, P, desc, stage_tgt, s);
-        if (fuse) return direct_fused2(type, op, tgt, n, start, step, P, m, desc, s);
+        for (int i = 1; i < P; ++i) {
+            if (desc[i].aux != desc[0].aux) {
+                trace(LOG_REDUCTION, "DIRECT: members disagree on SHMEMX_DIRECT_ONESHOT_KB / "
+                      "SHMEMX_FUSED_TWOSHOT_KB (set member %d: %llu/%llu KiB, member 0: %llu/%llu KiB)",
+                      i, (unsigned long long)(desc[i].aux >> 32), (unsigned long long)(desc[i].aux & 0xffffffffu),
+                      (unsigned long long)(desc[0].aux >> 32), (unsigned long long)(desc[0].aux & 0xffffffffu));
+                // nobody reads anyone's operands: the call ends here on every member
+                return set_error(SHMEMX_ENOTSUP);
+            }
+        }
+        if (one_shot || twoshot_size) {
+            const int bit = one_shot ? 4 : 8;
+            bool fuse = true;
+            for (int i = 0; i < P; ++i) fuse &= (desc[i].count & bit) != 0;
+            if (fuse && one_shot) return direct_fused(type, op, tgt, n, start, step, P, desc, stage_tgt, s);
+            if (fuse) return direct_fused2(type, op, tgt, n, start, step, P, m, desc, s);
+        }
         // my source (and its staging) is complete; reduce-op.c:217
         node_sync(start, step, P, s, &g_phase_us[kEntryWait], &g_phase_us[kEntryBarrier]);
     } else {

@@ -33,6 +33,7 @@ constexpr int kSignals[] = {SIGABRT, SIGSEGV, SIGBUS, SIGFPE, SIGILL, SIGTERM};
 constexpr int kNumSignals = sizeof kSignals / sizeof kSignals[0];
 
 struct Note {
+    const Note *older;   // notes are retired, never freed: kept reachable here
     int exit_code;
     size_t len;
     char text[1];
@@ -41,6 +42,7 @@ struct Note {
 struct sigaction g_prev[kNumSignals];
 bool g_installed = false;
 std::atomic<const Note *> g_note{nullptr};
+const Note *g_newest = nullptr;   // every note ever registered, newest first
 std::atomic<int> g_fired{0};
 
 void on_fatal(int sig, siginfo_t *si, void *) {
@@ -66,7 +68,16 @@ void on_fatal(int sig, siginfo_t *si, void *) {
 extern "C" int shmemx_set_fatal_note(const char *text, int exit_code) {
     if (text == nullptr) {
         if (g_installed) {
-            for (int i = 0; i < kNumSignals; ++i) sigaction(kSignals[i], &g_prev[i], nullptr);
+            for (int i = 0; i < kNumSignals; ++i) {
+                // SIGSEGV: a mirrored heap created after the note was
+                // installed chained its handler to ours; what we saved
+                // predates it, so the view's handler goes back in front
+                // (chaining to that saved disposition), not away
+                if (kSignals[i] == SIGSEGV && shmx::mirror::active())
+                    shmx::mirror::install_handler(&g_prev[i]);
+                else
+                    sigaction(kSignals[i], &g_prev[i], nullptr);
+            }
             g_installed = false;
         }
         g_note.store(nullptr, std::memory_order_release);
@@ -75,6 +86,8 @@ extern "C" int shmemx_set_fatal_note(const char *text, int exit_code) {
     const size_t len = strlen(text);
     Note *n = static_cast<Note *>(malloc(sizeof(Note) + len));
     if (!n) return SHMEMX_ENOMEM;
+    n->older = g_newest;
+    g_newest = n;
     n->exit_code = exit_code;
     n->len = len;
     memcpy(n->text, text, len + 1);

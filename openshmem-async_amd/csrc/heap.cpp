@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -94,8 +95,10 @@ struct Heap {
 // regions the first time a copy touches them, and the DMA engines then move
 // blocks straight between HBM and its pages; a region HIP refuses to lock
 // goes through a page-locked bounce buffer instead (CPU copy of one half
-// overlapping the DMA of the other).  A fetch first waits for all device
-// work: the collective that wrote the block may run on any stream.
+// overlapping the DMA of the other).  A fetch first waits for the streams
+// that wrote the view's blocks (the writers below), then copies on a stream
+// of its own, so it never queues behind unrelated work on the library's or
+// the caller's streams.
 constexpr size_t kMirRegion = size_t(256) << 20;
 constexpr size_t kMirStage = size_t(8) << 20;
 struct MirStage {
@@ -103,8 +106,67 @@ struct MirStage {
     hipEvent_t done[2] = {nullptr, nullptr};
     bool used[2] = {false, false};
     int next = 0;
+    hipStream_t fetch = nullptr;   // the fetches' own stream (non-blocking)
     std::vector<uint8_t> region;   // 0 untried, 1 page-locked, 2 refused
 } g_mst;
+
+// The streams collectives on view operands ran on, each with an event
+// recorded after its last such collective.  A fetch waits for the armed
+// ones (and for the whole device after shmemx_mirror_invalidate, whose
+// writers the library never saw).  Guarded by g_wmu: the fault service
+// thread fetches while the caller's thread may be recording.
+struct Writer {
+    hipStream_t stream;
+    hipEvent_t done;
+    bool armed;
+};
+std::mutex g_wmu;
+std::vector<Writer> g_writers;
+bool g_sync_device = false;
+
+void record_writer(void *stream) {
+    std::lock_guard<std::mutex> lk(g_wmu);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (!s || (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)) {
+        // unknown writers, or work captured into a graph that runs later:
+        // the next fetch waits for the device (a replayed graph's writes to
+        // the view need shmemx_mirror_invalidate afterwards)
+        g_sync_device = true;
+        return;
+    }
+    for (Writer &w : g_writers) {
+        if (w.stream == s) {
+            SHMX_HIP(hipEventRecord(w.done, s));
+            w.armed = true;
+            return;
+        }
+    }
+    Writer w{s, nullptr, true};
+    SHMX_HIP(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
+    SHMX_HIP(hipEventRecord(w.done, s));
+    g_writers.push_back(w);
+}
+
+void wait_writers() {
+    std::lock_guard<std::mutex> lk(g_wmu);
+    if (g_sync_device) {
+        SHMX_HIP(hipDeviceSynchronize());
+        g_sync_device = false;
+        for (Writer &w : g_writers) w.armed = false;
+        return;
+    }
+    for (Writer &w : g_writers) {
+        if (!w.armed) continue;
+        SHMX_HIP(hipEventSynchronize(w.done));
+        w.armed = false;
+    }
+}
+
+hipStream_t mir_fetch_stream() {
+    if (!g_mst.fetch) SHMX_HIP(hipStreamCreateWithFlags(&g_mst.fetch, hipStreamNonBlocking));
+    return g_mst.fetch;
+}
 
 void mir_stage_ready() {
     if (g_mst.buf) return;
@@ -165,22 +227,27 @@ void mir_to_device(uint64_t off, size_t bytes, void *) {
 }
 
 void mir_to_host(uint64_t off, size_t bytes, void *) {
-    SHMX_HIP(hipDeviceSynchronize());
-    mir_by_region(off, bytes, [](uint64_t o, size_t len, bool locked) {
+    wait_writers();
+    const hipStream_t fs = mir_fetch_stream();
+    mir_by_region(off, bytes, [fs](uint64_t o, size_t len, bool locked) {
         char *dst = mirror::alias_base() + o;
         if (locked) {
-            SHMX_HIP(hipMemcpy(dst, g_heap.base + o, len, hipMemcpyDeviceToHost));
+            SHMX_HIP(hipMemcpyAsync(dst, g_heap.base + o, len, hipMemcpyDeviceToHost, fs));
+            SHMX_HIP(hipStreamSynchronize(fs));
             return;
         }
         mir_stage_ready();
         // halves in turn: the DMA of chunk k + 1 overlaps the CPU copy of chunk k
         const size_t half = kMirStage / 2;
         const size_t nchunks = (len + half - 1) / half;
+        // the to_device half of the ring may still be in flight
+        for (int h = 0; h < 2; ++h)
+            if (g_mst.used[h]) SHMX_HIP(hipEventSynchronize(g_mst.done[h]));
         auto dma = [&](size_t k) {
             const size_t n = std::min(half, len - k * half);
             SHMX_HIP(hipMemcpyAsync(g_mst.buf + (k & 1) * half, g_heap.base + o + k * half, n,
-                                    hipMemcpyDeviceToHost, g_state.stream));
-            SHMX_HIP(hipEventRecord(g_mst.done[k & 1], g_state.stream));
+                                    hipMemcpyDeviceToHost, fs));
+            SHMX_HIP(hipEventRecord(g_mst.done[k & 1], fs));
         };
         dma(0);
         for (size_t k = 0; k < nchunks; ++k) {
@@ -357,8 +424,31 @@ void *device_operand_open(const void *p) {
     return g_heap.base + off;
 }
 
-void device_wrote(const void *p, size_t bytes) {
-    if (bytes && in_view(p)) mirror::device_wrote((uint64_t)(static_cast<const char *>(p) - g_heap.view), bytes);
+void device_wrote(const void *p, size_t bytes, void *stream) {
+    if (!bytes || !in_view(p)) return;
+    record_writer(stream);
+    mirror::device_wrote((uint64_t)(static_cast<const char *>(p) - g_heap.view), bytes);
+}
+
+void *twin(const void *p) {
+    return in_view(p) ? g_heap.base + (static_cast<const char *>(p) - g_heap.view) : const_cast<void *>(p);
+}
+
+DeviceWrite::DeviceWrite(void *p, size_t bytes, void *stream)
+    : dev_(p), stream_(stream), open_(false) {
+    if (!bytes || !in_view(p) ||
+        bytes > g_heap.arena.capacity() - (uint64_t)(static_cast<const char *>(p) - g_heap.view))
+        return;
+    const uint64_t off = (uint64_t)(static_cast<const char *>(p) - g_heap.view);
+    mirror::begin_device_write(off, bytes);
+    dev_ = g_heap.base + off;
+    open_ = true;
+}
+
+DeviceWrite::~DeviceWrite() {
+    if (!open_) return;
+    record_writer(stream_);
+    mirror::end_device_write();
 }
 
 bool host_acquire(const void *p, size_t bytes, bool write) {
@@ -389,7 +479,14 @@ void release_all() {
         (void)hipHostFree(g_mst.buf);
         for (hipEvent_t e : g_mst.done) (void)hipEventDestroy(e);
     }
+    if (g_mst.fetch) (void)hipStreamDestroy(g_mst.fetch);
     g_mst = MirStage{};
+    {
+        std::lock_guard<std::mutex> lk(g_wmu);
+        for (Writer &w : g_writers) (void)hipEventDestroy(w.done);
+        g_writers.clear();
+        g_sync_device = false;
+    }
     for (auto &kv : g_heap.priv) (void)priv_free(kv.second.base);
     if (g_heap.base) {
         node::unpublish(node::kHeap);

@@ -74,8 +74,34 @@ void *device_operand(const void *p, size_t bytes);
 // every host store from p to the end of the view goes to HBM.
 void *device_operand_open(const void *p);
 // After a collective wrote [p, p + bytes) (a host-view address) in HBM: the
-// host view of it is stale until the next host access fetches it.
-void device_wrote(const void *p, size_t bytes);
+// host view of it is stale until the next host access fetches it, which
+// first waits for `stream` (the stream the collective ran on) — or, for
+// nullptr (shmemx_mirror_invalidate: writes on streams the library never
+// saw), for the whole device.
+void device_wrote(const void *p, size_t bytes, void *stream);
+// A collective that writes [p, p + bytes): construct it before the
+// collective is enqueued and let it go after.  For a host-view target the
+// constructor flushes the host's stores, marks the blocks DEVICE_NEWER and
+// opens a write in flight (host accesses to them wait, mirror.h); the
+// destructor records `stream` as their writer (a fetch waits for what was
+// enqueued on it) and closes the write.  ptr() is the address to write: the
+// HBM twin of a host-view address, p itself otherwise.
+class DeviceWrite {
+  public:
+    DeviceWrite(void *p, size_t bytes, void *stream);
+    ~DeviceWrite();
+    DeviceWrite(const DeviceWrite &) = delete;
+    DeviceWrite &operator=(const DeviceWrite &) = delete;
+    void *ptr() const { return dev_; }
+
+  private:
+    void *dev_;
+    void *stream_;
+    bool open_;
+};
+// The HBM twin of a host-view address (p itself otherwise), with no change
+// of block state.
+void *twin(const void *p);
 // shmemx_mirror_acquire: [p, p + bytes) of the view made current (and, with
 // `write`, writable) for host code that cannot take a page fault; false if
 // the range is not in the view.

@@ -2,11 +2,16 @@
 // fault handler (mirror.h).  Host-only: the copies go through a Backend.
 #include "mirror.h"
 
+#include <linux/futex.h>
+#include <pthread.h>
+#include <sched.h>
 #include <sys/mman.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
+#include <climits>
 #include <cstring>
 
 namespace shmx {
@@ -34,6 +39,39 @@ std::atomic_flag g_lock = ATOMIC_FLAG_INIT;
 struct sigaction g_prev_segv;
 bool g_installed = false;
 
+// Device writes in flight (begin_device_write .. end_device_write): a fault
+// on a DEVICE_NEWER block waits for zero before it fetches.
+std::atomic<int> g_pending{0};
+
+// The fault service: one request slot, because the handler holds the lock
+// while it waits.  kIdle -> kAsked (handler) -> kDone (service) -> kIdle.
+enum { kIdle = 0, kAsked = 1, kDone = 2, kStop = 3 };
+std::atomic<int> g_req{kIdle};
+size_t g_req_b0 = 0, g_req_nb = 0;
+pthread_t g_service;
+bool g_service_up = false;
+
+void futex_wait(std::atomic<int> *a, int v) {
+    syscall(SYS_futex, reinterpret_cast<int *>(a), FUTEX_WAIT_PRIVATE, v, nullptr, nullptr, 0);
+}
+void futex_wake(std::atomic<int> *a) {
+    syscall(SYS_futex, reinterpret_cast<int *>(a), FUTEX_WAKE_PRIVATE, INT_MAX, nullptr, nullptr, 0);
+}
+
+void *service_main(void *) {
+    for (;;) {
+        const int r = g_req.load(std::memory_order_acquire);
+        if (r == kStop) return nullptr;
+        if (r != kAsked) {
+            futex_wait(&g_req, r);
+            continue;
+        }
+        g_view.be.to_host((uint64_t)g_req_b0 * kBlock, g_req_nb * kBlock, g_view.be.ctx);
+        g_req.store(kDone, std::memory_order_release);
+        futex_wake(&g_req);
+    }
+}
+
 struct Guard {
     Guard() {
         while (g_lock.test_and_set(std::memory_order_acquire)) {
@@ -50,8 +88,19 @@ size_t block_of(uint64_t off) { return (size_t)(off / kBlock); }
 
 // Blocks [b0, b0 + nb) of the device segment -> host view (through the
 // alias: the view stays inaccessible until the bytes are there), then CLEAN.
-void fetch_run(size_t b0, size_t nb) {
-    g_view.be.to_host((uint64_t)b0 * kBlock, nb * kBlock, g_view.be.ctx);
+// From the fault handler the copy runs on the service thread (the handler
+// only stores, loads and sleeps on a futex); elsewhere in the caller's.
+void fetch_run(size_t b0, size_t nb, bool in_handler) {
+    if (in_handler && g_service_up && !pthread_equal(pthread_self(), g_service)) {
+        g_req_b0 = b0;
+        g_req_nb = nb;
+        g_req.store(kAsked, std::memory_order_release);
+        futex_wake(&g_req);
+        for (int r; (r = g_req.load(std::memory_order_acquire)) != kDone;) futex_wait(&g_req, r);
+        g_req.store(kIdle, std::memory_order_relaxed);
+    } else {
+        g_view.be.to_host((uint64_t)b0 * kBlock, nb * kBlock, g_view.be.ctx);
+    }
     protect(b0, nb, PROT_READ);
     std::memset(g_view.state + b0, CLEAN, nb);
     g_view.st.blocks_fetched += nb;
@@ -104,6 +153,9 @@ bool create(size_t bytes, const Backend &be) {
     g_view.run_end = g_view.fetch_end = ~size_t(0);
     g_view.run_len = g_view.fetch_len = 0;
     g_view.st = Stats{};
+    g_pending.store(0);
+    g_req.store(kIdle);
+    g_service_up = pthread_create(&g_service, nullptr, service_main, nullptr) == 0;
     if (!g_installed) {
         struct sigaction sa;
         std::memset(&sa, 0, sizeof sa);
@@ -116,8 +168,34 @@ bool create(size_t bytes, const Backend &be) {
     return true;
 }
 
+void install_handler(const struct sigaction *prev) {
+    if (!g_view.base) {
+        if (prev) sigaction(SIGSEGV, prev, nullptr);
+        return;
+    }
+    if (prev && (prev->sa_flags & SA_SIGINFO) && prev->sa_sigaction == on_segv) {
+        sigaction(SIGSEGV, prev, nullptr);    // ours, with its own chain
+    } else {
+        struct sigaction sa;
+        std::memset(&sa, 0, sizeof sa);
+        sa.sa_sigaction = on_segv;
+        sa.sa_flags = SA_SIGINFO | SA_NODEFER;
+        sigemptyset(&sa.sa_mask);
+        sigaction(SIGSEGV, &sa, nullptr);
+        if (prev) g_prev_segv = *prev;
+        else std::memset(&g_prev_segv, 0, sizeof g_prev_segv);   // SIG_DFL
+    }
+    g_installed = true;
+}
+
 void destroy() {
     if (!g_view.base) return;
+    if (g_service_up) {
+        g_req.store(kStop, std::memory_order_release);
+        futex_wake(&g_req);
+        pthread_join(g_service, nullptr);
+        g_service_up = false;
+    }
     if (g_installed) {
         // put back what was there before, unless someone installed a handler
         // over ours since (it chains to ours, which then finds no view)
@@ -146,9 +224,10 @@ bool contains(const void *p, size_t bytes) {
 
 uint64_t offset_of(const void *p) { return (uint64_t)(static_cast<const char *>(p) - g_view.base); }
 
-size_t flush(uint64_t off, size_t bytes) {
-    if (!g_view.base || !bytes) return 0;
-    Guard g;
+namespace {
+
+// flush() with the lock held
+size_t flush_locked(uint64_t off, size_t bytes) {
     const size_t b0 = block_of(off), b1 = block_of(off + bytes - 1) + 1;
     size_t copied = 0;
     for (size_t b = b0; b < b1 && b < g_view.nblocks;) {
@@ -158,10 +237,12 @@ size_t flush(uint64_t off, size_t bytes) {
         }
         size_t e = b;
         while (e < b1 && e < g_view.nblocks && g_view.state[e] == HOST_NEWER) ++e;
-        g_view.be.to_device((uint64_t)b * kBlock, (e - b) * kBlock, g_view.be.ctx);
-        // read-only again: the next host store faults and marks it
+        // read-only first, then CLEAN, then the copy: a store another thread
+        // makes from here faults, waits for the lock, and finds the block
+        // CLEAN (HOST_NEWER again, flushed by the next collective)
         protect(b, e - b, PROT_READ);
         std::memset(g_view.state + b, CLEAN, e - b);
+        g_view.be.to_device((uint64_t)b * kBlock, (e - b) * kBlock, g_view.be.ctx);
         copied += e - b;
         b = e;
     }
@@ -171,10 +252,8 @@ size_t flush(uint64_t off, size_t bytes) {
     return copied;
 }
 
-size_t device_wrote(uint64_t off, size_t bytes) {
-    if (!g_view.base || !bytes) return 0;
-    Guard g;
-    const size_t b0 = block_of(off), b1 = std::min(block_of(off + bytes - 1) + 1, g_view.nblocks);
+// Blocks [b0, b1) become DEVICE_NEWER (no host access), lock held.
+size_t mark_device_newer(size_t b0, size_t b1) {
     size_t n = 0;
     for (size_t b = b0; b < b1;) {
         if (g_view.state[b] == DEVICE_NEWER) {
@@ -183,7 +262,6 @@ size_t device_wrote(uint64_t off, size_t bytes) {
         }
         size_t e = b;
         while (e < b1 && g_view.state[e] != DEVICE_NEWER) ++e;
-        // HOST_NEWER here would lose host stores: flush() runs first
         protect(b, e - b, PROT_NONE);
         std::memset(g_view.state + b, DEVICE_NEWER, e - b);
         n += e - b;
@@ -191,6 +269,36 @@ size_t device_wrote(uint64_t off, size_t bytes) {
     }
     g_view.st.blocks_device_newer += n;
     return n;
+}
+
+}  // namespace
+
+size_t flush(uint64_t off, size_t bytes) {
+    if (!g_view.base || !bytes) return 0;
+    Guard g;
+    return flush_locked(off, bytes);
+}
+
+size_t begin_device_write(uint64_t off, size_t bytes) {
+    if (!g_view.base || !bytes) return 0;
+    Guard g;
+    flush_locked(off, bytes);
+    const size_t b0 = block_of(off), b1 = std::min(block_of(off + bytes - 1) + 1, g_view.nblocks);
+    const size_t n = mark_device_newer(b0, b1);
+    g_pending.fetch_add(1, std::memory_order_acq_rel);
+    return n;
+}
+
+void end_device_write() {
+    if (g_pending.load(std::memory_order_acquire) > 0) g_pending.fetch_sub(1, std::memory_order_acq_rel);
+}
+
+size_t device_wrote(uint64_t off, size_t bytes) {
+    if (!g_view.base || !bytes) return 0;
+    Guard g;
+    // HOST_NEWER here would lose host stores: flush() runs first
+    const size_t b0 = block_of(off), b1 = std::min(block_of(off + bytes - 1) + 1, g_view.nblocks);
+    return mark_device_newer(b0, b1);
 }
 
 size_t acquire(uint64_t off, size_t bytes, bool write) {
@@ -202,7 +310,7 @@ size_t acquire(uint64_t off, size_t bytes, bool write) {
         size_t e = b;
         while (e < b1 && g_view.state[e] == g_view.state[b]) ++e;
         if (g_view.state[b] == DEVICE_NEWER) {
-            fetch_run(b, e - b);
+            fetch_run(b, e - b, false);
             fetched += e - b;
         }
         if (write && g_view.state[b] == CLEAN) {
@@ -224,47 +332,60 @@ void fetch_all() {
         }
         size_t e = b;
         while (e < g_view.nblocks && g_view.state[e] == DEVICE_NEWER) ++e;
-        fetch_run(b, e - b);
+        fetch_run(b, e - b, false);
         b = e;
     }
 }
 
 bool handle_fault(void *addr) {
     if (!contains(addr, 1)) return false;
-    Guard g;
-    const size_t b = block_of(offset_of(addr));
-    switch (g_view.state[b]) {
-    case DEVICE_NEWER: {
-        // a load or a store of a block a collective wrote: bring it (and the
-        // DEVICE_NEWER blocks right after it) back; a store faults once more
-        size_t want = 1;
-        if (b == g_view.fetch_end) want = std::min(kMaxFetchRun, 2 * g_view.fetch_len);
-        size_t e = b;
-        while (e < g_view.nblocks && e - b < want && g_view.state[e] == DEVICE_NEWER) ++e;
-        fetch_run(b, e - b);
-        g_view.fetch_end = e;
-        g_view.fetch_len = e - b;
-        g_view.st.read_faults += 1;
-        return true;
-    }
-    case CLEAN: {
-        // a store (CLEAN pages are readable): host newer from here; a
-        // sequential writer gets runs that double up to kMaxWriteRun
-        size_t want = 1;
-        if (b == g_view.run_end) want = std::min(kMaxWriteRun, 2 * g_view.run_len);
-        size_t e = b;
-        while (e < g_view.nblocks && e - b < want && g_view.state[e] == CLEAN) ++e;
-        protect(b, e - b, PROT_READ | PROT_WRITE);
-        std::memset(g_view.state + b, HOST_NEWER, e - b);
-        g_view.run_end = e;
-        g_view.run_len = e - b;
-        g_view.st.write_faults += 1;
-        return true;
-    }
-    default:
-        // already HOST_NEWER (another thread resolved it first)
-        protect(b, 1, PROT_READ | PROT_WRITE);
-        return true;
+    bool waited = false;
+    for (;; sched_yield()) {      // the lock is not held across the yield
+        Guard g;
+        const size_t b = block_of(offset_of(addr));
+        switch (g_view.state[b]) {
+        case DEVICE_NEWER: {
+            if (g_pending.load(std::memory_order_acquire) > 0) {
+                // a collective is being enqueued on blocks of the view: its
+                // result is not recorded yet, so fetching now would read
+                // the old bytes; retry once the write in flight has ended
+                waited = true;
+                continue;
+            }
+            // a load or a store of a block a collective wrote: bring it (and
+            // the DEVICE_NEWER blocks right after it) back; a store faults
+            // once more
+            size_t want = 1;
+            if (b == g_view.fetch_end) want = std::min(kMaxFetchRun, 2 * g_view.fetch_len);
+            size_t e = b;
+            while (e < g_view.nblocks && e - b < want && g_view.state[e] == DEVICE_NEWER) ++e;
+            fetch_run(b, e - b, true);
+            g_view.fetch_end = e;
+            g_view.fetch_len = e - b;
+            g_view.st.read_faults += 1;
+            g_view.st.fault_waits += waited ? 1 : 0;
+            return true;
+        }
+        case CLEAN: {
+            // a store (CLEAN pages are readable): host newer from here; a
+            // sequential writer gets runs that double up to kMaxWriteRun
+            size_t want = 1;
+            if (b == g_view.run_end) want = std::min(kMaxWriteRun, 2 * g_view.run_len);
+            size_t e = b;
+            while (e < g_view.nblocks && e - b < want && g_view.state[e] == CLEAN) ++e;
+            protect(b, e - b, PROT_READ | PROT_WRITE);
+            std::memset(g_view.state + b, HOST_NEWER, e - b);
+            g_view.run_end = e;
+            g_view.run_len = e - b;
+            g_view.st.write_faults += 1;
+            g_view.st.fault_waits += waited ? 1 : 0;
+            return true;
+        }
+        default:
+            // already HOST_NEWER (another thread resolved it first)
+            protect(b, 1, PROT_READ | PROT_WRITE);
+            return true;
+        }
     }
 }
 

@@ -56,8 +56,10 @@ enum State : uint8_t { CLEAN = 0, HOST_NEWER = 1, DEVICE_NEWER = 2 };
 struct Backend {
     // alias [off, off + bytes) -> device segment at offset off
     void (*to_device)(uint64_t off, size_t bytes, void *ctx);
-    // device segment at offset off -> alias (all device work that may have
-    // written it must be complete before the copy)
+    // device segment at offset off -> alias (it first waits for the device
+    // work that may have written it: every write ended by end_device_write
+    // or marked by device_wrote).  Called from an ordinary thread context
+    // (the caller's, or the fault service thread's), never a signal handler.
     void (*to_host)(uint64_t off, size_t bytes, void *ctx);
     // every to_device issued so far has landed
     void (*drain)(void *ctx);
@@ -65,14 +67,24 @@ struct Backend {
 };
 
 // Reserve a host view of `bytes` (rounded up to kBlock) and its alias, every
-// block CLEAN (the device segment must hold the same bytes: zero), and
-// install the SIGSEGV handler.  false on failure.
+// block CLEAN (the device segment must hold the same bytes: zero), install
+// the SIGSEGV handler and start the fault service thread.  false on failure.
+//
+// The fault handler itself makes no backend (HIP) call: those are not
+// async-signal-safe, and the faulting thread may be anywhere.  A fault that
+// needs bytes from the device hands the run to the service thread (one
+// request slot, futex wake-ups) and waits for it with plain atomics; the
+// service thread runs Backend::to_host in an ordinary thread context.
 bool create(size_t bytes, const Backend &be);
 void destroy();
 bool active();
 char *host_base();
 char *alias_base();
 size_t view_bytes();
+// (Re)install the view's SIGSEGV handler, chaining to `prev` for faults
+// outside the view (shmemx_set_fatal_note(NULL) restores its own saved
+// disposition, which may predate the view).
+void install_handler(const struct sigaction *prev);
 
 // Is [p, p + bytes) inside the host view?  Offset of p.
 bool contains(const void *p, size_t bytes);
@@ -80,10 +92,26 @@ uint64_t offset_of(const void *p);
 
 // Before a collective reads or writes [off, off + bytes) of the device
 // segment: copy every HOST_NEWER block that overlaps it to the device (whole
-// blocks), mark them CLEAN, and drain.  Returns the blocks copied.
+// blocks), mark them CLEAN, and drain.  Each run is made read-only BEFORE its
+// copy, so a store another thread makes meanwhile faults, waits for the lock
+// and marks the block HOST_NEWER again (it is not lost).  Returns the blocks
+// copied.
 size_t flush(uint64_t off, size_t bytes);
-// After a collective wrote [off, off + bytes) in HBM: the overlapped blocks
-// become DEVICE_NEWER (call flush on the range first).  Returns the blocks.
+// Before a collective WRITES [off, off + bytes): flush the overlapped
+// HOST_NEWER blocks, then mark every overlapped block DEVICE_NEWER (no host
+// access) and count one device write in flight, all under the lock.  A host
+// access to any of those blocks — the target itself, or a neighbouring
+// object in the same block, from any thread — waits until every write in
+// flight has ended (end_device_write), then fetches the block, whose bytes
+// are then the collective's.  Returns the blocks marked.
+size_t begin_device_write(uint64_t off, size_t bytes);
+// The write begun last is enqueued and its completion is recorded where
+// Backend::to_host waits for it.
+void end_device_write();
+// After a collective wrote [off, off + bytes) in HBM without
+// begin_device_write (a collect target, whose length is known only after
+// the exchange): the overlapped blocks become DEVICE_NEWER (call flush on the
+// range first).  Returns the blocks.
 size_t device_wrote(uint64_t off, size_t bytes);
 // Make [off, off + bytes) accessible to host code that cannot take the page
 // fault — system calls (write(2) of a result, read(2) into a source), other
@@ -102,6 +130,7 @@ bool handle_fault(void *addr);
 
 struct Stats {
     uint64_t write_faults, read_faults, blocks_flushed, blocks_fetched, blocks_device_newer;
+    uint64_t fault_waits;   // faults that waited for a device write in flight
 };
 Stats stats(bool reset);
 State state_of(uint64_t off);   // tests

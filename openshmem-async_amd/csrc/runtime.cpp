@@ -753,21 +753,20 @@ int reduce_on_stream(int type, int op, void *target, const void *source,
     // Operands in the mirrored heap's host view: the host's stores go to HBM
     // now (host-synchronous), and the call runs on the HBM twins.
     const size_t bytes = op_valid(type, op) && nreduce > 0 ? type_size(type) * (size_t)nreduce : 0;
-    void *t = bytes ? heap::device_operand(target, bytes) : target;
     const void *src = bytes ? heap::device_operand(source, bytes) : source;
     // the stream-ordered form takes device memory only (RCCL and the kernels
     // dereference it); host arrays go through the blocking entry points
-    if (nreduce > 0 && (!device_accessible(t) || !device_accessible(src)))
+    if (nreduce > 0 && (!device_accessible(heap::twin(target)) || !device_accessible(src)))
         return set_error(SHMEMX_EINVAL);
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : g_state.stream;
     if (nreduce >= 0 && op_valid(type, op))
         trace_reference_overlap(target, source, type_size(type) * (size_t)nreduce);
-    const int rc = reduce_device(type, op, t, src, nreduce, start, logstride, size,
-                                 algo == SHMEMX_ALGO_AUTO ? g_state.algo : algo, s);
-    // the host view of the target is stale from here; a host access waits
-    // for the device (mirror fetches synchronise it) and reads the result
-    if (rc == SHMEMX_OK && t != target) heap::device_wrote(target, bytes);
-    return rc;
+    // the host view of the target is stale from here: a host access to its
+    // blocks waits until the call is enqueued, then for `s` (the writer), and
+    // reads the result
+    heap::DeviceWrite t(target, bytes, s);
+    return reduce_device(type, op, t.ptr(), src, nreduce, start, logstride, size,
+                         algo == SHMEMX_ALGO_AUTO ? g_state.algo : algo, s);
 }
 
 }  // namespace shmx
@@ -859,10 +858,15 @@ void *shmemx_heap_ptr(const void *addr, int pe) {
     std::lock_guard<std::recursive_mutex> lk(g_mu);
     if (!g_state.inited || pe < 0 || pe >= g_state.npes) return nullptr;
     uint64_t off = 0;
-    if (pe == g_state.pe && heap::view_offset(addr, &off)) return const_cast<void *>(addr);
-    // a host-view address of the mirrored heap names the same offset in the
-    // peers' HBM segments (device addresses, for kernels)
-    if (!heap::offset_of(addr, 1, &off) && !heap::view_offset(addr, &off)) return nullptr;
+    // A host-view address of the mirrored heap: itself for this PE, NULL for
+    // a peer (as the reference's shmem_ptr).  A store through a peer's HBM
+    // address would change HBM behind that peer's view, which would go on
+    // serving (and later flush over it) its stale copy.  Device-side puts take
+    // the twin (shmemx_mirror_device_ptr), whose peers' addresses this
+    // returns, and the receiving PE calls shmemx_mirror_invalidate after the
+    // barrier.
+    if (heap::view_offset(addr, &off)) return pe == g_state.pe ? const_cast<void *>(addr) : nullptr;
+    if (!heap::offset_of(addr, 1, &off)) return nullptr;
     if (pe == g_state.pe) return const_cast<void *>(addr);
     char *b = node::peer_base(node::kHeap, pe);
     return b ? b + off : nullptr;
@@ -872,9 +876,9 @@ int shmemx_mirror_stats(unsigned long long *out, int nout, int reset) {
     std::lock_guard<std::recursive_mutex> lk(g_mu);
     if (!out || nout < 0) return set_error(SHMEMX_EINVAL);
     const mirror::Stats st = mirror::stats(reset != 0);
-    const unsigned long long all[5] = {st.write_faults, st.read_faults, st.blocks_flushed,
-                                       st.blocks_fetched, st.blocks_device_newer};
-    const int k = nout < 5 ? nout : 5;
+    const unsigned long long all[6] = {st.write_faults, st.read_faults, st.blocks_flushed,
+                                       st.blocks_fetched, st.blocks_device_newer, st.fault_waits};
+    const int k = nout < 6 ? nout : 6;
     for (int i = 0; i < k; ++i) out[i] = all[i];
     return k;
 }
@@ -899,7 +903,7 @@ int shmemx_mirror_invalidate(const void *addr, size_t bytes) {
     uint64_t off = 0;
     if (!heap::view_offset(addr, &off)) return set_error(SHMEMX_EINVAL);
     (void)heap::device_operand(addr, bytes);   // host stores first: they are not lost
-    heap::device_wrote(addr, bytes);
+    heap::device_wrote(addr, bytes, nullptr);  // writers unknown: the next fetch waits for the device
     return SHMEMX_OK;
 }
 

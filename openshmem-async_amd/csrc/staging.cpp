@@ -187,16 +187,14 @@ void reduce_blocking(int type, int op, void *target, const void *source,
     const size_t sz = type_size(type);
     if (nreduce > 0 && sz && target && source && op_valid(type, op)) {
         const size_t bytes = sz * (size_t)nreduce;
-        void *t = heap::device_operand(target, bytes);
-        const void *s = heap::device_operand(source, bytes);
-        if (t != target || s != source) {
-            shmemx_plan_t p;
-            const bool member = make_plan(type, op, nreduce, start, logstride, size, g_state.pe,
-                                          g_state.npes, g_state.algo, &p) == SHMEMX_OK;
+        if (heap::twin(target) != target || heap::twin(source) != source) {
+            const void *s = heap::device_operand(source, bytes);
             trace_reference_overlap(target, source, bytes);   // the caller's addresses
-            reduce_blocking_impl(type, op, t, s, nreduce, start, logstride, size, false);
-            if (member && t != target && shmemx_reduce_last_error() == SHMEMX_OK)
-                heap::device_wrote(target, bytes);
+            // blocks of a host-view target: DEVICE_NEWER from before the call
+            // (host accesses wait for it); the blocking call completes on the
+            // library stream, its recorded writer
+            heap::DeviceWrite t(target, bytes, g_state.stream);
+            reduce_blocking_impl(type, op, t.ptr(), s, nreduce, start, logstride, size, false);
             return;
         }
     }

@@ -384,7 +384,7 @@ def direct_stats(reset: bool = True) -> dict:
 
 
 MIRROR_STATS = ("write_faults", "read_faults", "blocks_flushed", "blocks_fetched",
-                "blocks_device_newer")
+                "blocks_device_newer", "fault_waits")
 
 
 def mirror_stats(reset: bool = False) -> dict:

@@ -70,10 +70,30 @@ def expected(t, op, srcs, st, algo):
     return ref[start] if algo != "gather" else ref[pe]
 
 
+def twin(p):
+    """The address the test's own HIP copies use for heap pointer p: on a
+    mirrored heap the host-view address's HBM twin (view addresses never go
+    to HIP, mirror.h), p itself otherwise.  The collectives still get p."""
+    return shm.mirror_device_ptr(p) if MIRRORED else p
+
+
+def heap_write(p, src, nbytes):
+    """Fill heap bytes [p, p + nbytes) with a HIP copy.  Mirrored heap: the
+    host's stores around them go up first (shmemx_mirror_sync), then the copy
+    into the twin, then the view learns its blocks changed on the device
+    (shmemx_mirror_invalidate), as INTEGRATION.md prescribes for the caller's
+    own device writes."""
+    if MIRRORED:
+        shm.mirror_sync(p, nbytes)
+    shm.memcpy(twin(p), src, nbytes)
+    if MIRRORED:
+        shm.mirror_invalidate(p, nbytes)
+
+
 def read(ptr, t, n):
     a = np.empty(n, oracle.NP_DTYPE[t])
     if n:
-        shm.memcpy(a, ptr, a.nbytes)
+        shm.memcpy(a, twin(ptr), a.nbytes)
     return a
 
 
@@ -124,9 +144,9 @@ def run_case(t, op, n, st, algo, mode, seed):
         else:  # "overlap": target = source + 3 elements (partial overlap)
             tgt_p = src_p + 3 * sz
         if n:
-            shm.memcpy(src_p, mine, mine.nbytes)
+            heap_write(src_p, mine, mine.nbytes)
         if mode in ("heap", "heapoff") and n:
-            shm.memcpy(tgt_p, np.full(mine.nbytes, 0xAB, np.uint8), mine.nbytes)
+            heap_write(tgt_p, np.full(mine.nbytes, 0xAB, np.uint8), mine.nbytes)
         shm.reduce_on_stream(t, op, tgt_p, src_p, n, *st, algo)
         torch.cuda.synchronize()
         got = read(tgt_p, t, n)
@@ -162,14 +182,14 @@ def place(arr, mode, heap_ptr):
         torch.cuda.synchronize()
         return t, lambda: t.cpu().numpy()
     if arr.nbytes:
-        shm.memcpy(heap_ptr, arr, arr.nbytes)
+        heap_write(heap_ptr, arr, arr.nbytes)
     return heap_ptr, lambda: read_raw(heap_ptr, arr.dtype, arr.size)
 
 
 def read_raw(ptr, dtype, n):
     a = np.empty(n, dtype)
     if n:
-        shm.memcpy(a, ptr, a.nbytes)
+        shm.memcpy(a, twin(ptr), a.nbytes)
     return a
 
 
@@ -226,10 +246,14 @@ HEAP_TGT = shm.malloc(CAP)
 assert HEAP_SRC and HEAP_TGT, "shmem_malloc failed"
 HOST_HEAP = os.environ.get("SHMEMX_HEAP_MEMORY") == "host"
 for q in range(npes):
-    # a host-kind heap is not peer-addressable: NULL, as the reference's shmem_ptr
-    want_null = HOST_HEAP and q != pe
+    # a host-kind heap is not peer-addressable: NULL, as the reference's
+    # shmem_ptr; nor is a mirrored heap's host view (a peer's store would go
+    # behind that peer's view), whose HBM twin is
+    want_null = (HOST_HEAP or MIRRORED) and q != pe
     if bool(shm.heap_ptr(HEAP_SRC, q)) == want_null:
         fails.append(f"heap_ptr(SRC, {q}) = {shm.heap_ptr(HEAP_SRC, q)}")
+    if MIRRORED and not shm.heap_ptr(twin(HEAP_SRC), q):
+        fails.append(f"heap_ptr(twin(SRC), {q}) is NULL")
 
 seed = 0x1000
 if scenario == "full":
@@ -255,14 +279,20 @@ if scenario == "full":
         for n in (1013, 100003):
             seed += 1
             run_case(t, op, n, (0, 0, npes), "direct", "heapoff", seed)
-    # put through heap_ptr, then a barrier: PE q's slot p holds p + 1
+    # put through heap_ptr, then a barrier: PE q's slot p holds p + 1.  On a
+    # mirrored heap the puts go to the peers' twins, and each PE invalidates
+    # its view of the slots after the barrier, then reads them with host loads
     slots = np.zeros(npes, np.int64)
-    shm.memcpy(HEAP_TGT, slots, slots.nbytes)
+    heap_write(HEAP_TGT, slots, slots.nbytes)
     shm.barrier_all()
     for q in range(npes):
-        shm.memcpy(shm.heap_ptr(HEAP_TGT, q) + 8 * pe, np.array([pe + 1], np.int64), 8)
+        shm.memcpy(shm.heap_ptr(twin(HEAP_TGT), q) + 8 * pe, np.array([pe + 1], np.int64), 8)
     shm.barrier_all()
-    got = read(HEAP_TGT, "long", npes)
+    if MIRRORED:
+        shm.mirror_invalidate(HEAP_TGT, 8 * npes)
+        got = host_view(HEAP_TGT, np.int64, npes).copy()
+    else:
+        got = read(HEAP_TGT, "long", npes)
     if list(got) != list(range(1, npes + 1)):
         fails.append(f"heap_ptr puts + barrier_all: {list(got)}")
     # the neighbouring collectives over IPC, against their oracles
@@ -351,7 +381,7 @@ elif scenario == "signal":
         for rep_i in range(5):
             seed += 1
             srcs = oracle.sources("double", 1, npes, n, base_seed=seed)
-            shm.memcpy(HEAP_SRC, np.ascontiguousarray(srcs[pe]), n * 8)
+            heap_write(HEAP_SRC, np.ascontiguousarray(srcs[pe]), n * 8)
             torch.cuda.synchronize()
             graph.replay()
             torch.cuda.synchronize()
@@ -536,15 +566,15 @@ elif scenario == "configs":
     for salt, (t, op, n) in enumerate(cases):
         ncases += 1
         print(f"config {t} {op} n={n}", flush=True)
-        shm.memcpy(BIG_SRC, gen(t, pe, n, salt), n * 8)
-        shm.memcpy(BIG_TGT, torch.zeros(n, dtype=torch.int64, device="cuda"), n * 8)
+        heap_write(BIG_SRC, gen(t, pe, n, salt), n * 8)
+        heap_write(BIG_TGT, torch.zeros(n, dtype=torch.int64, device="cuda"), n * 8)
         torch.cuda.synchronize()
         shm.to_all(t, op, BIG_TGT, BIG_SRC, n, 0, 0, npes)
         if shm.last_error():
             fails.append(f"config {t} {op}: last_error {shm.last_error()}")
             continue
         got = torch.empty(n, dtype=torch.int64 if t == "long" else torch.float64, device="cuda")
-        shm.memcpy(got, BIG_TGT, n * 8)
+        shm.memcpy(got, twin(BIG_TGT), n * 8)
         f = {"and": torch.bitwise_and, "or": torch.bitwise_or, "xor": torch.bitwise_xor,
              "sum": torch.add}[op]
         want = gen(t, 0, n, salt)
@@ -591,8 +621,8 @@ elif scenario == "configs8":
         print(f"configs8 {t} sum n={n} algo={algo}", flush=True)
         dt = torch.float64 if t == "double" else torch.float32
         sz = 8 if t == "double" else 4
-        shm.memcpy(BIG_SRC, gen(t, pe, n, salt), n * sz)
-        shm.memcpy(BIG_TGT, torch.zeros(n, dtype=dt, device="cuda"), n * sz)
+        heap_write(BIG_SRC, gen(t, pe, n, salt), n * sz)
+        heap_write(BIG_TGT, torch.zeros(n, dtype=dt, device="cuda"), n * sz)
         torch.cuda.synchronize()
         shm.set_algo(algo)
         shm.to_all(t, "sum", BIG_TGT, BIG_SRC, n, 0, 0, npes)
@@ -601,7 +631,7 @@ elif scenario == "configs8":
             fails.append(f"configs8 {t} n={n} {algo}: last_error {shm.last_error()}")
             continue
         got = torch.empty(n, dtype=dt, device="cuda")
-        shm.memcpy(got, BIG_TGT, n * sz)
+        shm.memcpy(got, twin(BIG_TGT), n * sz)
         order = list(range(npes))
         if algo == "gather":
             order = [pe] + [q for q in order if q != pe]
@@ -731,6 +761,58 @@ elif scenario == "mirrored":
     shm.free(p2)
     if npes > 1 and not shm.direct_stats(reset=False)["calls"] and os.environ.get("SHMEMX_TRANSPORT") == "ipc":
         fails.append("mirrored calls did not run DIRECT on the HBM twins")
+elif scenario == "mirror_stream":
+    # The mirrored view's fetch is ordered after the stream that wrote it, a
+    # non-blocking torch stream included (reduce-op.c:250-259 returns only
+    # once the target holds the result; here the stream-ordered form returns
+    # at once, and a host read of the target must still see the result).  On
+    # one non-blocking stream: a long run of 256 MiB folds on other buffers,
+    # then a fold that rewrites the source's HBM twin (source + 1), then
+    # shmemx_double_sum_to_all_on_stream on the view addresses (PE_size 1: a
+    # copy, reduce-op.c:213-216).  The host reads the target right away, with
+    # no synchronisation: it must be source + 1 everywhere, and still be after
+    # the stream completes.
+    assert MIRRORED and npes == 1
+    n = (64 << 20) // 8                      # 64 MiB target: 1024 blocks
+    big = (256 << 20) // 8
+    srcs = oracle.sources("double", 1, 1, n, base_seed=0xA11)
+    src, tgt = host_view(HEAP_SRC, np.float64, n), host_view(HEAP_TGT, np.float64, n)
+    src[:] = srcs[0]                         # host stores (HOST_NEWER)
+    tgt[:] = -1.0
+    want = srcs[0] + 1.0
+    stream = torch.cuda.Stream()
+    x = torch.rand(big, dtype=torch.float64, device="cuda")
+    y = torch.rand(big, dtype=torch.float64, device="cuda")
+    ones = torch.ones(n, dtype=torch.float64, device="cuda")
+    shm.mirror_sync(HEAP_SRC, n * 8)         # the host's source bytes in HBM
+    torch.cuda.synchronize()
+    shm.mirror_stats(reset=True)
+    for rep in range(2):
+        for _ in range(40):                  # ~5 ms of folds ahead of the call
+            shm.fold("double", "sum", y, x, big, stream.cuda_stream)
+        shm.fold("double", "sum", twin(HEAP_SRC), ones, n, stream.cuda_stream)   # source += 1 in HBM
+        shm.reduce_on_stream("double", "sum", HEAP_TGT, HEAP_SRC, n, 0, 0, 1, "auto", stream.cuda_stream)
+        ncases += 1
+        early = tgt.copy()                   # faults: waits for the stream, fetches
+        busy = not stream.query()            # (a sample only: the fetch has waited by now)
+        stream.synchronize()
+        late = tgt.copy()
+        if not same_bits(early, want):
+            fails.append(f"rep {rep}: host read right after the stream-ordered call: "
+                         f"{int((early != want).sum())} elements differ")
+        if not same_bits(late, want):
+            fails.append(f"rep {rep}: host read after stream.synchronize(): "
+                         f"{int((late != want).sum())} elements differ")
+        extra.setdefault("stream_busy_after_read", []).append(busy)
+        # next round: the source's twin was rewritten behind the view
+        shm.mirror_invalidate(HEAP_SRC, n * 8)
+        if not same_bits(src.copy(), want):   # (this fetch waits for the whole device)
+            fails.append(f"rep {rep}: invalidated source view reads stale bytes")
+        want = want + 1.0
+    st = shm.mirror_stats(reset=True)
+    extra["mirror_stats"] = st
+    if not st["blocks_fetched"]:
+        fails.append(f"no block was fetched: {st}")
 elif scenario == "mixed":
     # Members passing different memory kinds: host arrays above 256 KiB go in
     # 16 MiB staging chunks (one collective call each), device arrays in one

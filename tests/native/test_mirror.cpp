@@ -7,7 +7,10 @@
 // and nothing else crosses the "PCIe" backend.
 #include <unistd.h>
 
+#include <atomic>
 #include <cerrno>
+#include <chrono>
+#include <thread>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -16,6 +19,7 @@
 #include <vector>
 
 #include "mirror.h"
+#include "shmem_reduce_mi355x.h"   // shmemx_set_fatal_note (fatal_note.cpp)
 
 namespace M = shmx::mirror;
 
@@ -31,8 +35,13 @@ static int fails = 0;
 static std::vector<unsigned char> g_dev;   // the "device segment"
 static volatile size_t g_h2d = 0, g_d2h = 0;   // bytes moved
 
+// a hook the flush race test runs inside to_device, between the view's
+// protection change and the copy (another thread's store lands there)
+static void (*g_in_to_device)() = nullptr;
+
 // the backend works on the view's always-writable alias
 static void to_device(uint64_t off, size_t bytes, void *) {
+    if (g_in_to_device) g_in_to_device();
     std::memcpy(g_dev.data() + off, M::alias_base() + off, bytes);
     g_h2d += bytes;
 }
@@ -137,6 +146,65 @@ int main(int argc, char **argv) {
         close(fds[1]);
     }
 
+    // Two threads.  (1) A collective writes a 64-byte target at the start of
+    // block 50 while another thread stores to a neighbouring object in the
+    // same block: the store must wait for the write in flight, then land on
+    // top of the collective's result — neither is lost.
+    {
+        const size_t base = 50 * M::kBlock;
+        M::stats(true);
+        CHECK(M::begin_device_write(base, 64) == 1);
+        CHECK(M::state_of(base) == M::DEVICE_NEWER);
+        std::atomic<int> stored{0};
+        std::thread other([&] {
+            h[base + 100] = 42;              // faults, waits for end_device_write
+            stored.store(1);
+        });
+        std::this_thread::sleep_for(std::chrono::milliseconds(100));
+        CHECK(stored.load() == 0);           // still waiting: the write is in flight
+        for (size_t i = 0; i < 64; ++i) {    // the collective's result, "enqueued"
+            g_dev[base + i] = (unsigned char)(200 + i);
+            truth[base + i] = g_dev[base + i];
+        }
+        M::end_device_write();
+        other.join();
+        truth[base + 100] = 42;
+        CHECK(stored.load() == 1);
+        for (size_t i = 0; i < 128; ++i) CHECK(h[base + i] == truth[base + i]);
+        CHECK(M::state_of(base) == M::HOST_NEWER && M::stats(false).fault_waits >= 1);
+        CHECK(M::flush(base, 1) == 1 && g_dev[base + 100] == 42 && g_dev[base + 3] == 203);
+    }
+    // (2) A store another thread makes while a flush copies its block (after
+    // the protection change, before the copy) is not lost: it faults, waits,
+    // and leaves the block HOST_NEWER for the next flush.
+    {
+        const size_t base = 60 * M::kBlock;
+        h[base] = 1;                          // HOST_NEWER
+        truth[base] = 1;
+        static std::atomic<int> phase{0};
+        static volatile unsigned char *hv;
+        static size_t racing;
+        phase = 0;
+        hv = h;
+        racing = base + 777;
+        std::thread other([] {
+            while (phase.load() != 1) std::this_thread::yield();
+            hv[racing] = 77;                  // faults (read-only now), waits for the lock
+            phase.store(3);
+        });
+        g_in_to_device = [] {
+            phase.store(1);
+            std::this_thread::sleep_for(std::chrono::milliseconds(50));
+            if (phase.load() == 3) ++fails;   // the racing store did not fault
+        };
+        CHECK(M::flush(base, 1) == 1);
+        g_in_to_device = nullptr;
+        other.join();
+        truth[racing] = 77;
+        CHECK(phase.load() == 3 && M::state_of(base) == M::HOST_NEWER);
+        CHECK(M::flush(base, 1) == 1 && g_dev[racing] == 77 && g_dev[base] == 1);
+    }
+
     // random interleavings against the model
     std::mt19937_64 rng(12345);
     for (int it = 0; it < iters; ++it) {
@@ -177,6 +245,19 @@ int main(int argc, char **argv) {
     std::printf("stats: %llu write faults, %llu read faults, %llu flushed, %llu fetched blocks\n",
                 (unsigned long long)st.write_faults, (unsigned long long)st.read_faults,
                 (unsigned long long)st.blocks_flushed, (unsigned long long)st.blocks_fetched);
+    M::destroy();
+
+    // The fatal-note handler installed BEFORE the view exists, then removed:
+    // what it saved predates the view's handler, and removing it must put
+    // the view's handler back in front, not uninstall it (the next host
+    // store to a CLEAN block would kill the process).
+    CHECK(shmemx_set_fatal_note("last words\n", 3) == SHMEMX_OK);
+    g_dev.assign(bytes, 0);
+    CHECK(M::create(bytes, M::Backend{to_device, to_host, drain, nullptr}));
+    CHECK(shmemx_set_fatal_note(nullptr, 0) == SHMEMX_OK);
+    volatile unsigned char *h2 = reinterpret_cast<volatile unsigned char *>(M::host_base());
+    h2[3 * M::kBlock + 9] = 5;                        // faults into the view's handler
+    CHECK(M::state_of(3 * M::kBlock) == M::HOST_NEWER && h2[3 * M::kBlock + 9] == 5);
     M::destroy();
     if (fails) {
         std::printf("%d failures\n", fails);

@@ -329,6 +329,34 @@ def test_mixed_memory_kinds_fail_collectively(tmp_path, transport):
 
 
 @pytest.mark.gpu
+def test_mirrored_view_fetch_waits_for_non_blocking_stream(tmp_path):
+    """A host read of a mirrored target right after a stream-ordered call on
+    a non-blocking torch stream, behind ~5 ms of other work on that stream and
+    a kernel that rewrote the source's HBM twin: the fault waits for the
+    stream (the writer recorded at the call) and reads the result, not the
+    stale bytes; the view stays right after the stream completes."""
+    reports = run_pes(tmp_path, 1, "mirror_stream", {"SHMEMX_HEAP_MEMORY": "mirrored"}, timeout=300)
+    r = reports[0]
+    assert not r["fails"], r["fails"]
+    assert r["ncases"] == 2 and r["mirror_stats"]["blocks_fetched"] > 0, r
+
+
+@pytest.mark.gpu
+def test_ipc_full_scenario_on_mirrored_heap(tmp_path):
+    """The 2-PE "full" scenario (every reference pair and active set on heap
+    operands, in place, overlap, torch and host arrays, heap_ptr puts,
+    broadcast and [f]collect) with the library's default heap mode: the
+    collectives get host-view addresses, the test's own HIP copies the twins
+    (shmemx_mirror_device_ptr) with sync/invalidate around them, and peers'
+    heap_ptr of a view address is NULL while the twin's is not."""
+    reports = run_pes(tmp_path, 2, "full", {"SHMEMX_HEAP_MEMORY": None})
+    for r in reports:
+        assert r["ncases"] > 0
+        assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
+    fences_checked(reports)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("transport,npes,mode", [("ipc", 1, "mirrored"), ("ipc", 4, "mirrored"),
                                                 ("rccl", 3, "mirrored"), ("ipc", 2, None)])
 def test_mirrored_heap(tmp_path, transport, npes, mode):

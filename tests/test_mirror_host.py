@@ -12,7 +12,9 @@ import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(REPO, "openshmem-async_amd", "csrc")
-SRCS = [os.path.join(REPO, "tests", "native", "test_mirror.cpp"), os.path.join(CSRC, "mirror.cpp")]
+SRCS = [os.path.join(REPO, "tests", "native", "test_mirror.cpp"), os.path.join(CSRC, "mirror.cpp"),
+        os.path.join(CSRC, "fatal_note.cpp")]
+INCLUDE = os.path.join(REPO, "include")
 
 
 @pytest.mark.parametrize("flags", [["-O2"], ["-O1", "-g", "-fsanitize=address,undefined",
@@ -20,8 +22,8 @@ SRCS = [os.path.join(REPO, "tests", "native", "test_mirror.cpp"), os.path.join(C
                          ids=["plain", "asan_ubsan"])
 def test_mirror_core_against_model(tmp_path, flags):
     exe = tmp_path / "test_mirror"
-    subprocess.run(["g++", *flags, "-std=c++17", "-Wall", "-Wextra", "-I", CSRC, *SRCS, "-o", str(exe)],
-                   check=True)
+    subprocess.run(["g++", *flags, "-std=c++17", "-pthread", "-Wall", "-Wextra", "-I", CSRC, "-I", INCLUDE, *SRCS,
+                    "-o", str(exe)], check=True)
     env = dict(os.environ, ASAN_OPTIONS="handle_segv=0:allow_user_segv_handler=1:detect_leaks=1",
                UBSAN_OPTIONS="print_stacktrace=1")
     out = subprocess.run([str(exe), "4000"], capture_output=True, text=True, timeout=300, env=env)
