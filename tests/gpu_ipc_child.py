@@ -773,7 +773,7 @@ elif scenario == "mirror_stream":
     # no synchronisation: it must be source + 1 everywhere, and still be after
     # the stream completes.
     assert MIRRORED and npes == 1
-    n = (64 << 20) // 8                      # 64 MiB target: 1024 blocks
+    n = (32 << 20) // 8                      # 32 MiB target: 512 blocks (CAP is 48 MiB)
     big = (256 << 20) // 8
     srcs = oracle.sources("double", 1, 1, n, base_seed=0xA11)
     src, tgt = host_view(HEAP_SRC, np.float64, n), host_view(HEAP_TGT, np.float64, n)

@@ -88,6 +88,8 @@ def test_bench_multi_rank_line(tmp_path, transport, npes):
     for path, text in strings(extras):
         if path.endswith("_note") or path.startswith(".auto_recommendation"):
             continue     # labels and algorithm names, not outcomes
+        if path == ".partial_sets" and npes < 4 and text == "needs N >= 4":
+            continue
         refused = "ENOTSUP" in text and transport == "ipc" and any(
             f".{a}" in path or f"algo_{a}_" in path for a in RCCL_ONLY)
         if not refused:
