@@ -221,12 +221,17 @@ def config_extras(world, stream, barrier, max_over_ranks, cap=256 * 1024 * 1024)
 
     # Working sets under the 256 MiB Infinity Cache (MALL) stay on-die across
     # back-to-back steps, so a warm rate there is not HBM bandwidth (DESIGN.md
-    # §4.2).  The "cold" rate rewrites a 1 GiB scratch before every step and
-    # times the steps alone with HIP events on the stream: every step starts
-    # from HBM.
+    # §4.2).  The "cold" rate reads a 1 GiB scratch before every step (a
+    # read-only sweep: it evicts the step's arrays and leaves no dirty line)
+    # and times the steps alone with HIP events on the stream: every step
+    # starts from HBM.  Round 2 rewrote the scratch instead; the dirty lines
+    # that left in the MALL were then written back inside the timed step
+    # (profiles/r03_cold_midsize.txt) — that variant is kept, labelled, as
+    # the rate right after a producer's writes.
     scratch = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+    scratch64 = scratch.view(torch.float64)
 
-    def rate(type_name, op, n, elem, steps, cold=False):
+    def rate(type_name, op, n, elem, steps, cold=None):
         x = (torch.randint(-2**62, 2**62, (n,), dtype=torch.int64, device="cuda", generator=g)
              if elem == 8 and type_name == "long" else
              torch.rand(n, dtype=torch.float32, device="cuda", generator=g))
@@ -245,7 +250,10 @@ def config_extras(world, stream, barrier, max_over_ranks, cap=256 * 1024 * 1024)
             torch.cuda.synchronize()
             with torch.cuda.stream(stream):
                 for k, (e0, e1) in enumerate(ev):
-                    scratch.fill_(k & 0xFF)
+                    if cold == "dirty":
+                        scratch.fill_(k & 0xFF)
+                    else:
+                        scratch64.sum()
                     e0.record(stream)
                     fn()
                     e1.record(stream)
@@ -260,17 +268,24 @@ def config_extras(world, stream, barrier, max_over_ranks, cap=256 * 1024 * 1024)
     for op in ("and", "or", "xor"):
         key = "64Mi" if nlong == 64 * 1024 * 1024 else str(nlong)
         out[f"long_{op}_{key}_GiBps"] = rate("long", op, nlong, 8, 10)
-    cold, warm = {}, {}
+    cold, dirty, warm = {}, {}, {}
     n = 4 * 1024
     while n <= min(256 * 1024 * 1024, cap):
         steps = 20 if n >= 1 << 24 else 50
-        cold[str(n)] = rate("float", "sum", n, 4, steps, cold=True)
+        cold[str(n)] = rate("float", "sum", n, 4, steps, cold="clean")
+        dirty[str(n)] = rate("float", "sum", n, 4, steps, cold="dirty")
         warm[str(n)] = rate("float", "sum", n, 4, steps)
         n *= 4
     out["float_sum_GiBps_vs_nreduce"] = cold
     out["float_sum_GiBps_vs_nreduce_note"] = (
-        "cold: a 1 GiB scratch is rewritten before every step and only the steps are timed "
-        "(HIP events on the stream), so every step reads and writes HBM")
+        "cold: a 1 GiB scratch is read (read-only sweep: evicts, leaves nothing dirty) before every "
+        "step and only the steps are timed (HIP events on the stream), so every step reads and "
+        "writes HBM; GiB/s = PEs x nreduce x 4 B / step")
+    out["float_sum_GiBps_vs_nreduce_after_write_flush"] = dirty
+    out["float_sum_GiBps_vs_nreduce_after_write_flush_note"] = (
+        "the same, but the scratch is REWRITTEN before every step (round 2's flush): up to 256 MiB "
+        "of its dirty lines sit in the Infinity Cache and are written back inside the timed step, "
+        "as after a producer kernel's writes")
     out["float_sum_GiBps_vs_nreduce_warm_mall_resident"] = warm
     out["float_sum_GiBps_vs_nreduce_warm_note"] = (
         "back to back, no flush: working sets (3 x nreduce x 4 B at N = 1) under 256 MiB are served "

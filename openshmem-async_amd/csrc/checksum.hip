@@ -16,8 +16,24 @@
 //
 // Kernel shape: 16-byte loads per lane (2 words), a per-lane XOR, a wave XOR
 // reduction by DPP within 16-lane rows and v_readlane across rows, the 4 wave
-// partials combined in LDS, one partial per workgroup in its own slot, and a
-// one-workgroup kernel XORing the partials (same DPP + LDS reduction).
+// partials combined in LDS, one partial per workgroup in its own slot, and the
+// LAST workgroup to finish XORs the partials (same DPP + LDS reduction) and
+// stores the result where the caller asked — host-mapped memory included, so
+// the host reads it after the stream wait with no copy command.  One launch:
+// round 2's separate one-workgroup finish kernel and the 8-byte D2H copy cost
+// about 25 us per call over the 41 us of streaming.
+//
+// The hand-off of the partials to the last workgroup follows the guide's
+// measured form (MI355X_MICROARCH.md, "inter-workgroup visibility", the sc1
+// table): ONE lane per workgroup stores its partial with an agent-scope (sc1,
+// write-through) store, waits for it (vmcnt(0)), then adds to an agent-scope
+// arrival counter; the workgroup whose add returns the last count goes on.
+// No per-workgroup release fence (an L2 write-back in each of 4096 blocks).
+// The counter is sharded: 4096 adds to ONE address serialise at ~15 ns each
+// (~60 us, measured in round 2 with atomicXor and again here with one
+// counter: 89 us per call), so workgroup b adds to shard b % 16 (each on its
+// own 128-B line), the last of each shard adds to a top counter, and the last
+// of those (one agent acquire) reads every partial with sc1 loads.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -74,11 +90,20 @@ __device__ __forceinline__ uint64_t wave_xor(uint64_t v) {
 }
 
 // nwords full 8-byte words; `tail` bytes of a final partial word; LD: mask
-// 16-byte long double slots down to their 10 value bytes.
+// 16-byte long double slots down to their 10 value bytes.  work: the shard
+// counters (kShards of them, kLine words apart), the top counter, then the
+// per-workgroup partials (zero counters between launches: the last workgroup
+// resets them); *out the result.
+constexpr int kShards = 16;
+constexpr int kLine = 16;                       // 128 B between counters
+constexpr int kTop = kShards * kLine;           // the top counter's word
+constexpr int kPartials = (kShards + 1) * kLine;   // first partial's word
 template <bool LD>
 __global__ __launch_bounds__(kCkBlock) void checksum_kernel(const unsigned char *data, size_t nwords,
-                                                            size_t tail, unsigned long long *partials) {
+                                                            size_t tail, unsigned long long *work,
+                                                            unsigned long long *out) {
     __shared__ unsigned long long part[kCkBlock / 64];
+    __shared__ int is_last;
     const size_t tid = (size_t)blockIdx.x * kCkBlock + threadIdx.x;
     const size_t nthr = (size_t)gridDim.x * kCkBlock;
     uint64_t h = 0;
@@ -108,31 +133,69 @@ __global__ __launch_bounds__(kCkBlock) void checksum_kernel(const unsigned char 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) part[wave] = h;
     __syncthreads();
+    unsigned long long *partials = work + kPartials;
+    const unsigned nblocks = gridDim.x;
+    const unsigned nshards = nblocks < (unsigned)kShards ? nblocks : (unsigned)kShards;
     if (threadIdx.x == 0) {
         unsigned long long b = 0;
 #pragma unroll
         for (int w = 0; w < kCkBlock / 64; ++w) b ^= part[w];
-        partials[blockIdx.x] = b;   // one slot per block: no contended atomic
+        // one slot per block (no contended atomic on the result), written
+        // through to memory, drained, then counted
+        __hip_atomic_store(partials + blockIdx.x, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned sh = blockIdx.x % nshards;
+        const unsigned in_shard = (nblocks - sh + nshards - 1) / nshards;
+        unsigned *shard = reinterpret_cast<unsigned *>(work + sh * kLine);
+        int last = __hip_atomic_fetch_add(shard, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   in_shard - 1;
+        if (last) {
+            unsigned *top = reinterpret_cast<unsigned *>(work + kTop);
+            last = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nshards - 1;
+        }
+        is_last = last;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (!is_last) return;
+    // the last workgroup: every partial, with sc1 loads
+    uint64_t x = 0;
+    for (unsigned i = threadIdx.x; i < gridDim.x; i += kCkBlock)
+        x ^= __hip_atomic_load(partials + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    x = wave_xor(x);
+    __syncthreads();   // part[] is reused
+    if (lane == 0) part[wave] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long r = 0;
+#pragma unroll
+        for (int w = 0; w < kCkBlock / 64; ++w) r ^= part[w];
+        __hip_atomic_store(out, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // zero counters for the next launch (stream-ordered after this one)
+        for (unsigned k = 0; k < nshards; ++k)
+            __hip_atomic_store(reinterpret_cast<unsigned *>(work + k * kLine), 0u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(reinterpret_cast<unsigned *>(work + kTop), 0u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
-// The block partials XORed by one workgroup (DPP wave reduction + LDS), the
-// result in *out.  A same-address atomic per block cost ~15 ns each, 60 us
-// for 4096 blocks: more than streaming the 256 MiB (profiles/r02_checksum_lab.txt).
-__global__ __launch_bounds__(kCkBlock) void checksum_finish_kernel(const unsigned long long *partials,
-                                                                   int nparts, unsigned long long *out) {
-    __shared__ unsigned long long part[kCkBlock / 64];
-    uint64_t h = 0;
-    for (int i = threadIdx.x; i < nparts; i += kCkBlock) h ^= partials[i];
-    h = wave_xor(h);
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = h;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long b = 0;
-#pragma unroll
-        for (int w = 0; w < kCkBlock / 64; ++w) b ^= part[w];
-        *out = b;
-    }
+// The counter + partials: device memory of this process, the counter zeroed
+// once here and by every launch's last workgroup after that.
+unsigned long long *checksum_work() {
+    static unsigned long long *w = [] {
+        void *p = nullptr;
+        const size_t words = kPartials + (size_t)kChecksumMaxBlocks;
+        if (hipMalloc(&p, sizeof(unsigned long long) * words) != hipSuccess) return
+            static_cast<unsigned long long *>(nullptr);
+        if (hipMemset(p, 0, sizeof(unsigned long long) * kPartials) != hipSuccess ||
+            hipDeviceSynchronize() != hipSuccess) return static_cast<unsigned long long *>(nullptr);
+        return static_cast<unsigned long long *>(p);
+    }();
+    return w;
 }
 
 }  // namespace
@@ -141,26 +204,24 @@ hipError_t launch_checksum(int type, const void *ptr, size_t n, unsigned long lo
                            hipStream_t stream) {
     const size_t sz = type_size(type);
     if (!sz || !out) return hipErrorInvalidValue;
-    if (n == 0) return hipMemsetAsync(out, 0, sizeof *out, stream);
+    unsigned long long *work = checksum_work();
+    if (!work) return hipErrorOutOfMemory;
     const size_t bytes = n * sz;
     const bool ld = type == SHMEMX_TYPE_LONGDOUBLE;
     const size_t nwords = bytes / 8, tail = bytes % 8;
     // 16-byte loads need a 16-byte aligned base; otherwise hash bytewise
     // through the tail path is too slow, so require it (hipMalloc gives 256).
-    if ((reinterpret_cast<uintptr_t>(ptr) & 15u) != 0) return hipErrorInvalidValue;
+    if (n && (reinterpret_cast<uintptr_t>(ptr) & 15u) != 0) return hipErrorInvalidValue;
     size_t blocks = (nwords / 2 + kCkBlock - 1) / kCkBlock;
     if (blocks > (size_t)kChecksumMaxBlocks) blocks = kChecksumMaxBlocks;
     if (blocks < 1) blocks = 1;
     const unsigned char *p = static_cast<const unsigned char *>(ptr);
-    unsigned long long *partials = out + 1;
     if (ld)
         hipLaunchKernelGGL(checksum_kernel<true>, dim3((unsigned)blocks), dim3(kCkBlock), 0, stream, p,
-                           nwords, tail, partials);
+                           nwords, tail, work, out);
     else
         hipLaunchKernelGGL(checksum_kernel<false>, dim3((unsigned)blocks), dim3(kCkBlock), 0, stream, p,
-                           nwords, tail, partials);
-    hipLaunchKernelGGL(checksum_finish_kernel, dim3(1), dim3(kCkBlock), 0, stream, partials, (int)blocks,
-                       out);
+                           nwords, tail, work, out);
     return hipGetLastError();
 }
 

@@ -291,12 +291,16 @@ int checksum_impl(int type, const void *ptr, size_t nelems, unsigned long long *
     if (bytes) ptr = heap::device_operand(ptr, bytes);   // mirrored heap: the HBM twin
     DevBuf in = device_in(ptr, bytes, g_state.cws_src, g_state.cws_src_bytes, s);
     if (bytes && !in.dev) return set_error(SHMEMX_ENOMEM);
-    unsigned long long *dres = static_cast<unsigned long long *>(
-        grow(g_state.token, g_state.token_bytes, sizeof(unsigned long long) * (1 + kChecksumMaxBlocks)));
-    if (!dres) return set_error(SHMEMX_ENOMEM);
-    if (launch_checksum(type, in.dev, nelems, dres, s) != hipSuccess) return set_error(SHMEMX_EINVAL);
-    SHMX_HIP(hipMemcpyAsync(out, dres, sizeof *out, hipMemcpyDeviceToHost, s));
+    // the kernel stores the result straight into a page-locked host word:
+    // no copy command, one stream wait
+    static unsigned long long *host_word = [] {
+        void *p = nullptr;
+        SHMX_HIP(hipHostMalloc(&p, sizeof(unsigned long long), hipHostMallocCoherent));
+        return static_cast<unsigned long long *>(p);
+    }();
+    if (launch_checksum(type, in.dev, nelems, host_word, s) != hipSuccess) return set_error(SHMEMX_EINVAL);
     SHMX_HIP(hipStreamSynchronize(s));
+    *out = *static_cast<volatile unsigned long long *>(host_word);
     return SHMEMX_OK;
 }
 

@@ -158,13 +158,18 @@ constexpr int kUnrollN = 4;
 // (all blocks start at input 0 together and stay in step behind that one
 // link), so only one of the P - 1 links would carry traffic at a time.  Here
 // every lane issues its U vectors of ALL inputs before folding any (uniform
-// predicates, unrolled), so each wave has loads in flight on every link; U =
-// 16 / MAXIN keeps 16 vectors in registers (4 per input up to 4 inputs, 2 up
-// to 8, 1 up to 16).  The fold order is unchanged: input 0, then 1, ...
+// predicates, unrolled), so each wave has loads in flight on every link: 4
+// vectors per input up to 8 inputs (32 in registers), 2 up to 16.  Round 2
+// kept 16 vectors (2 per input at 8 inputs); at P = 8 x 16 Mi doubles on
+// local HBM 4 per input runs 201.0 against 204.2 us, 1 per input 345 us
+// (tools/peers_gather_lab.hip, profiles/r03_peers_gather_lab.txt).  The fold
+// order is unchanged: input 0, then 1, ...
+constexpr int peers_unroll(int maxin) { return maxin <= 8 ? 4 : 2; }
+
 template <typename T, int OP, int MAXIN, int NT>
 __global__ __launch_bounds__(kBlock) void fold_peers_kernel(FoldArgs args) {
     constexpr int E = 16 / sizeof(T);
-    constexpr int U = kMaxFoldInputs / MAXIN;
+    constexpr int U = peers_unroll(MAXIN);
     const int nins = args.nins;
     const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
     const size_t nthr = (size_t)gridDim.x * kBlock;
@@ -253,13 +258,13 @@ hipError_t launch_typed(const FoldArgs &a, hipStream_t stream) {
         }
     } else if (a.peers && !kHeavyOp<T, OP> && (NT == 0 || NT == 3)) {
         if (a.nins <= 4)
-            hipLaunchKernelGGL((fold_peers_kernel<T, OP, 4, NT>), dim3((unsigned)grid_for(a, 4)),
+            hipLaunchKernelGGL((fold_peers_kernel<T, OP, 4, NT>), dim3((unsigned)grid_for(a, peers_unroll(4))),
                                dim3(kBlock), 0, stream, a);
         else if (a.nins <= 8)
-            hipLaunchKernelGGL((fold_peers_kernel<T, OP, 8, NT>), dim3((unsigned)grid_for(a, 2)),
+            hipLaunchKernelGGL((fold_peers_kernel<T, OP, 8, NT>), dim3((unsigned)grid_for(a, peers_unroll(8))),
                                dim3(kBlock), 0, stream, a);
         else
-            hipLaunchKernelGGL((fold_peers_kernel<T, OP, 16, NT>), dim3((unsigned)grid_for(a, 1)),
+            hipLaunchKernelGGL((fold_peers_kernel<T, OP, 16, NT>), dim3((unsigned)grid_for(a, peers_unroll(16))),
                                dim3(kBlock), 0, stream, a);
     } else {
         hipLaunchKernelGGL((fold_kernel<T, OP, 0, kUnrollN, NT>), dim3((unsigned)grid_for(a, kUnrollN)),
@@ -268,11 +273,17 @@ hipError_t launch_typed(const FoldArgs &a, hipStream_t stream) {
     return hipGetLastError();
 }
 
-// Cache policy: streams larger than the 256 MiB Infinity Cache go
-// non-temporal on both loads and stores (measured +15-20 % at 768 MiB,
-// profiles/ and DESIGN.md); smaller working sets keep the default policy so
-// back-to-back calls can hit in the MALL.
-constexpr size_t kNtThresholdBytes = size_t(256) << 20;
+// Cache policy: working sets of 32 MiB and more go non-temporal on both
+// loads and stores.  Round 1 set the cut at the 256 MiB Infinity Cache from
+// back-to-back (warm) runs; round 3 measured the 4-64 Mi-float fold cold
+// (tools/cold_midsize_probe.py, profiles/r03_cold_midsize.txt): after a
+// producer's writes leave dirty lines in the MALL, the default policy runs
+// 3.1 / 4.1 TB/s at 48 / 192 MiB against 4.3 / 5.8 non-temporal (the
+// default's stores evict those lines and pay their write-back); from a clean
+// cache the default leads by 5-7 %, back to back the two tie.  So
+// non-temporal, whose worst case is the better one, from 32 MiB up; below
+// it a call is launch-bound and the default keeps L2/MALL hits.
+constexpr size_t kNtThresholdBytes = size_t(32) << 20;
 
 template <typename T, int OP>
 hipError_t launch_nt(const FoldArgs &a, hipStream_t stream) {
@@ -455,6 +466,10 @@ hipError_t launch_fold_peers(int type, int op, void *out, const void *const *ins
 // the same peer, one link at a time.  On local HBM (one GPU) this costs 4 %
 // against the y-major order (80.5 vs 77.4 us, 7 x 32 MiB), and runs of 16
 // blocks per segment cost 15 % (89.3 us): profiles/r02c_pmc_kernels.json.
+// Two vectors per lane per step, not four: interleaved, 79.3 against 82.7 us
+// warm, 81.4 against 85.0 cold (tools/peers_gather_lab.hip,
+// profiles/r03_peers_gather_lab.txt); the resident grid still keeps ~16 MiB
+// of loads in flight, far more than the links' bandwidth-latency product.
 namespace {
 
 struct CopySeg {
@@ -467,7 +482,7 @@ struct GatherArgs {
     int nseg;
 };
 
-constexpr int kGatherUnroll = 4;
+constexpr int kGatherUnroll = 2;
 
 __global__ __launch_bounds__(kBlock) void gather_kernel(GatherArgs a) {
     const CopySeg sg = a.seg[blockIdx.x % a.nseg];   // the segments in turn

@@ -115,8 +115,9 @@ struct SignalFoldArgs {
 hipError_t launch_signal_fold(int type, int op, const SignalFoldArgs &a, hipStream_t stream);
 
 // Position-aware 64-bit checksum of n elements of `type` at device address
-// ptr (16-byte aligned) into out[0] (device memory, with room for
-// kChecksumMaxBlocks more words of block partials after it), stream-ordered.
+// ptr (16-byte aligned) into *out (device memory or host-mapped page-locked
+// memory: the kernel stores it with a system-scope store), stream-ordered,
+// one launch.  Calls must not overlap in time (one arrival counter per process).
 constexpr int kChecksumMaxBlocks = 4096;
 hipError_t launch_checksum(int type, const void *ptr, size_t n, unsigned long long *out,
                            hipStream_t stream);

@@ -114,3 +114,6 @@ assert torch.equal(dst[sl:], src[sl:]), "gather copied wrong bytes"
 del dst
 
 timed("checksum", lambda: shm.checksum("double", src, n), 8 * n, None, blocking=True)
+# shmemx_verify at one PE: the checksum launch, the stream wait and the
+# (here empty) exchange — the whole call on the host clock
+timed("verify", lambda: shm.verify("double", src, n, 0, 0, 1), 8 * n, None, blocking=True)
