@@ -37,6 +37,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "internal.h"
 #include "shmem_reduce_mi355x.h"
@@ -93,15 +94,16 @@ __device__ __forceinline__ uint64_t wave_xor(uint64_t v) {
 // 16-byte long double slots down to their 10 value bytes.  work: the shard
 // counters (kShards of them, kLine words apart), the top counter, then the
 // per-workgroup partials (zero counters between launches: the last workgroup
-// resets them); *out the result.
+// resets them); out[0] the result, then out[1] = epoch.
 constexpr int kShards = 16;
 constexpr int kLine = 16;                       // 128 B between counters
 constexpr int kTop = kShards * kLine;           // the top counter's word
 constexpr int kPartials = (kShards + 1) * kLine;   // first partial's word
-template <bool LD>
+template <bool LD, int UNROLL>
 __global__ __launch_bounds__(kCkBlock) void checksum_kernel(const unsigned char *data, size_t nwords,
                                                             size_t tail, unsigned long long *work,
-                                                            unsigned long long *out) {
+                                                            unsigned long long *out,
+                                                            unsigned long long epoch) {
     __shared__ unsigned long long part[kCkBlock / 64];
     __shared__ int is_last;
     const size_t tid = (size_t)blockIdx.x * kCkBlock + threadIdx.x;
@@ -115,7 +117,16 @@ __global__ __launch_bounds__(kCkBlock) void checksum_kernel(const unsigned char 
     // VALU-heavy enough to share the bound with HBM).
     uint64_t c = (2 * (uint64_t)tid + 1) * kPhi;
     const uint64_t dc = 2 * (uint64_t)nthr * kPhi;
-    for (size_t i = tid; i < npairs; i += nthr, c += dc)
+    size_t i = tid;
+    if (UNROLL == 2) {
+        // two vectors in flight per lane per trip
+        for (; i + nthr < npairs; i += 2 * nthr, c += 2 * dc) {
+            const u32x4 a = __builtin_nontemporal_load(v + i);
+            const u32x4 b = __builtin_nontemporal_load(v + i + nthr);
+            h ^= mix_pair<LD>(a, c) ^ mix_pair<LD>(b, c + dc);
+        }
+    }
+    for (; i < npairs; i += nthr, c += dc)
         h ^= mix_pair<LD>(__builtin_nontemporal_load(v + i), c);
     if (tid == 0) {
         if (nwords & 1) {  // odd word count (only when !LD)
@@ -161,10 +172,21 @@ __global__ __launch_bounds__(kCkBlock) void checksum_kernel(const unsigned char 
     }
     __syncthreads();
     if (!is_last) return;
-    // the last workgroup: every partial, with sc1 loads
+    // the last workgroup: every partial, with sc1 loads, all issued before
+    // any is used (a load per loop trip would wait out each one's latency:
+    // 16 round trips to memory per lane at 4096 blocks); slots past the grid
+    // are loaded from a valid address and masked, so no load is guarded
+    constexpr int kPer = kChecksumMaxBlocks / kCkBlock;
+    uint64_t pv[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const unsigned i = threadIdx.x + k * kCkBlock;
+        pv[k] = __hip_atomic_load(partials + (i < nblocks ? i : nblocks - 1), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+    }
     uint64_t x = 0;
-    for (unsigned i = threadIdx.x; i < gridDim.x; i += kCkBlock)
-        x ^= __hip_atomic_load(partials + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) x ^= threadIdx.x + k * kCkBlock < nblocks ? pv[k] : 0;
     x = wave_xor(x);
     __syncthreads();   // part[] is reused
     if (lane == 0) part[wave] = x;
@@ -173,7 +195,11 @@ __global__ __launch_bounds__(kCkBlock) void checksum_kernel(const unsigned char 
         unsigned long long r = 0;
 #pragma unroll
         for (int w = 0; w < kCkBlock / 64; ++w) r ^= part[w];
+        // the result, then (ordered behind it: one lane, drained) the call's
+        // epoch, which the host polls instead of waiting for the stream
         __hip_atomic_store(out, r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(out + 1, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         // zero counters for the next launch (stream-ordered after this one)
         for (unsigned k = 0; k < nshards; ++k)
             __hip_atomic_store(reinterpret_cast<unsigned *>(work + k * kLine), 0u, __ATOMIC_RELAXED,
@@ -201,7 +227,7 @@ unsigned long long *checksum_work() {
 }  // namespace
 
 hipError_t launch_checksum(int type, const void *ptr, size_t n, unsigned long long *out,
-                           hipStream_t stream) {
+                           unsigned long long epoch, hipStream_t stream) {
     const size_t sz = type_size(type);
     if (!sz || !out) return hipErrorInvalidValue;
     unsigned long long *work = checksum_work();
@@ -213,15 +239,29 @@ hipError_t launch_checksum(int type, const void *ptr, size_t n, unsigned long lo
     // through the tail path is too slow, so require it (hipMalloc gives 256).
     if (n && (reinterpret_cast<uintptr_t>(ptr) & 15u) != 0) return hipErrorInvalidValue;
     size_t blocks = (nwords / 2 + kCkBlock - 1) / kCkBlock;
-    if (blocks > (size_t)kChecksumMaxBlocks) blocks = kChecksumMaxBlocks;
+    // 2048 workgroups: 44.6 us at 32 Mi doubles against 45.3 at 4096 (fewer
+    // arrivals); 1024 and fewer lose bytes in flight (profiles/r03_checksum.txt)
+    static const size_t cap = [] {
+        const char *e = std::getenv("SHMEMX_CHECKSUM_BLOCKS");   // tuning experiments
+        const long v = e ? std::atol(e) : 0;
+        return v > 0 && v <= kChecksumMaxBlocks ? (size_t)v : (size_t)2048;
+    }();
+    if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
     const unsigned char *p = static_cast<const unsigned char *>(ptr);
+    static const int unroll = [] {
+        const char *e = std::getenv("SHMEMX_CHECKSUM_UNROLL");   // tuning experiments
+        return e && std::atoi(e) == 2 ? 2 : 1;
+    }();
     if (ld)
-        hipLaunchKernelGGL(checksum_kernel<true>, dim3((unsigned)blocks), dim3(kCkBlock), 0, stream, p,
-                           nwords, tail, work, out);
+        hipLaunchKernelGGL((checksum_kernel<true, 1>), dim3((unsigned)blocks), dim3(kCkBlock), 0, stream, p,
+                           nwords, tail, work, out, epoch);
+    else if (unroll == 2)
+        hipLaunchKernelGGL((checksum_kernel<false, 2>), dim3((unsigned)blocks), dim3(kCkBlock), 0, stream, p,
+                           nwords, tail, work, out, epoch);
     else
-        hipLaunchKernelGGL(checksum_kernel<false>, dim3((unsigned)blocks), dim3(kCkBlock), 0, stream, p,
-                           nwords, tail, work, out);
+        hipLaunchKernelGGL((checksum_kernel<false, 1>), dim3((unsigned)blocks), dim3(kCkBlock), 0, stream, p,
+                           nwords, tail, work, out, epoch);
     return hipGetLastError();
 }
 

@@ -291,16 +291,31 @@ int checksum_impl(int type, const void *ptr, size_t nelems, unsigned long long *
     if (bytes) ptr = heap::device_operand(ptr, bytes);   // mirrored heap: the HBM twin
     DevBuf in = device_in(ptr, bytes, g_state.cws_src, g_state.cws_src_bytes, s);
     if (bytes && !in.dev) return set_error(SHMEMX_ENOMEM);
-    // the kernel stores the result straight into a page-locked host word:
-    // no copy command, one stream wait
-    static unsigned long long *host_word = [] {
+    // The kernel stores the result straight into page-locked host memory,
+    // then this call's epoch behind it: the host polls the epoch instead of
+    // waiting for the stream (no copy command, no completion signal to wake
+    // on; ~10 us per call).  A kernel that never gets there (an error) is
+    // caught by the stream query every few microseconds, and then by the
+    // stream wait, which reports it.
+    static volatile unsigned long long *host_word = [] {
         void *p = nullptr;
-        SHMX_HIP(hipHostMalloc(&p, sizeof(unsigned long long), hipHostMallocCoherent));
-        return static_cast<unsigned long long *>(p);
+        SHMX_HIP(hipHostMalloc(&p, 2 * sizeof(unsigned long long), hipHostMallocCoherent));
+        return static_cast<volatile unsigned long long *>(p);
     }();
-    if (launch_checksum(type, in.dev, nelems, host_word, s) != hipSuccess) return set_error(SHMEMX_EINVAL);
-    SHMX_HIP(hipStreamSynchronize(s));
-    *out = *static_cast<volatile unsigned long long *>(host_word);
+    static unsigned long long epoch = 0;
+    ++epoch;
+    if (launch_checksum(type, in.dev, nelems, const_cast<unsigned long long *>(host_word), epoch, s) !=
+        hipSuccess)
+        return set_error(SHMEMX_EINVAL);
+    for (unsigned spins = 1; host_word[1] != epoch; ++spins) {
+        if ((spins & 1023) == 0 && hipStreamQuery(s) != hipErrorNotReady) {
+            SHMX_HIP(hipStreamSynchronize(s));   // done (or failed: FATAL)
+            if (host_word[1] != epoch) fatal("shmemx_checksum", "the checksum kernel finished without a result");
+            break;
+        }
+        __builtin_ia32_pause();
+    }
+    *out = host_word[0];
     return SHMEMX_OK;
 }
 

@@ -115,12 +115,13 @@ struct SignalFoldArgs {
 hipError_t launch_signal_fold(int type, int op, const SignalFoldArgs &a, hipStream_t stream);
 
 // Position-aware 64-bit checksum of n elements of `type` at device address
-// ptr (16-byte aligned) into *out (device memory or host-mapped page-locked
-// memory: the kernel stores it with a system-scope store), stream-ordered,
-// one launch.  Calls must not overlap in time (one arrival counter per process).
+// ptr (16-byte aligned) into out[0], then `epoch` into out[1] (device memory
+// or host-mapped page-locked memory: system-scope stores, in that order),
+// stream-ordered, one launch.  Calls must not overlap in time (one arrival
+// counter per process).
 constexpr int kChecksumMaxBlocks = 4096;
 hipError_t launch_checksum(int type, const void *ptr, size_t n, unsigned long long *out,
-                           hipStream_t stream);
+                           unsigned long long epoch, hipStream_t stream);
 
 // Tuning knobs for the fold kernels (initialised from the environment:
 // SHMEMX_FOLD_MAX_BLOCKS, SHMEMX_FOLD_NT, SHMEMX_FOLD_UNROLL; changed at run
