@@ -393,10 +393,21 @@ int direct_fused(int type, int op, char *tgt, size_t n, int start, int step, int
                     desc[i].src.off;
     fa.nins = P;
     fa.n = n;
+    // The host spins on a page-locked word instead of waiting for the
+    // stream: the kernel stores it itself when one workgroup did all the
+    // work (an array of at most 4 elements per lane of one block: the ISx
+    // nreduce = 1 call), a marker kernel after it otherwise.
+    const HostSignal sig = next_host_signal();
+    const bool self_signal = !stage_tgt && n <= kFusedTinyElems;
+    if (self_signal) {
+        fa.host_word = sig.word;
+        fa.host_value = sig.value;
+    }
     const double t0 = now_us();
     SHMX_HIP(launch_signal_fold(type, op, fa, s));   // reduce-op.c:217-250
     if (stage_tgt) SHMX_HIP(hipMemcpyAsync(tgt, scratch_tgt, n * sz, hipMemcpyDeviceToDevice, s));
-    SHMX_HIP(hipStreamSynchronize(s));
+    if (!self_signal) SHMX_HIP(launch_host_signal(sig, s));
+    wait_host_signal(sig, s);
     g_phase_us[kFold] += now_us() - t0;
     count_fused_call();
     switch (signal_error()) {
@@ -443,7 +454,9 @@ int direct_fused2(int type, int op, char *tgt, size_t n, int start, int step, in
     }
     const double t0 = now_us();
     SHMX_HIP(launch_signal_fold(type, op, fa, s));   // reduce-op.c:217-250
-    SHMX_HIP(hipStreamSynchronize(s));
+    const HostSignal sig = next_host_signal();       // a marker: the host spins, no stream wait
+    SHMX_HIP(launch_host_signal(sig, s));
+    wait_host_signal(sig, s);
     g_phase_us[kFold] += now_us() - t0;
     count_fused_twoshot_call();
     switch (signal_error()) {

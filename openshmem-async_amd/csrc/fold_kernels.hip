@@ -41,13 +41,28 @@ struct FoldArgs {
     size_t nvec;   // 16-B vectors in the aligned body
     size_t tail;   // scalar elements after it
     int peers;     // the inputs are other GPUs' HBM (launch_fold_peers)
+    // one-workgroup launches of launch_fold_signal: store sig_value here when done
+    unsigned long long *sig_word;
+    unsigned long long sig_value;
 };
+
+// The end of a one-workgroup fold that signals the host (launch_fold_signal):
+// every wave drains its stores, the workgroup meets, and lane 0 stores the
+// value with a system-scope release (the L2 written back first), so the host
+// that sees it may use the result at once.
+__device__ __forceinline__ void signal_host_done(const FoldArgs &args) {
+    if (!args.sig_word) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(args.sig_word, args.sig_value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 
 // NIN > 0: number of inputs fixed at compile time (all loads hoisted);
 // NIN == 0: runtime args.nins.
 template <typename T, int OP, int NIN, int UNROLL, int NT>
-__global__ __launch_bounds__(kBlock) void fold_kernel(FoldArgs args) {
+__device__ __forceinline__ void fold_body(const FoldArgs &args) {
     constexpr int E = 16 / sizeof(T);
     const int nins = NIN > 0 ? NIN : args.nins;
     const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
@@ -148,6 +163,12 @@ __global__ __launch_bounds__(kBlock) void fold_kernel(FoldArgs args) {
     }
 }
 
+template <typename T, int OP, int NIN, int UNROLL, int NT>
+__global__ __launch_bounds__(kBlock) void fold_kernel(FoldArgs args) {
+    fold_body<T, OP, NIN, UNROLL, NT>(args);
+    signal_host_done(args);
+}
+
 // 16-B vectors per lane per input for the runtime-nins kernel.
 constexpr int kUnrollN = 4;
 
@@ -238,8 +259,32 @@ static size_t grid_for(const FoldArgs &a, int unroll) {
     return blocks;
 }
 
+__global__ void host_signal_kernel(unsigned long long *word, unsigned long long value) {
+    if (threadIdx.x == 0) __hip_atomic_store(word, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 template <typename T, int OP, int NT>
-hipError_t launch_typed(const FoldArgs &a, hipStream_t stream) {
+hipError_t launch_typed_grid(const FoldArgs &a, hipStream_t stream);
+
+// A fold whose grid is not one workgroup cannot signal from inside (no
+// arrival counter): it runs without, and the marker kernel follows it.
+template <typename T, int OP, int NT>
+hipError_t launch_typed(const FoldArgs &a0, hipStream_t stream) {
+    if (!a0.sig_word) return launch_typed_grid<T, OP, NT>(a0, stream);
+    // the grid launch_typed_grid will use (fold_kernel in every case but
+    // the peers kernel, which never signals)
+    const int u = a0.nins != 2 ? kUnrollN : std::is_same<T, ld80>::value ? 4 : fold_tuning().unroll;
+    if (!a0.peers && grid_for(a0, u) == 1) return launch_typed_grid<T, OP, NT>(a0, stream);
+    FoldArgs a = a0;
+    a.sig_word = nullptr;
+    const hipError_t e = launch_typed_grid<T, OP, NT>(a, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(host_signal_kernel, dim3(1), dim3(64), 0, stream, a0.sig_word, a0.sig_value);
+    return hipGetLastError();
+}
+
+template <typename T, int OP, int NT>
+hipError_t launch_typed_grid(const FoldArgs &a, hipStream_t stream) {
     if (a.nins == 2) {
         // the two-input fold (reduce-op.c:231-235): the hot kernel.  The
         // soft-float long double kernels exist at unroll 4 only.
@@ -435,6 +480,32 @@ hipError_t launch_fold(int type, int op, void *out, const void *const *ins,
         ptrs[k + 1] = ins[k];
     }
     return dispatch(type, op, a, ptrs, nins + 1, n, stream);
+}
+
+hipError_t launch_fold_signal(int type, int op, void *out, const void *const *ins, int nins, size_t n,
+                              hipStream_t stream, const HostSignal &sig) {
+    if (!op_on_device(type, op) || nins < 1 || nins > kMaxFoldInputs || !out || !sig.word)
+        return hipErrorInvalidValue;
+    if (n == 0) return launch_host_signal(sig, stream);
+    FoldArgs a{};
+    a.out = out;
+    a.nins = nins;
+    a.sig_word = sig.word;
+    a.sig_value = sig.value;
+    const void *ptrs[kMaxFoldInputs + 1];
+    ptrs[0] = out;
+    for (int k = 0; k < nins; ++k) {
+        if (!ins[k]) return hipErrorInvalidValue;
+        a.ins[k] = ins[k];
+        ptrs[k + 1] = ins[k];
+    }
+    return dispatch(type, op, a, ptrs, nins + 1, n, stream);
+}
+
+hipError_t launch_host_signal(const HostSignal &sig, hipStream_t stream) {
+    if (!sig.word) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(host_signal_kernel, dim3(1), dim3(64), 0, stream, sig.word, sig.value);
+    return hipGetLastError();
 }
 
 hipError_t launch_fold_peers(int type, int op, void *out, const void *const *ins, int nins, size_t n,

@@ -27,6 +27,32 @@ bool op_on_device(int type, int op);   // this build has a HIP kernel for it
 hipError_t launch_fold(int type, int op, void *out, const void *const *ins,
                        int nins, size_t n, hipStream_t stream);
 
+// A host-visible completion signal: a page-locked, host-coherent word and
+// the value a launch stores there (system-scope release) once its work is
+// done.  A blocking call spins on the word instead of waiting for the stream:
+// 6.8 against 11.9 us for a one-element copy when the kernel stores it
+// itself, 9.6 with a one-thread marker kernel after it
+// (tools/latency_breakdown.hip, profiles/r03_latency_breakdown.txt).
+struct HostSignal {
+    unsigned long long *word;
+    unsigned long long value;
+};
+// The next signal value (the word is shared: blocking calls hold the
+// library lock), and the wait for it: spin until the word holds the value or
+// the stream has drained; after ~2 ms of spinning (long work) or an error
+// the stream wait takes over (and reports the error).
+HostSignal next_host_signal();
+void wait_host_signal(const HostSignal &sig, hipStream_t s);
+// launch_fold whose completion stores sig: the fold kernel itself when the
+// launch is one workgroup (every wave drains its stores, then lane 0 of the
+// workgroup stores the value with a system-scope release), otherwise a
+// one-thread marker kernel right after it.
+hipError_t launch_fold_signal(int type, int op, void *out, const void *const *ins, int nins, size_t n,
+                              hipStream_t stream, const HostSignal &sig);
+// The one-thread marker kernel alone: stores sig once everything enqueued
+// before it on the stream has completed.
+hipError_t launch_host_signal(const HostSignal &sig, hipStream_t stream);
+
 // launch_fold for inputs in other GPUs' HBM (DIRECT and SIGNAL): every lane
 // issues its loads of all inputs before folding any, so every peer's link is
 // busy at once; same results as launch_fold.
@@ -98,8 +124,15 @@ hipError_t launch_signal(const SignalArgs &a, hipStream_t stream);
 // the grid; every block drops stale peer lines (system acquire) and copies
 // the nseg byte ranges gsrc[k] -> gdst[k] (the peers' result slices); the
 // last block to finish does the exit handshake.
+// The fused one shot folds an array of at most this many elements (4 per
+// lane of one 256-lane workgroup) in the last workgroup to arrive alone.
+constexpr size_t kFusedTinyElems = 4 * 256;
 struct SignalFoldArgs {
     SignalArgs sig;
+    // the one shot's tiny case (one workgroup does all the work): stores
+    // host_value into host_word after its exit handshake (nullptr: no store)
+    unsigned long long *host_word;
+    unsigned long long host_value;
     unsigned int *gsync;
     void *out;
     const void *ins[kMaxFoldInputs];

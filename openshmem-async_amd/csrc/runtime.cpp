@@ -110,6 +110,34 @@ void trace(int level, const char *fmt, ...) {
     std::abort();
 }
 
+HostSignal next_host_signal() {
+    static unsigned long long *word = [] {
+        void *p = nullptr;
+        SHMX_HIP(hipHostMalloc(&p, sizeof(unsigned long long), hipHostMallocCoherent));
+        *static_cast<volatile unsigned long long *>(p) = 0;
+        return static_cast<unsigned long long *>(p);
+    }();
+    static unsigned long long value = 0;
+    return HostSignal{word, ++value};
+}
+
+void wait_host_signal(const HostSignal &sig, hipStream_t s) {
+    const volatile unsigned long long *w = sig.word;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned k = 1;; ++k) {
+        if (*w == sig.value) return;
+        __builtin_ia32_pause();
+        if ((k & 1023) == 0) {
+            // a drained stream (its work is complete whatever the word says)
+            // or an error: the stream wait settles it; long work: stop spinning
+            const hipError_t e = hipStreamQuery(s);
+            if (e != hipErrorNotReady) break;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+        }
+    }
+    SHMX_HIP(hipStreamSynchronize(s));
+}
+
 static int env_int(const char *a, const char *b, int dflt) {
     for (const char *k : {a, b}) {
         if (!k) continue;

@@ -123,7 +123,8 @@ __global__ __launch_bounds__(kBlock) void signal_fold_kernel(SignalFoldArgs a) {
     unsigned int *const count = a.gsync, *const gen = a.gsync + 1;
     // up to 4 elements per lane of one block: the last block to arrive folds
     // alone, and no block waits for a release or arrives at the exit
-    const bool tiny = a.n <= (size_t)4 * kBlock;
+    const bool tiny = a.n <= kFusedTinyElems;
+    static_assert(kFusedTinyElems == (size_t)4 * kBlock, "the tiny case is 4 elements per lane of one block");
     __shared__ int s_last;
     __shared__ unsigned int s_gen0;
     if (threadIdx.x == 0) {
@@ -185,8 +186,15 @@ __global__ __launch_bounds__(kBlock) void signal_fold_kernel(SignalFoldArgs a) {
     T *out = static_cast<T *>(a.out);
     if (tiny) {
         for (size_t i = threadIdx.x; i < a.n; i += kBlock) out[i] = fold_elem<T, OP>(a, i);
+        if (a.host_word) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's stores landed
         __syncthreads();
-        if (threadIdx.x == 0) peer_handshake(a.sig);   // reduce-op.c:250
+        if (threadIdx.x == 0) {
+            peer_handshake(a.sig);   // reduce-op.c:250
+            // this workgroup did all the work: tell the host (system-scope
+            // release: the L2 is written back first)
+            if (a.host_word)
+                __hip_atomic_store(a.host_word, a.host_value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         return;
     }
     const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x, nthr = (size_t)gridDim.x * kBlock;

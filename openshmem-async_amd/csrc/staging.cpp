@@ -238,8 +238,29 @@ static void reduce_blocking_impl(int type, int op, void *target, const void *sou
     if (trace_call) trace_reference_overlap(target, source, bytes);   // the caller's arrays
     if (tdev && sdev) {
         if (collective && bytes > kSmallHostBytes && !calls_agree(start, logstride, size, 1)) return;
-        reduce_device(type, op, target, source, nreduce, start, logstride, size, g_state.algo, s);
-        SHMX_HIP(hipStreamSynchronize(s));
+        if (plan.nmembers == 1 && !collective && !overlap(target, source, bytes)) {
+            // a one-member set is a copy (reduce-op.c:213-216), and the copy
+            // kernel tells the host itself when it is done (one workgroup;
+            // a marker kernel otherwise): no stream wait
+            const HostSignal sig = next_host_signal();
+            const void *in[1] = {source};
+            SHMX_HIP(launch_fold_signal(type, op, target, in, 1, (size_t)nreduce, s, sig));
+            wait_host_signal(sig, s);
+            return;
+        }
+        const int rc = reduce_device(type, op, target, source, nreduce, start, logstride, size,
+                                     g_state.algo, s);
+        // DIRECT and own-order GATHER over IPC wait for their own launches;
+        // the stream-ordered algorithms end with a marker the host spins on
+        const bool waits_itself = collective && (plan.algo == SHMEMX_ALGO_DIRECT ||
+                                                 (plan.algo == SHMEMX_ALGO_GATHER && g_state.ipc_only));
+        if (rc == SHMEMX_OK && !waits_itself) {
+            const HostSignal sig = next_host_signal();
+            SHMX_HIP(launch_host_signal(sig, s));
+            wait_host_signal(sig, s);
+        } else {
+            SHMX_HIP(hipStreamSynchronize(s));
+        }
         switch (signal_error()) {
         case 0: break;
         case 2: fatal("SIGNAL reduction", "a system fence before a device barrier missed an XCD");
@@ -263,10 +284,19 @@ static void reduce_blocking_impl(int type, int op, void *target, const void *sou
         char *bin = static_cast<char *>(g_state.bounce);
         char *bout = bin + kSmallHostBytes;
         if (!sdev) std::memcpy(bin, source, bytes);
-        const int rc = reduce_device(type, op, tdev ? target : bout, sdev ? source : bin, nreduce,
-                                     start, logstride, size, g_state.algo, s);
-        SHMX_HIP(hipStreamSynchronize(s));
-        if (!rc && !tdev) std::memcpy(target, bout, bytes);
+        void *t = tdev ? target : bout;
+        const void *in[1] = {sdev ? source : bin};
+        if (overlap(t, in[0], bytes)) {
+            const int rc = reduce_device(type, op, t, in[0], nreduce, start, logstride, size, g_state.algo, s);
+            SHMX_HIP(hipStreamSynchronize(s));
+            if (!rc && !tdev) std::memcpy(target, bout, bytes);
+            return;
+        }
+        // the copy kernel signals the host when its stores have landed
+        const HostSignal sig = next_host_signal();
+        SHMX_HIP(launch_fold_signal(type, op, t, in, 1, (size_t)nreduce, s, sig));
+        wait_host_signal(sig, s);
+        if (!tdev) std::memcpy(target, bout, bytes);
         return;
     }
     if (bytes > g_state.stage_bytes) {
@@ -301,11 +331,24 @@ static void reduce_blocking_impl(int type, int op, void *target, const void *sou
         void *dtgt = tdev ? target : g_state.stage_tgt;
         const int rc = reduce_device(type, op, dtgt, dsrc, nreduce, start, logstride, size,
                                      g_state.algo, s);
-        if (!rc && !tdev) {
-            const void *in[1] = {dtgt};
-            fold_chain(type, op, bout, in, 1, (size_t)nreduce, s);
+        if (!rc) {
+            // the last copy (or a marker) signals the host: no stream wait
+            const HostSignal sig = next_host_signal();
+            if (!tdev) {
+                const void *in[1] = {dtgt};
+                SHMX_HIP(launch_fold_signal(type, op, bout, in, 1, (size_t)nreduce, s, sig));
+            } else {
+                SHMX_HIP(launch_host_signal(sig, s));
+            }
+            wait_host_signal(sig, s);
+        } else {
+            SHMX_HIP(hipStreamSynchronize(s));
         }
-        SHMX_HIP(hipStreamSynchronize(s));
+        switch (signal_error()) {
+        case 0: break;
+        case 2: fatal("SIGNAL reduction", "a system fence before a device barrier missed an XCD");
+        default: fatal("SIGNAL reduction", "a member never reached the device barrier");
+        }
         if (!rc && !tdev) std::memcpy(target, bout, bytes);
         return;
     }
