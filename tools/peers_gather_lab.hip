@@ -86,11 +86,23 @@ struct Segs {
     f64x2 *dst[P];
 };
 
-// nvec vectors per segment, one chunk of 256 * U vectors per block
+// nvec vectors per segment, one chunk of 256 * U vectors per block.  IL = 0:
+// segment from blockIdx.y; IL = 1: consecutive blocks take the segments in
+// turn; IL = R > 1: runs of R consecutive blocks per segment, in turn (every
+// segment still has blocks resident at once while R * nseg stays under the
+// resident grid, ~2048 blocks).
 template <int U, int IL>
 __global__ __launch_bounds__(256) void gather(Segs s, int nseg, size_t nvec) {
-    const int seg = IL ? blockIdx.x % nseg : blockIdx.y;
-    const size_t bx = IL ? blockIdx.x / nseg : blockIdx.x;
+    int seg;
+    size_t bx;
+    if (IL == 0) {
+        seg = blockIdx.y;
+        bx = blockIdx.x;
+    } else {
+        const size_t run = blockIdx.x / IL, in_run = blockIdx.x % IL;
+        seg = run % nseg;
+        bx = (run / nseg) * IL + in_run;
+    }
     const size_t v0 = bx * 256 * U + threadIdx.x;
     if (v0 >= nvec) return;
     f64x2 x[U];
@@ -149,7 +161,7 @@ void L_gather(hipStream_t s) {
     }
     const unsigned bx = (unsigned)(g_seg / (256 * U));
     if (IL)
-        hipLaunchKernelGGL((gather<U, 1>), dim3(bx * 7), dim3(256), 0, s, sg, 7, g_seg);
+        hipLaunchKernelGGL((gather<U, IL>), dim3(bx * 7), dim3(256), 0, s, sg, 7, g_seg);
     else
         hipLaunchKernelGGL((gather<U, 0>), dim3(bx, 7), dim3(256), 0, s, sg, 7, g_seg);
 }
@@ -182,11 +194,18 @@ int main() {
         {"peers_u2_b512", fold_bytes, L_peers<2, 512>},
         {"peers_u1_b512", fold_bytes, L_peers<1, 512>},
         {"rt_u4 (runtime loop)", fold_bytes, L_rt<4>},
-        {"gather_u4_il (shipped)", gather_bytes, L_gather<4, 1>},
+        {"gather_u4_il (round 2)", gather_bytes, L_gather<4, 1>},
         {"gather_u8_il", gather_bytes, L_gather<8, 1>},
-        {"gather_u2_il", gather_bytes, L_gather<2, 1>},
+        {"gather_u2_il (round 3)", gather_bytes, L_gather<2, 1>},
         {"gather_u4_y", gather_bytes, L_gather<4, 0>},
         {"gather_u8_y", gather_bytes, L_gather<8, 0>},
+        {"gather_u8_run32", gather_bytes, L_gather<8, 32>},
+        {"gather_u8_run64", gather_bytes, L_gather<8, 64>},
+        {"gather_u8_run128", gather_bytes, L_gather<8, 128>},
+        {"gather_u8_run256", gather_bytes, L_gather<8, 256>},
+        {"gather_u4_run128", gather_bytes, L_gather<4, 128>},
+        {"gather_u4_run256", gather_bytes, L_gather<4, 256>},
+        {"gather_u2_run256", gather_bytes, L_gather<2, 256>},
         {"copy_u4 (same bytes, contiguous)", gather_bytes, L_copy<4>},
     };
     hipStream_t s;
