@@ -531,16 +531,18 @@ hipError_t launch_fold_peers(int type, int op, void *out, const void *const *ins
 // DIRECT's all-gather phase: up to kMaxFoldInputs byte ranges (each a slice
 // of a peer's result, read over xGMI) copied into this PE's target by ONE
 // launch, so the reads from all peers are in flight at once (one copy per
-// peer would serialise the links).  Consecutive blocks take the segments in
-// turn: workgroups are dispatched in block order, and with the segment as
-// the slow index (blockIdx.y) the first ~2048 resident blocks would all read
-// the same peer, one link at a time.  On local HBM (one GPU) this costs 4 %
-// against the y-major order (80.5 vs 77.4 us, 7 x 32 MiB), and runs of 16
-// blocks per segment cost 15 % (89.3 us): profiles/r02c_pmc_kernels.json.
-// Two vectors per lane per step, not four: interleaved, 79.3 against 82.7 us
-// warm, 81.4 against 85.0 cold (tools/peers_gather_lab.hip,
-// profiles/r03_peers_gather_lab.txt); the resident grid still keeps ~16 MiB
-// of loads in flight, far more than the links' bandwidth-latency product.
+// peer would serialise the links).  Workgroups are dispatched in block
+// order, so the block -> segment map decides which links are busy: with the
+// segment as the slow index (blockIdx.y) the first ~2048 resident blocks
+// would all read the same peer, one link at a time.  Consecutive RUNS of
+// kGatherRun blocks take the segments in turn: a resident grid of ~2048
+// blocks still spans every segment (kGatherRun x 7 = 1792), and each run
+// streams 8 MiB contiguous per segment.  Measured on local HBM, 7 x 32 MiB
+// (profiles/r02c_pmc_kernels.json, profiles/r03_peers_gather_lab*.txt):
+// blockIdx.y-major 77.4 us; single blocks in turn (round 2) 80.5, with 2
+// vectors per lane 79.3; runs of 16-64 blocks 82-89; runs of 256 blocks
+// with 8 vectors per lane 72.5 us warm, 74.9 cold (6.48 / 6.27 TB/s), the
+// fastest shape of all, y-major included.
 namespace {
 
 struct CopySeg {
@@ -551,13 +553,16 @@ struct CopySeg {
 struct GatherArgs {
     CopySeg seg[kMaxFoldInputs];
     int nseg;
+    unsigned run;   // blocks per run (divides the blocks per segment)
 };
 
-constexpr int kGatherUnroll = 2;
+constexpr int kGatherUnroll = 8;
+constexpr unsigned kGatherRun = 256;
 
 __global__ __launch_bounds__(kBlock) void gather_kernel(GatherArgs a) {
-    const CopySeg sg = a.seg[blockIdx.x % a.nseg];   // the segments in turn
-    const size_t bx = blockIdx.x / a.nseg, nbx = gridDim.x / a.nseg;
+    const unsigned r = blockIdx.x / a.run;   // the run, and its segment
+    const CopySeg sg = a.seg[r % a.nseg];
+    const size_t bx = (size_t)(r / a.nseg) * a.run + blockIdx.x % a.run, nbx = gridDim.x / a.nseg;
     const size_t tid = bx * kBlock + threadIdx.x;
     const size_t nthr = nbx * kBlock;
     const uintptr_t d = reinterpret_cast<uintptr_t>(sg.dst);
@@ -605,10 +610,15 @@ hipError_t launch_gather(const void *const *srcs, void *const *dsts, const size_
         most = bytes[i] > most ? bytes[i] : most;
     }
     if (!k) return hipSuccess;
+    // blocks per segment: one chunk of kBlock x kGatherUnroll vectors each
+    // (a grid-stride loop beyond 65536), rounded up to whole runs
     size_t bx = (most / 16 + (size_t)kBlock * kGatherUnroll - 1) / ((size_t)kBlock * kGatherUnroll);
     if (bx < 1) bx = 1;
-    if (bx > 65535) bx = 65535;
+    if (bx > 65536) bx = 65536;
+    const size_t run = bx < kGatherRun ? bx : kGatherRun;
+    bx = (bx + run - 1) / run * run;
     a.nseg = k;
+    a.run = (unsigned)run;
     hipLaunchKernelGGL(gather_kernel, dim3((unsigned)(bx * k)), dim3(kBlock), 0, stream, a);
     return hipGetLastError();
 }
