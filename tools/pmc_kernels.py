@@ -94,6 +94,15 @@ timed("foldP8_peers_double_sum", lambda: shm.fold_n("double", "sum", out, ins, m
       9 * 8 * m, blocks(m // 2, 2))
 del ins, out
 
+# configs[2]'s own shape for DIRECT's fold: 32 Mi doubles on 8 PEs, each PE
+# folds one 4 Mi-double slice from 8 separate arrays (the peers' sources)
+n = 4 * Mi
+ins = [torch.rand(n, dtype=torch.float64, device="cuda") for _ in range(8)]
+out = torch.empty(n, dtype=torch.float64, device="cuda")
+timed("foldP8_peers_slice4Mi", lambda: shm.fold_n("double", "sum", out, ins, n, s.cuda_stream, peers=True),
+      9 * 8 * n, blocks(n // 2, 4))
+del ins, out
+
 n = 4 * Mi
 ws = torch.rand(8 * n, dtype=torch.float64, device="cuda")
 shard = [ws[i * n:(i + 1) * n] for i in range(8)]
