@@ -110,6 +110,8 @@ void trace(int level, const char *fmt, ...) {
     std::abort();
 }
 
+static int env_int(const char *a, const char *b, int dflt);
+
 HostSignal next_host_signal() {
     static unsigned long long *word = [] {
         void *p = nullptr;
@@ -122,6 +124,18 @@ HostSignal next_host_signal() {
 }
 
 void wait_host_signal(const HostSignal &sig, hipStream_t s) {
+    // Only a blocking entry point spins on the word and returns the moment it
+    // arrives.  Anywhere else (DIRECT under the stream-ordered API) the caller
+    // may wait for the stream right after, and a hipStreamSynchronize entered
+    // while a kernel is still retiring costs ~9 us more than the retiring
+    // itself; polling hipStreamQuery until the stream is idle is worse still
+    // (profiles/r03_latency_ab.txt): there the stream wait is the wait.
+    // $SHMEMX_HOST_SIGNAL=0: stream waits everywhere (A/B and a way out).
+    static const bool on = env_int("SHMEMX_HOST_SIGNAL", nullptr, 1) != 0;
+    if (!on || !g_state.return_on_signal) {
+        SHMX_HIP(hipStreamSynchronize(s));
+        return;
+    }
     const volatile unsigned long long *w = sig.word;
     const auto t0 = std::chrono::steady_clock::now();
     for (unsigned k = 1;; ++k) {

@@ -201,8 +201,21 @@ void reduce_blocking(int type, int op, void *target, const void *source,
     reduce_blocking_impl(type, op, target, source, nreduce, start, logstride, size, true);
 }
 
+static void reduce_blocking_impl2(int type, int op, void *target, const void *source, int nreduce,
+                                  int start, int logstride, int size, bool trace_call);
+
+// A blocking call returns as soon as its work's host signal arrives.
 static void reduce_blocking_impl(int type, int op, void *target, const void *source, int nreduce,
                                  int start, int logstride, int size, bool trace_call) {
+    struct Early {
+        Early() { g_state.return_on_signal = true; }
+        ~Early() { g_state.return_on_signal = false; }
+    } early;
+    reduce_blocking_impl2(type, op, target, source, nreduce, start, logstride, size, trace_call);
+}
+
+static void reduce_blocking_impl2(int type, int op, void *target, const void *source, int nreduce,
+                                  int start, int logstride, int size, bool trace_call) {
     if (ensure_init()) {
         trace(LOG_FATAL, "reduction called before shmem_init with npes > 1");
         return;
@@ -250,15 +263,19 @@ static void reduce_blocking_impl(int type, int op, void *target, const void *sou
         }
         const int rc = reduce_device(type, op, target, source, nreduce, start, logstride, size,
                                      g_state.algo, s);
-        // DIRECT and own-order GATHER over IPC wait for their own launches;
-        // the stream-ordered algorithms end with a marker the host spins on
+        // DIRECT and own-order GATHER over IPC return with their work done
+        // (host barriers, or the fused launch's host signal): no stream wait
+        // on top — a hipStreamSynchronize entered while a kernel is still
+        // retiring costs ~9 us more than the kernel's remaining time
+        // (profiles/r03_latency_ab.txt).  The stream-ordered algorithms end
+        // with a marker the host spins on.
         const bool waits_itself = collective && (plan.algo == SHMEMX_ALGO_DIRECT ||
                                                  (plan.algo == SHMEMX_ALGO_GATHER && g_state.ipc_only));
         if (rc == SHMEMX_OK && !waits_itself) {
             const HostSignal sig = next_host_signal();
             SHMX_HIP(launch_host_signal(sig, s));
             wait_host_signal(sig, s);
-        } else {
+        } else if (rc != SHMEMX_OK) {
             SHMX_HIP(hipStreamSynchronize(s));
         }
         switch (signal_error()) {

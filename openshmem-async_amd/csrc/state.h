@@ -31,6 +31,9 @@ struct State {
     // communicator and runs the collective schedules, so a one-GPU box can
     // execute every RCCL call of the path
     bool force_collective = false;
+    // inside a blocking entry point: wait_host_signal returns as soon as the
+    // work's host signal arrives, without seeing the stream idle
+    bool return_on_signal = false;
     // grow-only device workspaces
     void *ws = nullptr;        // A2A shard receive area / GATHER sources
     size_t ws_bytes = 0;
