@@ -61,6 +61,12 @@ def main():
     def measure():
         out = {"barrier_all": per_call(shm.barrier_all)}
 
+        def signal():
+            shm.reduce_on_stream("longlong", "sum", ht, hs, 1, 0, 0, world, "signal")
+            torch.cuda.synchronize()
+        if os.environ.get("PROBE_SIGNAL_FIRST") == "1":   # order check (shared-GPU artefacts)
+            out["signal_n1_first"] = per_call(signal)
+
         def direct():
             shm.reduce_on_stream("longlong", "sum", ht, hs, 1, 0, 0, world, "direct")
             torch.cuda.synchronize()
@@ -71,9 +77,6 @@ def main():
         out["direct_n1_phases"] = {k.replace("_us", ""): round(maxr(st[k] / calls), 1)
                                    for k in shm.DIRECT_PHASES if st[k]}
 
-        def signal():
-            shm.reduce_on_stream("longlong", "sum", ht, hs, 1, 0, 0, world, "signal")
-            torch.cuda.synchronize()
         out["signal_n1"] = per_call(signal)
         out["blocking_n1_device"] = per_call(lambda: shm.to_all("longlong", "sum", tgt1, src1, 1, 0, 0, world))
         return out
