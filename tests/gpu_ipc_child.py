@@ -584,6 +584,13 @@ elif scenario == "configs":
         if not torch.equal(got.view(torch.int64), want.view(torch.int64)):
             bad = int((got.view(torch.int64) != want.view(torch.int64)).sum())
             fails.append(f"config {t} {op} n={n}: {bad} elements differ")
+        # and 64 Ki sampled elements against the oracle itself (the restated
+        # reduce-op.c fold, PE_start's order), not only torch's fold
+        smp = torch.arange(0, n, n // 65536, device="cuda")
+        srcs = np.stack([gen(t, q, n, salt)[smp].cpu().numpy() for q in range(npes)])
+        ref = oracle.reduce_sim(t, op, srcs, 0, 0, npes)[0]
+        if not same_bits(got[smp].cpu().numpy(), ref):
+            fails.append(f"config {t} {op} n={n}: sampled elements differ from the oracle")
         if not shm.verify(t, BIG_TGT, n, 0, 0, npes):
             fails.append(f"config {t} {op} n={n}: targets differ across PEs")
         del got, want
@@ -643,6 +650,13 @@ elif scenario == "configs8":
         if not torch.equal(got.view(iv), want.view(iv)):
             bad = int((got.view(iv) != want.view(iv)).sum())
             fails.append(f"configs8 {t} n={n} {algo}: {bad} elements differ")
+        # up to 64 Ki sampled elements against the oracle itself (each PE's
+        # own order for GATHER, PE_start's otherwise)
+        smp = torch.arange(0, n, max(1, n // 65536), device="cuda")
+        srcs = np.stack([gen(t, q, n, salt)[smp].cpu().numpy() for q in range(npes)])
+        ref = oracle.reduce_sim(t, "sum", srcs, 0, 0, npes)[pe if algo == "gather" else 0]
+        if not same_bits(got[smp].cpu().numpy(), ref):
+            fails.append(f"configs8 {t} n={n} {algo}: sampled elements differ from the oracle")
         if algo != "gather" and not shm.verify(t, BIG_TGT, n, 0, 0, npes):
             fails.append(f"configs8 {t} n={n} {algo}: targets differ across PEs")
         del got, want
