@@ -97,15 +97,16 @@ def read(ptr, t, n):
     return a
 
 
-def run_case(t, op, n, st, algo, mode, seed):
-    """One collective call; every PE runs the same sequence, non-members skip."""
+def run_case(t, op, n, st, algo, mode, seed, expect_algo=None):
+    """One collective call; every PE runs the same sequence, non-members skip.
+    expect_algo: the algorithm `auto` resolved to, for the fold order."""
     global ncases
     srcs = oracle.sources(t, 1, npes, n, base_seed=seed)
     if not member(*st):
         return
     ncases += 1
     mine = np.ascontiguousarray(srcs[pe])
-    want = expected(t, op, srcs, st, algo)
+    want = expected(t, op, srcs, st, expect_algo or algo)
     sz = mine.itemsize
     tag = f"{t} {op} n={n} set={st} algo={algo} mode={mode}"
     print(tag, flush=True)   # progress, in the PE's log
@@ -512,6 +513,21 @@ elif scenario == "soak":
             continue                               # not a valid (set, algo) pair here
         seed += 1
         run_case(t, op, n, st, algo, mode, seed)
+elif scenario == "autotable":
+    # $SHMEMX_AUTO_FULL / $SHMEMX_AUTO_PARTIAL (runtime.cpp make_plan): the
+    # plan `auto` resolves to for each case of $AUTO_EXPECT ([type, op, n,
+    # PE_start, logPE_stride, PE_size, expected algorithm] rows), then the
+    # call itself through `auto`, against the oracle
+    for t, op, n, st0, st1, st2, want_algo in json.loads(os.environ["AUTO_EXPECT"]):
+        st = (st0, st1, st2)
+        seed += 1
+        if not member(*st):
+            continue
+        got_algo = shm.plan(t, op, n, *st, pe, npes, "auto").algo
+        extra.setdefault("plans", []).append([t, op, n, list(st), got_algo])
+        if got_algo != want_algo:
+            fails.append(f"auto plan {t} {op} n={n} set={st}: {got_algo}, want {want_algo}")
+        run_case(t, op, n, st, "auto", "device", seed, expect_algo=got_algo)
 elif scenario == "config0":
     # BASELINE.json configs[0]: shmem_int_sum_to_all, nreduce = 1024, on 2 PEs
     # (the reference's "oshrun loopback"), through the C entry point itself

@@ -137,6 +137,41 @@ def test_baseline_config0_int_sum_1024_two_pes(tmp_path, transport, heap):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("table", ["set", "bad"])
+def test_auto_table_from_environment(tmp_path, table):
+    """`auto`'s per-size choice read from $SHMEMX_AUTO_FULL /
+    $SHMEMX_AUTO_PARTIAL (the values the N > 1 bench prints as
+    extras.auto_recommendation.env), on 4 PE processes over the RCCL
+    transport with the RCCL test double: the plan each size resolves to, a
+    cut RCCL cannot serve (long xor) falling back to the built-in rule, and
+    every call bit-exact against the oracle.  "bad": an unparsable value
+    leaves the built-in rule alone."""
+    fake = os.path.join(HERE, "native", "libfake_rccl.so")
+    KiB = 1024
+    if table == "set":
+        env = {"SHMEMX_AUTO_FULL": f"0:gather,{4 * KiB}:a2a,{64 * KiB}:rccl",
+               "SHMEMX_AUTO_PARTIAL": "0:direct"}
+        expect = [["double", "sum", 16, 0, 0, 4, "gather"],          # 128 B
+                  ["double", "sum", 1024, 0, 0, 4, "a2a"],           # 8 KiB
+                  ["double", "sum", 65536, 0, 0, 4, "rccl"],         # 512 KiB
+                  ["long", "xor", 65536, 0, 0, 4, "a2a"],            # no RCCL op: built-in rule
+                  ["int", "max", 3000, 0, 0, 4, "a2a"],
+                  ["double", "sum", 4099, 0, 1, 2, "direct"],        # every other PE
+                  ["float", "min", 777, 1, 0, 3, "direct"]]
+    else:
+        env = {"SHMEMX_AUTO_FULL": "fast please", "SHMEMX_AUTO_PARTIAL": "0:signal"}
+        expect = [["double", "sum", 16, 0, 0, 4, "allreduce"],
+                  ["double", "sum", 1 << 20, 0, 0, 4, "rccl"],
+                  ["long", "xor", 4096, 0, 0, 4, "a2a"],
+                  ["double", "sum", 4099, 0, 1, 2, "a2a"]]
+    env.update({"SHMEMX_TRANSPORT": "rccl", "FAKE_RCCL": fake, "AUTO_EXPECT": json.dumps(expect)})
+    reports = run_pes(tmp_path, 4, "autotable", env, timeout=300)
+    for r in reports:
+        assert not r["fails"], f"PE {r['pe']}: {r['fails']}"
+        assert r["ncases"] > 0
+
+
+@pytest.mark.gpu
 def test_ipc_eight_pe_baseline_configs(tmp_path):
     """BASELINE.json configs[2] (double sum, 32 Mi, 8 PEs) on DIRECT, SIGNAL
     and own-order GATHER, and configs[4] (float sum sweep 4 Ki .. 256 Mi, 8
