@@ -156,6 +156,11 @@ bool create(size_t bytes, const Backend &be) {
     g_pending.store(0);
     g_req.store(kIdle);
     g_service_up = pthread_create(&g_service, nullptr, service_main, nullptr) == 0;
+    // a forked child has no service thread: its faults copy in place (and
+    // fail loudly if the GPU runtime is unusable there) instead of waiting
+    // for a thread that does not exist
+    static bool atfork_set = false;
+    if (!atfork_set) atfork_set = pthread_atfork(nullptr, nullptr, [] { g_service_up = false; }) == 0;
     if (!g_installed) {
         struct sigaction sa;
         std::memset(&sa, 0, sizeof sa);

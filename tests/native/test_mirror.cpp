@@ -5,6 +5,7 @@
 // writes are checked against a model: after every step the host view reads
 // what the model says, flush pushes exactly the blocks the host stored to,
 // and nothing else crosses the "PCIe" backend.
+#include <sys/wait.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -203,6 +204,27 @@ int main(int argc, char **argv) {
         truth[racing] = 77;
         CHECK(phase.load() == 3 && M::state_of(base) == M::HOST_NEWER);
         CHECK(M::flush(base, 1) == 1 && g_dev[racing] == 77 && g_dev[base] == 1);
+    }
+
+    // (3) A forked child has no fault service thread: its fault on a
+    // device-newer block copies in place instead of waiting forever.
+    {
+        const size_t base = 70 * M::kBlock;
+        M::flush(base, M::kBlock);
+        for (size_t i = base; i < base + M::kBlock; ++i) {
+            g_dev[i] = (unsigned char)(i * 3 + 1);
+            truth[i] = g_dev[i];
+        }
+        M::device_wrote(base, M::kBlock);
+        const pid_t pid = fork();
+        if (pid == 0) {
+            alarm(10);   // a hang fails the check instead of the suite
+            const bool ok = h[base + 5] == truth[base + 5] && M::state_of(base) == M::CLEAN;
+            _exit(ok ? 0 : 3);
+        }
+        int status = 0;
+        CHECK(pid > 0 && waitpid(pid, &status, 0) == pid);
+        CHECK(WIFEXITED(status) && WEXITSTATUS(status) == 0);
     }
 
     // random interleavings against the model
