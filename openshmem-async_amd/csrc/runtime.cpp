@@ -402,6 +402,12 @@ static std::vector<AutoCut> parse_auto_table(const char *var) {
     return cuts;
 }
 
+// Set while reduce_device plans a call being captured into a hipGraph:
+// the table's DIRECT (host barriers, refused under capture) then falls back
+// to the built-in rule, so captured calls still plan.  Every PE of a set
+// must capture its calls alike (as for every stream-ordered collective).
+static thread_local bool t_planning_capture = false;
+
 // The table's algorithm for an array of `bytes` per PE, or AUTO.
 static int auto_table_algo(bool world, long long bytes) {
     static const std::vector<AutoCut> full = parse_auto_table("SHMEMX_AUTO_FULL");
@@ -434,7 +440,7 @@ int make_plan(int type, int op, int nreduce, int start, int logstride,
     if (algo == SHMEMX_ALGO_AUTO && P > 1) {
         const int t = auto_table_algo(world, n * sz);
         const bool rccl_ok = world && rccl_native(type, op) && !g_state.ipc_only;
-        const bool pull_ok = node::up() && P <= kMaxFoldInputs;
+        const bool pull_ok = node::up() && P <= kMaxFoldInputs && !t_planning_capture;
         if (((t == SHMEMX_ALGO_RCCL || t == SHMEMX_ALGO_ALLREDUCE) && rccl_ok) ||
             (t == SHMEMX_ALGO_A2A && !g_state.ipc_only) || (t == SHMEMX_ALGO_DIRECT && pull_ok) ||
             t == SHMEMX_ALGO_GATHER)
@@ -585,8 +591,10 @@ int reduce_device(int type, int op, void *target, const void *source,
                          int nreduce, int start, int logstride, int size,
                          int algo, hipStream_t s) {
     shmemx_plan_t p;
+    t_planning_capture = algo == SHMEMX_ALGO_AUTO && stream_capturing(s);
     int rc = make_plan(type, op, nreduce, start, logstride, size, g_state.pe,
                        g_state.npes, algo, &p);
+    t_planning_capture = false;
     if (rc) return set_error(rc);
     if (nreduce == 0) return SHMEMX_OK;
     const bool collective = size > 1 || g_state.force_collective;
