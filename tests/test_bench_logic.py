@@ -1,0 +1,64 @@
+"""CPU checks of bench.py's host-side logic that the driver's multi-GPU run
+depends on: the auto_recommendation table built from the crossover and
+partial-set extras, and the $SHMEMX_AUTO_* values it prints (the library's
+parser accepts exactly this form; tests/test_gpu_ipc.py::
+test_auto_table_from_environment runs it)."""
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+@pytest.fixture(scope="module")
+def bench():
+    import bench as b
+    return b
+
+
+def table(us, ok=None):
+    """crossover-style {algo: {str(n): value}} from {algo: [v per bucket]}."""
+    sizes = [str(n) for n in (1, 1 << 9, 1 << 16, 1 << 19, 1 << 24)]
+    t = {a: dict(zip(sizes, v)) for a, v in us.items()}
+    c = {a: {n: True for n in sizes} for a in us}
+    for (a, i) in ok or ():
+        c[a][sizes[i]] = False
+    return t, c
+
+
+def test_auto_recommendation_full_and_partial(bench):
+    us, ok = table({"allreduce": [10, 12, 40, 200, 5000],
+                    "rccl": [30, 31, 45, 150, 3000],
+                    "direct": [20, 11, 35, 160, 2500],
+                    "signal": [9, 9, 30, 140, 2400],      # fastest, but never a table choice
+                    "a2a": ["shmemx_reduce_on_stream(double,sum): ENOTSUP"] * 5},
+                   ok=[("direct", 4)])                   # a wrong result at 128 MiB: excluded
+    half_us, half_ok = table({"a2a": [15, 16, 50, 300, 9000], "direct": [14, 20, 40, 250, 8000],
+                              "gather": [30, 30, 60, 400, 12000], "signal": [13, 13, 35, 240, 7000]})
+    rec = bench.auto_recommendation({"us_per_call": us, "correct": ok},
+                                    {"first_half_us_per_call": half_us, "first_half_correct": half_ok,
+                                     "every_other_us_per_call": half_us, "every_other_correct": half_ok})
+    full = rec["full"]
+    assert full["8B"]["fastest"] == "signal" and full["8B"]["table"] == "allreduce"
+    assert full["4KiB"]["table"] == "direct"
+    assert full["512KiB"]["table"] == "direct"
+    assert full["4MiB"]["table"] == "rccl"
+    assert full["128MiB"]["table"] == "rccl"              # direct's 2500 us cell was wrong
+    assert "a2a" not in full["8B"]["us"]                   # error strings are not timings
+    # cut points between buckets at the geometric mean of their byte sizes
+    assert rec["env"]["SHMEMX_AUTO_FULL"] == "0:allreduce,181:direct,1482910:rccl"
+    assert rec["env"]["SHMEMX_AUTO_PARTIAL"] == "0:direct,181:a2a,46340:direct"
+    for shape in ("half", "strided"):
+        assert rec[shape]["8B"]["table"] == "direct" and rec[shape]["8B"]["fastest"] == "signal"
+
+
+def test_auto_recommendation_env_is_parseable_form(bench):
+    """bytes ascending, one algorithm per cut, names the library accepts."""
+    us, ok = table({"allreduce": [1, 1, 1, 1, 1]})
+    rec = bench.auto_recommendation({"us_per_call": us, "correct": ok}, "needs N >= 4")
+    assert rec["env"] == {"SHMEMX_AUTO_FULL": "0:allreduce"}
+    assert set(rec) == {"full", "env"}
+    rec = bench.auto_recommendation("error: boom", None)
+    assert rec == {"env": {}}
