@@ -22,10 +22,13 @@
  * Floating point is IEEE binary32/64 via SSE, x87 80-bit for long double, and
  * C99 complex (double complex * uses libgcc __muldc3, as the reference does).
  *
- * The reference itself cannot be built in this container (its reduce-op.c
+ * The reference's fold cannot be built in this container (its reduce-op.c
  * pulls in comms/gasnet/comms-shared.h:46 -> <gasnet.h>, an external library
- * that is not installed); see DESIGN.md "Oracle" for how this restatement is
- * pinned instead.
+ * that is not installed).  Its element ops (:71-150) need only <complex.h>:
+ * oracle/build_ref.sh compiles them from the reference's text into
+ * oracle/_ref/libref_ops.so, and tests/test_ref_ops.py holds the ops below to
+ * that build bit for bit (fixture: tests/golden/ref_element_ops.json).  See
+ * DESIGN.md §3 for the rest of the pinning.
  */
 #ifndef _GNU_SOURCE
 #define _GNU_SOURCE
@@ -80,7 +83,29 @@ ORC_FP_OPS(float, float)
 ORC_FP_OPS(double, double)
 ORC_FP_OPS(longdouble, ldouble)
 ORC_CPLX_OPS(complexd, cdouble)
-ORC_CPLX_OPS(complexf, cfloat)
+/* complex float sum, component by component.  `a + b` on float complex lets
+ * gcc -O2 commute the adds (b.im + a.im), and which operand an SSE add puts
+ * first decides only which NaN payload survives a NaN + NaN.  The reference
+ * built with its configure defaults (-std=c99, no -O) keeps a's in both
+ * components: SSE returns its first operand, quieted, when that is a NaN,
+ * else the second, quieted, when that is one.  That choice is made here
+ * explicitly, and tests/test_ref_ops.py holds this file to that build
+ * (oracle/_ref, reduce-op.c:71-93 compiled from the reference's text).    */
+static float orc_addf_first(float a, float b)
+{
+    uint32_t u;
+    if (a != a) { memcpy(&u, &a, 4); u |= 0x00400000u; memcpy(&a, &u, 4); return a; }
+    if (b != b) { memcpy(&u, &b, 4); u |= 0x00400000u; memcpy(&b, &u, 4); return b; }
+    return a + b;
+}
+static cfloat orc_sum_complexf(cfloat a, cfloat b)
+{
+    float c[2] = {orc_addf_first(crealf(a), crealf(b)), orc_addf_first(cimagf(a), cimagf(b))};
+    cfloat r;
+    memcpy(&r, c, sizeof r);
+    return r;
+}
+static cfloat orc_prod_complexf(cfloat a, cfloat b) { return a * b; }
 
 /* ----------------------------------------------------- linear fold ------ */
 /* fold_<T>: the body of the per-peer loop, reduce-op.c:224-245.  `peer` is the

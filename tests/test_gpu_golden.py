@@ -75,3 +75,52 @@ def test_gpu_reproduces_golden_special_values(cuda, shm):
                 assert got[m].tobytes() == want[m].tobytes(), key
             else:
                 assert got.view(ut).tolist() == c[pe], (key, pe)
+
+
+def _nan_rule_equal(got, want, ft):
+    """IEEE sum/prod: NaN where the reference has NaN (the payload is the
+    hardware's choice), every other value bit for bit."""
+    g, w = got.view(ft), want.view(ft)
+    if not np.array_equal(np.isnan(g), np.isnan(w)):
+        return False
+    m = ~np.isnan(w)
+    return g[m].tobytes() == w[m].tobytes()
+
+
+@pytest.mark.parametrize("peers", [False, True])
+def test_gpu_matches_reference_element_ops(cuda, shm, oracle, peers):
+    """The GPU's element ops against the REFERENCE'S OWN: tests/golden/
+    ref_element_ops.json holds what reduce-op.c:71-150, compiled from its text
+    (oracle/build_ref.sh), computes on special values and random bits for all
+    44 pairs, both operand orders (PE 0 and PE 1 of a 2-PE reduction).  Through
+    the runtime-nins fold and, with peers=True, the every-input-in-flight fold
+    DIRECT and SIGNAL use.  Bit for bit, except the NaN payload of an IEEE
+    float/double (or complex component) sum or product; long double (soft x87)
+    is bit for bit, NaN payloads included."""
+    import base64
+
+    import torch
+    from gpu_util import empty_like_dev, value_bytes
+    with open(os.path.join(GOLDEN, "ref_element_ops.json")) as f:
+        g = json.load(f)["cases"]
+    checked = 0
+    for t, c in g.items():
+        dt = np.dtype(oracle.NP_DTYPE[t])
+        a = np.frombuffer(base64.b64decode(c["a"]), dtype=dt).copy()
+        b = np.frombuffer(base64.b64decode(c["b"]), dtype=dt).copy()
+        da, db = to_dev(torch, a), to_dev(torch, b)
+        for op, o in c["ops"].items():
+            assert shm.op_on_device(t, op), (t, op)
+            for ins, key in (([da, db], "ab"), ([db, da], "ba")):
+                out = empty_like_dev(torch, a)
+                shm.fold_n(t, op, out, ins, a.size, peers=peers)
+                torch.cuda.synchronize()
+                got = from_dev(out, dt)
+                want = np.frombuffer(base64.b64decode(o[key]), dtype=dt)
+                if op in ("sum", "prod") and t in ("float", "double", "complexd", "complexf"):
+                    ft = np.float32 if t in ("float", "complexf") else np.float64
+                    assert _nan_rule_equal(got, want, ft), (t, op, key)
+                else:
+                    assert value_bytes(got) == value_bytes(want), (t, op, key)
+                checked += a.size
+    assert checked > 40000
