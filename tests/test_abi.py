@@ -95,6 +95,71 @@ int main(void) {
     assert exe.exists()
 
 
+REF_SRC = "/root/reference/src"
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(REF_SRC, "shmem.h")),
+                    reason="no /root/reference on this host")
+def test_reference_header_and_ours_agree(tmp_path):
+    """The drop-in boundary against the reference's OWN public headers
+    (src/shmem.h, src/pshmem.h, read where they lie; they build standalone):
+      * one translation unit includes the reference's shmem.h and pshmem.h and
+        then ours: C allows a function to be redeclared only with a compatible
+        type, so any of our prototypes that differs from the reference's (the
+        44 reductions at shmem.h:1412-1648, their pshmem names, and the
+        runtime/collective entry points both headers declare) is a compile
+        error under -Werror;
+      * the reduction constants our header gives a program (shmem.h:1400-1410)
+        equal the reference header's values;
+      * a program compiled against the reference's shmem.h alone (no header
+        of ours: a reference user's source as it stands) links against
+        libshmem_reduce_mi355x.so with every symbol resolved."""
+    both = tmp_path / "both.c"
+    both.write_text('#include <shmem.h>\n#include <pshmem.h>\n'
+                    '#include "shmem_reduce_mi355x.h"\nint main(void){return 0;}\n')
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", REF_SRC,
+                    "-I", os.path.dirname(HEADER), "-c", str(both), "-o", str(tmp_path / "both.o")],
+                   check=True)
+    names = ["SHMEM_REDUCE_SYNC_SIZE", "SHMEM_REDUCE_MIN_WRKDATA_SIZE", "SHMEM_SYNC_VALUE",
+             "_SHMEM_REDUCE_SYNC_SIZE", "_SHMEM_REDUCE_MIN_WRKDATA_SIZE", "_SHMEM_SYNC_VALUE"]
+    prog = ("#include <stdio.h>\n#include HDR\nint main(void){\n" +
+            "".join(f'#ifdef {n}\n printf("{n} %ld\\n", (long)({n}));\n#endif\n' for n in names) +
+            "return 0;}\n")
+    src = tmp_path / "consts.c"
+    src.write_text(prog)
+    vals = {}
+    for tag, hdr, inc in (("ref", "<shmem.h>", REF_SRC),
+                          ("ours", '"shmem_reduce_mi355x.h"', os.path.dirname(HEADER))):
+        exe = tmp_path / f"consts_{tag}"
+        subprocess.run(["gcc", "-std=c99", f"-DHDR={hdr}", "-I", inc, str(src), "-o", str(exe)],
+                       check=True)
+        out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout
+        vals[tag] = dict(line.split() for line in out.splitlines())
+    for n in ("SHMEM_REDUCE_SYNC_SIZE", "SHMEM_REDUCE_MIN_WRKDATA_SIZE", "SHMEM_SYNC_VALUE"):
+        assert vals["ours"][n] == vals["ref"][n], n
+    user = tmp_path / "user.c"
+    user.write_text(r'''
+#include <shmem.h>
+static long pSync[_SHMEM_REDUCE_SYNC_SIZE];
+static double dWrk[_SHMEM_REDUCE_MIN_WRKDATA_SIZE];
+static long long llWrk[_SHMEM_REDUCE_MIN_WRKDATA_SIZE];
+int main(void) {
+    static double t[4], s[4];
+    static long long total, mine = 1;
+    for (int i = 0; i < _SHMEM_REDUCE_SYNC_SIZE; i++) pSync[i] = _SHMEM_SYNC_VALUE;
+    shmem_init();
+    shmem_double_sum_to_all(t, s, 4, 0, 0, shmem_n_pes(), dWrk, pSync);
+    shmem_longlong_sum_to_all(&total, &mine, 1, 0, 0, shmem_n_pes(), llWrk, pSync);
+    shmem_barrier_all();
+    shmem_finalize();
+    return 0;
+}
+''')
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", REF_SRC, str(user),
+                    "-L", LIBDIR, "-lshmem_reduce_mi355x", f"-Wl,-rpath,{LIBDIR}",
+                    "-Wl,--no-undefined", "-o", str(tmp_path / "user")], check=True)
+
+
 def test_header_compiles_as_cpp(tmp_path):
     src = tmp_path / "caller.cpp"
     src.write_text('#include "shmem_reduce_mi355x.h"\n'
