@@ -528,6 +528,41 @@ elif scenario == "autotable":
         if got_algo != want_algo:
             fails.append(f"auto plan {t} {op} n={n} set={st}: {got_algo}, want {want_algo}")
         run_case(t, op, n, st, "auto", "device", seed, expect_algo=got_algo)
+elif scenario == "refops":
+    # The multi-PE kernels' element ops against the REFERENCE'S OWN
+    # (tests/golden/ref_element_ops.json: reduce-op.c:71-150 compiled from its
+    # text).  2 PEs: PE 0's source is the fixture's a, PE 1's is b, for all 44
+    # pairs on special values and random bits.  DIRECT and SIGNAL give every PE
+    # PE_start's order, op(a, b); own-order GATHER gives PE 1 op(b, a).  The
+    # one-shot/two-shot and fused/unfused schedules come from the test's env.
+    import base64
+    with open(os.path.join(HERE, "golden", "ref_element_ops.json")) as f:
+        cases = json.load(f)["cases"]
+    for t, c in cases.items():
+        dt = np.dtype(oracle.NP_DTYPE[t])
+        ab = [np.frombuffer(base64.b64decode(c[k]), dtype=dt).copy() for k in ("a", "b")]
+        mine = ab[pe]
+        n = mine.size
+        for op, o in c["ops"].items():
+            for algo in ("direct", "signal", "gather"):
+                ncases += 1
+                key = "ba" if (algo == "gather" and pe == 1) else "ab"
+                want = np.frombuffer(base64.b64decode(o[key]), dtype=dt)
+                heap_write(HEAP_SRC, mine, mine.nbytes)
+                heap_write(HEAP_TGT, np.full(mine.nbytes, 0xAB, np.uint8), mine.nbytes)
+                shm.reduce_on_stream(t, op, HEAP_TGT, HEAP_SRC, n, 0, 0, npes, algo)
+                torch.cuda.synchronize()
+                got = read(HEAP_TGT, t, n)
+                if op in ("sum", "prod") and t in ("float", "double", "complexd", "complexf"):
+                    ft = np.float32 if t in ("float", "complexf") else np.float64
+                    g, w = got.view(ft), want.view(ft)
+                    ok = (np.array_equal(np.isnan(g), np.isnan(w))
+                          and g[~np.isnan(w)].tobytes() == w[~np.isnan(w)].tobytes())
+                else:
+                    ok = same_bits(got, want)
+                if not ok or shm.last_error():
+                    fails.append(f"refops {t} {op} algo={algo}: differs from the reference "
+                                 f"(last_error {shm.last_error()})")
 elif scenario == "config0":
     # BASELINE.json configs[0]: shmem_int_sum_to_all, nreduce = 1024, on 2 PEs
     # (the reference's "oshrun loopback"), through the C entry point itself

@@ -110,6 +110,32 @@ def test_ipc_transport_all_pairs_sets_placements(tmp_path, npes, shots):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("schedule", ["fused-one", "fused-two", "unfused-two"])
+def test_ipc_reference_element_ops_two_pes(tmp_path, schedule):
+    """DIRECT, SIGNAL and own-order GATHER across 2 PE processes against the
+    reference's own compiled element ops (tests/golden/ref_element_ops.json,
+    reduce-op.c:71-150): all 44 pairs on special values and random bits, PE 0
+    holding a and PE 1 b, through the fused one-shot launch, the fused
+    two-shot launch, and the multi-launch two shot (peers fold + gather)."""
+    env = {"fused-one": {},
+           "fused-two": {"SHMEMX_DIRECT_ONESHOT_KB": "0"},
+           "unfused-two": {"SHMEMX_DIRECT_ONESHOT_KB": "0", "SHMEMX_FUSED_TWOSHOT_KB": "0",
+                           "SHMEMX_FUSED_ONESHOT": "0"}}[schedule]
+    reports = run_pes(tmp_path, 2, "refops", env, timeout=600)
+    for r in reports:
+        assert r["ncases"] == 44 * 3
+        assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
+    fences_checked(reports)
+    if schedule == "fused-one":
+        assert all(r["fences"]["fused_calls"] > 0 for r in reports)
+    elif schedule == "fused-two":
+        assert all(r["fences"]["fused_twoshot_calls"] > 0 for r in reports)
+    else:
+        assert all(r["fences"]["fused_calls"] == 0 and r["fences"]["fused_twoshot_calls"] == 0
+                   for r in reports)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("transport,heap", [("ipc", "device"), ("ipc", "mirrored"), ("rccl", "device")])
 def test_baseline_config0_int_sum_1024_two_pes(tmp_path, transport, heap):
     """BASELINE.json configs[0]: shmem_int_sum_to_all, nreduce = 1024, 2 PEs,
