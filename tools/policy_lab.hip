@@ -9,7 +9,7 @@
 // (back to back) and cold (a 1 GiB read-only sweep before every step, so no
 // dirty line is left in the Infinity Cache).
 //   hipcc --offload-arch=gfx950 -O3 tools/policy_lab.hip -o tools/policy_lab
-//   tools/policy_lab [n_elems] [cold 0|1]
+//   tools/policy_lab [n_elems] [cold 0|1] [list 0|1]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -129,7 +129,20 @@ int main(int argc, char **argv) {
         {"buf u8 ld nt st sc1nt", L_buffer<256, 8, 2, 2, 18>},
         {"global_nt (again)", L_global<256, 4>},
     };
-    const int K = cold ? 1 : 20, R = 7;
+    // list 1: the store's sc0 bit (round-3 follow-up), more rounds
+    std::vector<Variant> focus = {
+        {"global_nt (shipped)", L_global<256, 4>},
+        {"buf ld nt/nt st sc0nt", L_buffer<256, 4, 2, 2, 3>},
+        {"buf ld sc0nt/sc0nt st nt", L_buffer<256, 4, 3, 3, 2>},
+        {"buf ld sc0nt all", L_buffer<256, 4, 3, 3, 3>},
+        {"buf ld nt/nt st nt", L_buffer<256, 4, 2, 2, 2>},
+        {"buf u2 ld nt st sc0nt", L_buffer<256, 2, 2, 2, 3>},
+        {"global_nt (again)", L_global<256, 4>},
+        {"buf ld nt/nt st sc0nt (again)", L_buffer<256, 4, 2, 2, 3>},
+    };
+    const int list = argc > 3 ? atoi(argv[3]) : 0;
+    if (list == 1) vs = focus;
+    const int K = cold ? 1 : 20, R = list == 1 ? 15 : 7;
     std::vector<std::vector<float>> t(vs.size());
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
