@@ -489,18 +489,20 @@ AUTO_TABLE_ALGOS = {"full": ("allreduce", "rccl", "a2a", "direct", "gather"),
                     "partial": ("a2a", "direct", "gather")}
 
 
-def crossover_extra(world, rank, sp, stream, barrier, max_over_ranks, cap=1 << 24):
+def crossover_extra(world, rank, sp, stream, barrier, max_over_ranks, cap=1 << 24, out=None):
     """double sum over the full set, per algorithm and size, with source and
     target in the symmetric heap (so DIRECT and SIGNAL can run too): GiB/s of
     the whole job (N * n * 8 B / max-over-ranks time), microseconds per call,
     and whether every element of every PE's target was exact after the timed
     calls.  The data `auto`'s per-size choice (auto_recommendation) is set
-    from."""
+    from.  `out` (if given) is filled cell by cell, so a watchdog that prints
+    the line part-way still carries the cells measured so far."""
     sizes = sorted(set([1, 1 << 9, 1 << 12, 1 << 16, 1 << 18, 1 << 19, 1 << 20, 1 << 24]))
     sizes = [n for n in sizes if n <= cap] or [1]
     nbytes = sizes[-1] * 8
     hs, ht = malloc_pair(nbytes)
-    out = {"GiBps": {}, "us_per_call": {}, "correct": {}}
+    out = {} if out is None else out
+    out.update({"GiBps": {}, "us_per_call": {}, "correct": {}})
     try:
         if not (hs and ht):
             return "shmem_malloc failed"
@@ -508,6 +510,9 @@ def crossover_extra(world, rank, sp, stream, barrier, max_over_ranks, cap=1 << 2
         torch.cuda.synchronize()
         for algo in ("rccl", "allreduce", "a2a", "direct", "signal", "gather"):
             row, row_us, row_ok = {}, {}, {}
+            out["GiBps"][algo] = row
+            out["us_per_call"][algo] = row_us
+            out["correct"][algo] = row_ok
             for n in sizes:
                 def step(n=n, algo=algo):
                     shm.reduce_on_stream("double", "sum", ht, hs, n, 0, 0, world, algo, sp)
@@ -523,9 +528,6 @@ def crossover_extra(world, rank, sp, stream, barrier, max_over_ranks, cap=1 << 2
                     row_ok[str(n)] = max_over_ranks(0.0 if ok else 1.0) == 0.0
                 except shm.ShmemError as e:
                     row[str(n)] = row_us[str(n)] = row_ok[str(n)] = str(e)
-            out["GiBps"][algo] = row
-            out["us_per_call"][algo] = row_us
-            out["correct"][algo] = row_ok
         # the fused two-shot launch against the multi-launch two shot at the
         # same sizes (512 KiB, 2 MiB, 8 MiB per PE), to set
         # $SHMEMX_FUSED_TWOSHOT_KB's default from (every rank sets the same
@@ -561,18 +563,19 @@ def crossover_extra(world, rank, sp, stream, barrier, max_over_ranks, cap=1 << 2
     return out
 
 
-def subset_extra(world, rank, sp, stream, barrier, max_over_ranks, cap=1 << 24):
+def subset_extra(world, rank, sp, stream, barrier, max_over_ranks, cap=1 << 24, out=None):
     """double sum on partial active sets (N >= 4): the first half of the PEs
     (PE_start 0, stride 1) and every other PE (PE_start 0, logPE_stride 1),
     heap operands, per algorithm, microseconds per call (max over ranks;
     non-members skip the call, as OpenSHMEM's do) and whether every member's
     target was exact.  `auto` sends these through grouped-p2p A2A on the RCCL
-    transport by default; this is the data to revisit it (auto_recommendation)."""
+    transport by default; this is the data to revisit it (auto_recommendation).
+    `out` (if given) is filled cell by cell, as in crossover_extra."""
     if world < 4:
         return "needs N >= 4"
     sizes = [n for n in AUTO_BUCKETS.values() if n <= cap] or [1]
     hs, ht = malloc_pair(sizes[-1] * 8)
-    out = {}
+    out = {} if out is None else out
     try:
         if not (hs and ht):
             return "shmem_malloc failed"
@@ -583,8 +586,12 @@ def subset_extra(world, rank, sp, stream, barrier, max_over_ranks, cap=1 << 24):
             members = [start + (i << logstride) for i in range(size)]
             member = rank in members
             table, table_ok = {}, {}
+            out[f"{name}_us_per_call"] = table
+            out[f"{name}_correct"] = table_ok
             for algo in ("a2a", "direct", "signal", "gather"):
                 row, row_ok = {}, {}
+                table[algo] = row
+                table_ok[algo] = row_ok
                 for n in sizes:
                     failed = []
 
@@ -608,10 +615,6 @@ def subset_extra(world, rank, sp, stream, barrier, max_over_ranks, cap=1 << 24):
                         row[str(n)] = round(w / k * 1e6, 1)
                         ok = exact_target_ok(ht, base[:n], n, members) if member else True
                         row_ok[str(n)] = max_over_ranks(0.0 if ok else 1.0) == 0.0
-                table[algo] = row
-                table_ok[algo] = row_ok
-            out[f"{name}_us_per_call"] = table
-            out[f"{name}_correct"] = table_ok
     finally:
         if ht:
             shm.free(ht)
@@ -664,7 +667,7 @@ def auto_recommendation(crossover, partial):
             prev_n = n
         return ",".join(cuts)
     env = {}
-    if "full" in out:
+    if "full" in out and env_value(out["full"]):
         env["SHMEMX_AUTO_FULL"] = env_value(out["full"])
     # one partial table for both partial shapes: the strided set's choice
     # (every other PE crosses the most links), else the half set's
@@ -902,6 +905,15 @@ def main():
         shm.set_fatal_note(None)       # the line is printed here, not by the handler
         if note:
             line["extras"] = dict(extras, note=note)
+            # cut short by the watchdog: the recommendation from the cells
+            # the crossover / partial-set tables hold so far
+            if world > 1 and "auto_recommendation" not in extras:
+                try:
+                    line["extras"]["auto_recommendation"] = dict(
+                        auto_recommendation(extras.get("algo_crossover"), extras.get("partial_sets")),
+                        note="from the cells measured before the extras were cut short")
+                except Exception as e:   # noqa: BLE001
+                    line["extras"]["auto_recommendation"] = f"error: {type(e).__name__}: {e}"
         if rank == 0:
             print(json.dumps(line), flush=True)
 
@@ -981,10 +993,15 @@ def main():
                                                     max_over_ranks, max(3, a.steps // 4), "signal"))
         guarded("coherence", lambda: coherence_extra(world, rank, sp, max_over_ranks))
         guarded("heap_latency", lambda: heap_latency_extras(world, barrier, max_over_ranks))
+        # these two fill their tables cell by cell in place (extras[name] is
+        # the table from the start), so a watchdog cut keeps what they measured
+        extras["algo_crossover"] = {}
         guarded("algo_crossover", lambda: crossover_extra(world, rank, sp, stream, barrier,
-                                                          max_over_ranks, a.extras_max_nreduce))
+                                                          max_over_ranks, a.extras_max_nreduce,
+                                                          out=extras["algo_crossover"]))
+        extras["partial_sets"] = {}
         guarded("partial_sets", lambda: subset_extra(world, rank, sp, stream, barrier, max_over_ranks,
-                                                     a.extras_max_nreduce))
+                                                     a.extras_max_nreduce, out=extras["partial_sets"]))
         guarded("auto_recommendation", lambda: auto_recommendation(extras.get("algo_crossover"),
                                                                    extras.get("partial_sets")))
 

@@ -62,3 +62,22 @@ def test_auto_recommendation_env_is_parseable_form(bench):
     assert set(rec) == {"full", "env"}
     rec = bench.auto_recommendation("error: boom", None)
     assert rec == {"env": {}}
+
+
+def test_auto_recommendation_from_a_table_cut_short(bench):
+    """The watchdog may print the line while the crossover is being measured:
+    the tables then hold rows for the algorithms done so far and a partial
+    row for the current one (bench.py fills them in place); the
+    recommendation uses the cells present and leaves empty buckets out."""
+    us, ok = table({"rccl": [30, 31, 45, 150, 3000], "allreduce": [10, 12, 40, 200, 5000]})
+    # the third algorithm was cut after two sizes; the fourth never started
+    us["direct"], ok["direct"] = {"1": 5, "512": 50}, {"1": True, "512": True}
+    us["signal"], ok["signal"] = {}, {}
+    rec = bench.auto_recommendation({"us_per_call": us, "correct": ok}, {})
+    assert rec["full"]["8B"]["table"] == "direct"
+    assert rec["full"]["4KiB"]["table"] == "allreduce"
+    assert rec["full"]["128MiB"]["table"] == "rccl"
+    assert rec["env"]["SHMEMX_AUTO_FULL"].startswith("0:direct,")
+    # a crossover cut before its first cell: nothing to recommend, no error
+    rec = bench.auto_recommendation({}, {})
+    assert rec["env"] == {}
