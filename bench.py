@@ -61,6 +61,8 @@ def parse():
     ap.add_argument("--extras", type=int, default=1, help="also time the other algorithms / API forms")
     ap.add_argument("--extras-timeout", type=float, default=300.0,
                     help="seconds the extras may take before the line is printed without the rest")
+    ap.add_argument("--extras-only", default="",
+                    help="comma-separated names of the extras to run (default: all)")
     ap.add_argument("--extras-max-nreduce", type=int, default=256 * 1024 * 1024,
                     help="cap on the extras' array sizes (elements; the tests' short N > 1 runs "
                          "lower it; the driver's runs keep the full BASELINE.json sizes)")
@@ -934,12 +936,22 @@ def main():
     # (rank 0) and leaves.
     def watchdog():
         emit(f"extras stopped after {a.extras_timeout} s (timeout)")
+        if rank != 0:
+            # every rank's timer fires within milliseconds of the others';
+            # the others leave a moment after rank 0 has printed, so rank 0
+            # does not first see a peer vanish from a collective and take
+            # the extra's error path instead
+            time.sleep(2.0)
         os._exit(0 if ok else 1)
     timer = threading.Timer(a.extras_timeout, watchdog)
     timer.daemon = True
     timer.start()
 
+    only = {x for x in a.extras_only.split(",") if x}
+
     def guarded(name, fn):
+        if only and name not in only:
+            return
         arm_fatal_note(name)
         stage(rank, f"extra {name}")
         try:
@@ -995,13 +1007,15 @@ def main():
         guarded("heap_latency", lambda: heap_latency_extras(world, barrier, max_over_ranks))
         # these two fill their tables cell by cell in place (extras[name] is
         # the table from the start), so a watchdog cut keeps what they measured
-        extras["algo_crossover"] = {}
+        if not only or "algo_crossover" in only:
+            extras["algo_crossover"] = {}
         guarded("algo_crossover", lambda: crossover_extra(world, rank, sp, stream, barrier,
                                                           max_over_ranks, a.extras_max_nreduce,
-                                                          out=extras["algo_crossover"]))
-        extras["partial_sets"] = {}
+                                                          out=extras.get("algo_crossover")))
+        if not only or "partial_sets" in only:
+            extras["partial_sets"] = {}
         guarded("partial_sets", lambda: subset_extra(world, rank, sp, stream, barrier, max_over_ranks,
-                                                     a.extras_max_nreduce, out=extras["partial_sets"]))
+                                                     a.extras_max_nreduce, out=extras.get("partial_sets")))
         guarded("auto_recommendation", lambda: auto_recommendation(extras.get("algo_crossover"),
                                                                    extras.get("partial_sets")))
 

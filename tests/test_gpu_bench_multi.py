@@ -108,3 +108,37 @@ def test_bench_multi_rank_line(tmp_path, transport, npes):
                 for n, ok in row.items():
                     assert ok is True or (transport == "ipc" and algo in RCCL_ONLY), (shape, algo, n, ok)
         assert rec["env"].get("SHMEMX_AUTO_PARTIAL", "").startswith("0:"), rec
+
+
+@pytest.mark.gpu
+def test_bench_multi_watchdog_cut_keeps_line(tmp_path):
+    """The extras' watchdog fires in the middle of the crossover table (2
+    ranks, RCCL test double, only that extra, a 1.5 s budget): rank 0 still
+    prints the one line, correct, with the watchdog's note, the crossover
+    cells measured so far, and an auto_recommendation built from them."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env.update(SHMEMX_SHARE_GPU="1", SHMEMX_BARRIER_TIMEOUT="120", PYTHONUNBUFFERED="1",
+               FAKE_RCCL=os.path.join(HERE, "native", "libfake_rccl.so"))
+    env.pop("SHMEMX_TRANSPORT", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}",
+           os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+           "--nreduce", str(1 << 20), "--extras-max-nreduce", str(1 << 20),
+           "--extras-only", "algo_crossover", "--extras-timeout", "1.5"]
+    err_path = str(tmp_path / "bench.err")
+    with open(err_path, "w") as err:
+        p = subprocess.run(cmd, env=env, cwd=REPO, stdout=subprocess.PIPE, stderr=err, text=True,
+                           timeout=300, start_new_session=True)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{"metric"')]
+    tail = open(err_path).read()[-3000:]
+    assert p.returncode == 0, f"exit {p.returncode}\n{p.stdout[-2000:]}\n{tail}"
+    assert len(lines) == 1, f"want one JSON line, got {len(lines)}\n{p.stdout[-2000:]}"
+    line = json.loads(lines[0])
+    assert line["correct"] is True and line["value"] > 0
+    extras = line["extras"]
+    assert "timeout" in extras.get("note", ""), extras.get("note")
+    assert set(extras) <= {"note", "algo_crossover", "auto_recommendation"}, sorted(extras)
+    assert isinstance(extras["algo_crossover"], dict)
+    rec = extras["auto_recommendation"]
+    assert isinstance(rec, dict) and "cut short" in rec.get("note", ""), rec
+    assert isinstance(rec.get("env"), dict)
