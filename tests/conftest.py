@@ -66,6 +66,11 @@ def _ensure_built():
         subprocess.run(["make", "-j8", "-C", os.path.join(REPO, "openshmem-async_amd")], check=True)
     if not os.path.exists(os.path.join(REPO, "oracle", "liboracle_reduce.so")):
         subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle")], check=True)
+    # the reference's own element ops (oracle/build_ref.sh), where the
+    # reference is present (not on the GPU box: its tests then use the fixture)
+    if (os.path.exists("/root/reference/src/reduce/reduce-op.c")
+            and not os.path.exists(os.path.join(REPO, "oracle", "_ref", "libref_ops.so"))):
+        subprocess.run(["make", "-s", "-C", os.path.join(REPO, "oracle"), "ref"], check=True)
     if not os.path.exists(os.path.join(REPO, "tests", "native", "libfake_rccl.so")):
         subprocess.run(["make", "-s", "-C", os.path.join(REPO, "tests", "native")], check=True)
 
