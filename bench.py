@@ -973,6 +973,13 @@ def main():
                         "hbm_GBps": round(2 * nbytes / (e2 / k2) / 1e9, 1),
                         "us_per_call": round(e2 / k2 * 1e6, 2)}
             guarded("api_pe_size_1", api_pe_size_1)
+            # the same chip's measured streaming ceiling beside the spec peak
+            # ("vs a measured device-copy ceiling"): the PE_size 1
+            # call is one copy kernel over the same 256 MiB (read + write)
+            cp = extras.get("api_pe_size_1")
+            if isinstance(cp, dict) and cp.get("hbm_GBps"):
+                line["roofline"]["measured_copy_GBps"] = cp["hbm_GBps"]
+                line["roofline"]["frac_of_measured_copy"] = round(achieved / cp["hbm_GBps"], 4)
             guarded("host_resident_e2e", lambda: host_e2e(n))
             guarded("configs", lambda: config_extras(world, stream, barrier, max_over_ranks,
                                                      a.extras_max_nreduce))
