@@ -648,7 +648,11 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
         std::vector<const void *> from;
         std::vector<void *> to;
         std::vector<size_t> len;
-        for (int i = 0; i < P; ++i) {
+        // from member m + 1 on, wrapping (m itself last, when staged): the
+        // gather kernel gives its first blocks to its first segment, so the
+        // members start on different peers' slices
+        for (int r = 1; r <= P; ++r) {
+            const int i = (m + r) % P;
             if (i == m && !stage_tgt) continue;
             if (hi_of(i) <= lo_of(i)) continue;
             from.push_back(at(tbase[i], desc[i].tgt, c0 + lo_of(i)));

@@ -177,8 +177,12 @@ int signal_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     void *to[kMaxFoldInputs];
     size_t len[kMaxFoldInputs];
     int k = 0;
-    for (int i = 0; i < P; ++i) {
-        if (i == m || hi_of(i) <= lo_of(i)) continue;
+    // the segments from member m + 1 on, wrapping: the gather kernel gives
+    // its first blocks to its first segment, so member m starts on m + 1's
+    // slice and no member's HBM and links take every reader at once
+    for (int r = 1; r < P; ++r) {
+        const int i = (m + r) % P;
+        if (hi_of(i) <= lo_of(i)) continue;
         from[k] = hb[i] + toff + lo_of(i) * sz;
         to[k] = tgt + lo_of(i) * sz;
         len[k++] = (hi_of(i) - lo_of(i)) * sz;
