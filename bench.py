@@ -677,8 +677,46 @@ def auto_recommendation(crossover, partial):
         if shape in out and env_value(out[shape]):
             env["SHMEMX_AUTO_PARTIAL"] = env_value(out[shape])
             break
+    # $SHMEMX_FUSED_TWOSHOT_KB: the array size up to which DIRECT's and
+    # SIGNAL's two shot runs as one fused launch, from the fused-vs-unfused
+    # cells (512 KiB, 2 MiB, 8 MiB per PE): up to the last size where the
+    # fused launch won for both, cut at the geometric mean with the first size
+    # where it lost (256 KiB, the one shot's own limit, if it lost at once)
+    kb = fused_twoshot_kb(crossover.get("twoshot_fused_vs_unfused_us")
+                          if isinstance(crossover, dict) else None)
+    if kb is not None:
+        env["SHMEMX_FUSED_TWOSHOT_KB"] = str(kb)
     out["env"] = env
     return out
+
+
+def fused_twoshot_kb(cells):
+    """$SHMEMX_FUSED_TWOSHOT_KB from {algo: {str(n doubles): {"fused": us,
+    "unfused": us}}}, or None without a usable cell."""
+    if not isinstance(cells, dict):
+        return None
+    sizes = sorted({int(n) for row in cells.values() if isinstance(row, dict) for n in row})
+    wins = []
+    for n in sizes:
+        verdicts = []
+        for row in cells.values():
+            c = row.get(str(n)) if isinstance(row, dict) else None
+            if isinstance(c, dict) and all(isinstance(c.get(k), (int, float)) for k in ("fused", "unfused")):
+                verdicts.append(c["fused"] <= c["unfused"])
+        if not verdicts:
+            break
+        wins.append(all(verdicts))
+    if not wins:
+        return None
+    lead = 0
+    while lead < len(wins) and wins[lead]:
+        lead += 1
+    kib = [n * 8 // 1024 for n in sizes[:len(wins)]]
+    if lead == 0:
+        return 256
+    if lead == len(wins):
+        return kib[-1]
+    return int((kib[lead - 1] * kib[lead]) ** 0.5)
 
 
 def time_region(fn, steps, stream, barrier):

@@ -81,3 +81,26 @@ def test_auto_recommendation_from_a_table_cut_short(bench):
     # a crossover cut before its first cell: nothing to recommend, no error
     rec = bench.auto_recommendation({}, {})
     assert rec["env"] == {}
+
+
+def test_fused_twoshot_recommendation(bench):
+    """$SHMEMX_FUSED_TWOSHOT_KB from the fused-vs-unfused cells (sizes in
+    doubles per PE: 64 Ki = 512 KiB, 256 Ki = 2 MiB, 1 Mi = 8 MiB)."""
+    def cells(d, s):
+        return {"direct": {"65536": {"fused": d[0], "unfused": 50}, "262144": {"fused": d[1], "unfused": 60},
+                           "1048576": {"fused": d[2], "unfused": 90}},
+                "signal": {"65536": {"fused": s[0], "unfused": 50}, "262144": {"fused": s[1], "unfused": 60},
+                           "1048576": {"fused": s[2], "unfused": 90}}}
+    f = bench.fused_twoshot_kb
+    assert f(cells((40, 50, 80), (40, 50, 80))) == 8192            # fused wins everywhere
+    assert f(cells((40, 50, 100), (40, 50, 80))) == 4096           # loses at 8 MiB for one algo
+    assert f(cells((40, 70, 100), (40, 50, 80))) == 1024           # loses from 2 MiB
+    assert f(cells((60, 50, 80), (40, 50, 80))) == 256             # loses at once
+    assert f(None) is None and f({}) is None
+    assert f({"direct": {"65536": {"fused": "ENOTSUP", "unfused": 5}}}) is None
+    # through auto_recommendation, beside the table variables
+    us = {"rccl": {"1": 5.0}}
+    ok = {"rccl": {"1": True}}
+    rec = bench.auto_recommendation({"us_per_call": us, "correct": ok,
+                                     "twoshot_fused_vs_unfused_us": cells((40, 50, 100), (40, 50, 80))}, {})
+    assert rec["env"]["SHMEMX_FUSED_TWOSHOT_KB"] == "4096"
