@@ -422,6 +422,76 @@ def direct_extra(world, n, src, sp, stream, barrier, max_over_ranks, steps, algo
             shm.free(hs)
 
 
+def xgmi_extra(world, rank, sp, stream, barrier, max_over_ranks, nbytes=64 << 20):
+    """Raw link rates between this GPU and its peers, measured with the
+    library's gather (copy) kernel on IPC-mapped symmetric-heap blocks:
+    pull = loads from the peers' HBM into my HBM (what DIRECT and SIGNAL do),
+    push = stores from my HBM into the peers' HBM (what they never do: the
+    data for deciding whether a store-based exchange would beat the pulls);
+    from one peer (PE me+1) and from / to all peers at once.  GB/s per GPU,
+    the slowest rank's; plus whether pushed bytes were visible to the peer
+    after shmem_barrier_all (system fences on every XCD)."""
+    if world < 2:
+        return "needs N >= 2"
+    blk = shm.malloc(nbytes)
+    if not blk:
+        return "shmem_malloc failed"
+    try:
+        peers = [q for q in range(world) if q != rank]
+        paddr = {q: shm.heap_ptr(blk, q) for q in peers}
+        # collective: every rank takes the same path
+        if max_over_ranks(0.0 if all(paddr.values()) else 1.0) != 0.0:
+            return "no IPC mapping of the peers' heap (node block down) on some rank"
+        loc = torch.full((nbytes,), (rank + 1) & 0xFF, dtype=torch.uint8, device="cuda")
+        nxt = (rank + 1) % world
+        seg = (nbytes // len(peers)) // 16 * 16
+        slot = (nbytes // world) // 16 * 16
+        base = loc.data_ptr()
+        cases = {
+            "pull_one": ([paddr[nxt]], [base], [nbytes]),
+            "pull_all": ([paddr[q] for q in peers], [base + i * seg for i in range(len(peers))],
+                         [seg] * len(peers)),
+            "push_one": ([base], [paddr[nxt]], [nbytes]),
+            "push_all": ([base] * len(peers), [paddr[q] + rank * slot for q in peers], [slot] * len(peers)),
+        }
+        out = {"bytes_per_gpu": {}, "GBps_per_gpu": {}}
+        for name, (src, dst, lens) in cases.items():
+            if name.startswith("push"):
+                # the pulls overwrote my buffer with the peers' bytes: my own
+                # pattern again before anything is pushed from it
+                loc.fill_((rank + 1) & 0xFF)
+                torch.cuda.synchronize()
+
+            def step(src=src, dst=dst, lens=lens):
+                shm.gather(src, dst, lens, sp)
+            for _ in range(2):
+                step()
+            k = 10
+            w, _ = time_region(step, k, stream, barrier)
+            w = max_over_ranks(w)
+            out["bytes_per_gpu"][name] = sum(lens)
+            out["GBps_per_gpu"][name] = round(sum(lens) * k / w / 1e9, 1)
+        # visibility of stores into a peer's HBM: PE me - 1 writes its
+        # pattern over my whole block once more, and after the library's
+        # barrier (system fences on every XCD) my copy must read it
+        src, dst, lens = cases["push_one"]
+        shm.gather(src, dst, lens, sp)
+        torch.cuda.synchronize()
+        shm.barrier_all()
+        got = torch.empty(4096, dtype=torch.uint8, device="cuda")
+        shm.memcpy(got, blk + nbytes - 4096, 4096)
+        writer = (rank - 1) % world
+        ok = bool((got == ((writer + 1) & 0xFF)).all())
+        out["push_visible_after_barrier"] = max_over_ranks(0.0 if ok else 1.0) == 0.0
+        out["note"] = ("gather kernel (csrc/fold_kernels.hip) on IPC-mapped heap blocks: pull = peers' HBM -> "
+                       "mine, push = mine -> peers' HBM; GB/s = bytes this GPU moved / time, max over ranks")
+        return out
+    finally:
+        torch.cuda.synchronize()
+        barrier()
+        shm.free(blk)
+
+
 def coherence_extra(world, rank, sp, max_over_ranks, iters=20):
     """Cross-GPU coherence check of the IPC pulls (N > 1): DIRECT and SIGNAL
     on heap operands whose contents change on every call, at a fused one-shot
@@ -1049,6 +1119,7 @@ def main():
         guarded("signal_heap", lambda: direct_extra(world, n, src, sp, stream, barrier,
                                                     max_over_ranks, max(3, a.steps // 4), "signal"))
         guarded("coherence", lambda: coherence_extra(world, rank, sp, max_over_ranks))
+        guarded("xgmi_links", lambda: xgmi_extra(world, rank, sp, stream, barrier, max_over_ranks))
         guarded("heap_latency", lambda: heap_latency_extras(world, barrier, max_over_ranks))
         # these two fill their tables cell by cell in place (extras[name] is
         # the table from the start), so a watchdog cut keeps what they measured

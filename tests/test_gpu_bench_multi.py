@@ -84,6 +84,10 @@ def test_bench_multi_rank_line(tmp_path, transport, npes):
         assert isinstance(c, dict) and c["calls"] == 60 and c["mismatched_elements"] == 0, c
     for k in ("direct_heap", "signal_heap"):
         assert isinstance(extras[k], dict) and extras[k]["correct"] is True, extras[k]
+    x = extras["xgmi_links"]     # raw pull / push rates over the IPC-mapped heap
+    assert isinstance(x, dict) and x["push_visible_after_barrier"] is True, x
+    assert set(x["GBps_per_gpu"]) == {"pull_one", "pull_all", "push_one", "push_all"}
+    assert all(v > 0 for v in x["GBps_per_gpu"].values()), x
     bad = []
     for path, text in strings(extras):
         if path.endswith("_note") or path.startswith(".auto_recommendation"):
