@@ -483,7 +483,7 @@ def xgmi_extra(world, rank, sp, stream, barrier, max_over_ranks, nbytes=64 << 20
         writer = (rank - 1) % world
         ok = bool((got == ((writer + 1) & 0xFF)).all())
         out["push_visible_after_barrier"] = max_over_ranks(0.0 if ok else 1.0) == 0.0
-        out["note"] = ("gather kernel (csrc/fold_kernels.hip) on IPC-mapped heap blocks: pull = peers' HBM -> "
+        out["method_note"] = ("gather kernel (csrc/fold_kernels.hip) on IPC-mapped heap blocks: pull = peers' HBM -> "
                        "mine, push = mine -> peers' HBM; GB/s = bytes this GPU moved / time, max over ranks")
         return out
     finally:
