@@ -492,6 +492,75 @@ def xgmi_extra(world, rank, sp, stream, barrier, max_over_ranks, nbytes=64 << 20
         shm.free(blk)
 
 
+def push_extra(world, rank, n, sp, stream, barrier, max_over_ranks, steps):
+    """A store-based all-reduce composed from the library's public pieces (a
+    measurement for the next algorithm, not a library path): every PE
+    stores slice q of its source into PE q's receive block over the IPC
+    mapping (one gather launch), shmem_barrier_all (system fences on every
+    XCD), folds its slice from the P copies in its own HBM in set order
+    (shmemx_fold_n), barrier, stores its result slice into every peer's
+    target, barrier.  The same bytes cross the links as in DIRECT, as stores
+    instead of loads, and the fold reads local HBM.  Sources are small
+    integers, so every element of the target is checked exactly."""
+    P = world
+    if P < 2:
+        return "needs N >= 2"
+    sl = ((n + P - 1) // P + 1) // 2 * 2          # elements per slice, 16-B multiple
+
+    def lo(i):
+        return min(n, i * sl)
+
+    def hi(i):
+        return min(n, (i + 1) * sl)
+    hs, ht = malloc_pair(n * 8)
+    recv = shm.malloc(P * sl * 8)
+    try:
+        if not (hs and ht and recv):
+            return "shmem_malloc failed"
+        peers = [q for q in range(P) if q != rank]
+        ps = {q: shm.heap_ptr(recv, q) for q in peers}
+        pt = {q: shm.heap_ptr(ht, q) for q in peers}
+        if max_over_ranks(0.0 if all(ps.values()) and all(pt.values()) else 1.0) != 0.0:
+            return "no IPC mapping of the peers' heap (node block down) on some rank"
+        base = exact_source(hs, n, rank)
+        mlo, mhi = lo(rank), hi(rank)
+        qs = [q for q in peers if hi(q) > lo(q)]
+        p1 = ([hs + lo(q) * 8 for q in qs], [ps[q] + rank * sl * 8 for q in qs],
+              [(hi(q) - lo(q)) * 8 for q in qs])
+        ins = [hs + mlo * 8 if i == rank else recv + i * sl * 8 for i in range(P)]
+        p3 = ([ht + mlo * 8] * len(peers), [pt[q] + mlo * 8 for q in peers], [(mhi - mlo) * 8] * len(peers))
+
+        def call():
+            if qs:
+                shm.gather(*p1, sp)
+            torch.cuda.synchronize()
+            shm.barrier_all()
+            if mhi > mlo:
+                shm.fold_n("double", "sum", ht + mlo * 8, ins, mhi - mlo, sp)
+            torch.cuda.synchronize()
+            shm.barrier_all()
+            if mhi > mlo:
+                shm.gather(*p3, sp)
+            torch.cuda.synchronize()
+            shm.barrier_all()
+        for _ in range(2):
+            call()
+        w, _ = time_region(call, steps, stream, barrier)
+        w = max_over_ranks(w)
+        ok = exact_target_ok(ht, base, n, range(P))
+        return {"GiBps": round(P * n * 8 * steps / w / GiB, 2), "ms_per_call": round(w / steps * 1e3, 3),
+                "correct": max_over_ranks(0.0 if ok else 1.0) == 0.0,
+                "method_note": "push slices (gather kernel, stores over IPC) -> barrier_all -> local fold "
+                               "(shmemx_fold_n) -> barrier_all -> push result slice -> barrier_all; "
+                               "compare direct_heap (the same exchange as loads)"}
+    finally:
+        torch.cuda.synchronize()
+        barrier()
+        for h in (recv, ht, hs):
+            if h:
+                shm.free(h)
+
+
 def coherence_extra(world, rank, sp, max_over_ranks, iters=20):
     """Cross-GPU coherence check of the IPC pulls (N > 1): DIRECT and SIGNAL
     on heap operands whose contents change on every call, at a fused one-shot
@@ -1120,6 +1189,8 @@ def main():
                                                     max_over_ranks, max(3, a.steps // 4), "signal"))
         guarded("coherence", lambda: coherence_extra(world, rank, sp, max_over_ranks))
         guarded("xgmi_links", lambda: xgmi_extra(world, rank, sp, stream, barrier, max_over_ranks))
+        guarded("push_allreduce", lambda: push_extra(world, rank, n, sp, stream, barrier, max_over_ranks,
+                                                     max(3, a.steps // 4)))
         guarded("heap_latency", lambda: heap_latency_extras(world, barrier, max_over_ranks))
         # these two fill their tables cell by cell in place (extras[name] is
         # the table from the start), so a watchdog cut keeps what they measured

@@ -88,6 +88,8 @@ def test_bench_multi_rank_line(tmp_path, transport, npes):
     assert isinstance(x, dict) and x["push_visible_after_barrier"] is True, x
     assert set(x["GBps_per_gpu"]) == {"pull_one", "pull_all", "push_one", "push_all"}
     assert all(v > 0 for v in x["GBps_per_gpu"].values()), x
+    pa = extras["push_allreduce"]      # the store-based exchange, exact integer sums
+    assert isinstance(pa, dict) and pa["correct"] is True and pa["GiBps"] > 0, pa
     bad = []
     for path, text in strings(extras):
         if path.endswith("_note") or path.startswith(".auto_recommendation"):
