@@ -1188,9 +1188,6 @@ def main():
         guarded("signal_heap", lambda: direct_extra(world, n, src, sp, stream, barrier,
                                                     max_over_ranks, max(3, a.steps // 4), "signal"))
         guarded("coherence", lambda: coherence_extra(world, rank, sp, max_over_ranks))
-        guarded("xgmi_links", lambda: xgmi_extra(world, rank, sp, stream, barrier, max_over_ranks))
-        guarded("push_allreduce", lambda: push_extra(world, rank, n, sp, stream, barrier, max_over_ranks,
-                                                     max(3, a.steps // 4)))
         guarded("heap_latency", lambda: heap_latency_extras(world, barrier, max_over_ranks))
         # these two fill their tables cell by cell in place (extras[name] is
         # the table from the start), so a watchdog cut keeps what they measured
@@ -1205,6 +1202,12 @@ def main():
                                                      a.extras_max_nreduce, out=extras.get("partial_sets")))
         guarded("auto_recommendation", lambda: auto_recommendation(extras.get("algo_crossover"),
                                                                    extras.get("partial_sets")))
+        # the very last: the first stores into the peers' HBM over xGMI any
+        # run makes (the library itself only loads from the peers), after
+        # everything the next round's settings are read from
+        guarded("xgmi_links", lambda: xgmi_extra(world, rank, sp, stream, barrier, max_over_ranks))
+        guarded("push_allreduce", lambda: push_extra(world, rank, n, sp, stream, barrier, max_over_ranks,
+                                                     max(3, a.steps // 4)))
 
     timer.cancel()
     faulthandler.cancel_dump_traceback_later()
