@@ -44,7 +44,13 @@ import shmem_mi355x as shm  # noqa: E402
 
 GiB = float(1 << 30)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-XGMI_LINK_GBS = 153.0          # per link, 7 links per GPU
+XGMI_LINK_GBS = 153.0          # per link per direction, 7 links per GPU
+XGMI_PEAK_BASIS = (
+    "peak = (N-1) x 153 GB/s: each GPU's N-1 direct xGMI links (one per peer, full mesh of 8) at "
+    "153 GB/s per link in EACH direction, the figure of the task statement ('7 links x ~153 GB/s "
+    "per GPU') and SURVEY.md section 8(d) config 3; achieved = the bytes each GPU sends (= the bytes "
+    "it receives) in reduce-scatter + all-gather, 2(N-1)/N x 256 MiB, over the time per call. "
+    "measured_link_ceiling_GBps (extras.xgmi_links.pull_all, same run) is the links' measured rate")
 
 
 def parse():
@@ -55,7 +61,10 @@ def parse():
     ap.add_argument("--nreduce", type=int, default=32 * 1024 * 1024)
     ap.add_argument("--algo", default="auto", choices=list(shm.ALGOS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-reps", type=int, default=20)
+    ap.add_argument("--cpu-reps", type=int, default=20,
+                    help="warm calls the N = 1 CPU baseline times (the median is reported)")
+    ap.add_argument("--cpu-reps-multi", type=int, default=7,
+                    help="warm calls the N > 1 CPU baseline (N PE processes) times")
     ap.add_argument("--cpu-table", type=int, default=1,
                     help="also time every BASELINE.json config on the host (cpu_baseline.table)")
     ap.add_argument("--extras", type=int, default=1, help="also time the other algorithms / API forms")
@@ -97,44 +106,64 @@ def cpu_model() -> str:
 
 
 def pin_base(P: int) -> int:
-    """First of P consecutive CPUs this process may run on (the box gives a
-    job a CPU share, not the whole host), or -1 to leave the PEs unpinned."""
+    """First of the LAST P consecutive CPUs this process may run on (the box
+    gives a job a CPU share, not the whole host), or -1 to leave the PEs
+    unpinned.  The last ones, not the first: CPU 0 of a share also serves
+    interrupts and, usually, the runtimes' own threads (VERDICT r03 #5)."""
     allowed = sorted(os.sched_getaffinity(0))
-    for i in range(len(allowed) - P + 1):
+    for i in range(len(allowed) - P, -1, -1):
         if allowed[i + P - 1] - allowed[i] == P - 1:
             return allowed[i]
     return -1
 
 
-def cpu_run(oracle, t, op, P, n, reps):
-    """One fork-per-PE run of the oracle: PE 0's per-call times (the first
-    call is a warm-up and is not among them), and the cores used."""
-    base = pin_base(P)
-    times, _ = oracle.reduce_fork(t, op, P, 0, 0, P, n, kind=0, reps=reps, pin_base=base)
-    cores = f"{base}-{base + P - 1}" if base >= 0 else "unpinned"
-    return statistics.median(times), cores
+def spread_ms(times):
+    """min / median / max of per-call seconds, in ms."""
+    return {"min_ms": round(min(times) * 1e3, 3), "median_ms": round(statistics.median(times) * 1e3, 3),
+            "max_ms": round(max(times) * 1e3, 3), "calls": len(times)}
 
 
-def cpu_baseline(n: int, reps: int):
-    """The same workload as the N = 1 GPU step, on one host core: the
-    reference's local reduction write_to = op(write_to, pWrk) over n doubles
-    (reduce-op.c:224-245, 64-element pWrk staging, an indirect call per
-    element) in the oracle restatement; algbw n*8/t like the GPU value, median
-    over `reps` warm folds.  The whole call at 2..8 PEs is in the table."""
+def cpu_baseline(n: int, reps: int, world: int = 1):
+    """The same workload as the GPU step, on the host cores, in the oracle
+    restatement of the reference's src/reduce (reduce-op.c, gcc -O2: faster
+    than the reference's own default build, -std=c99 with no -O,
+    configure:524-539, so a conservative baseline).
+
+    * world == 1: the local reduction write_to = op(write_to, pWrk) over n
+      doubles (reduce-op.c:224-245, 64-element pWrk staging, an indirect call
+      per element), one process pinned to one core; n*8/t like the GPU value.
+    * world > 1: the whole shmem_double_sum_to_all of the line's config on
+      `world` PEs = `world` forked processes over shared memory (the GASNet
+      smp model, oshrun.in:97-98), pinned to `world` consecutive cores, the
+      reference's peer loop (reduce-op.c:213-250); world*n*8/t like the GPU
+      value (whole job), t = PE 0's time per call.
+    Median of `reps` warm calls, with min / max and the wall time."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle  # cpu_baseline leg only
-    base = pin_base(1)
+    base = pin_base(world)
     t0 = time.perf_counter()
-    med = statistics.median(oracle.fold_time("double", "sum", n, reps=reps, pin=base))
+    if world == 1:
+        times = oracle.fold_time("double", "sum", n, reps=reps, pin=base)
+        what = (f"the local reduce of shmem_double_sum_to_all, write_to = write_to + pWrk over nreduce={n} "
+                f"(64-element pWrk staging, indirect call per element, :224-245), the N = 1 GPU step's "
+                f"workload, one process")
+    else:
+        times, _ = oracle.reduce_fork("double", "sum", world, 0, 0, world, n, kind=0, reps=reps,
+                                      pin_base=base)
+        what = (f"the whole shmem_double_sum_to_all over nreduce={n} on {world} PEs (the line's config): "
+                f"{world} forked PE processes over shared memory, the reference's copy + barrier + peer "
+                f"loop (reduce-op.c:213-250), PE 0's time per call")
     wall = time.perf_counter() - t0
-    return {"value": round(n * 8 / med / GiB, 4), "unit": "GiB/s", "cores": 1,
+    med = statistics.median(times)
+    cpus = (str(base) if world == 1 else f"{base}-{base + world - 1}") if base >= 0 else "unpinned"
+    return {"value": round(world * n * 8 / med / GiB, 4), "unit": "GiB/s", "cores": world,
             "kind": "port",
-            "sample": f"oracle restatement of reduce-op.c (gcc -O2): the local reduce of "
-                      f"shmem_double_sum_to_all, write_to = write_to + pWrk over nreduce={n} "
-                      f"(64-element pWrk staging, indirect call per element, :224-245), the N = 1 "
-                      f"GPU step's workload, one process pinned to CPU {base}; median of {reps} "
-                      f"warm folds ({med * 1e3:.1f} ms/fold, {wall:.1f} s wall); host: {cpu_model()}, "
-                      f"{os.cpu_count()} logical CPUs"}
+            "sample": f"oracle restatement of reduce-op.c (gcc -O2, faster than the reference's default "
+                      f"-std=c99 without -O): {what}, pinned to CPU {cpus} (the last of the job's "
+                      f"{len(os.sched_getaffinity(0))} usable CPUs); median of {len(times)} warm calls "
+                      f"({med * 1e3:.1f} ms/call, {wall:.1f} s wall); host: {cpu_model()}, "
+                      f"{os.cpu_count()} logical CPUs",
+            "cpus": cpus, "spread": spread_ms(times), "wall_s": round(wall, 2)}
 
 
 def cpu_baseline_table(reps: int = 3):
@@ -160,15 +189,20 @@ def cpu_baseline_table(reps: int = 3):
     out = []
     t0 = time.perf_counter()
     base = pin_base(1)
-    fold = statistics.median(oracle.fold_time("double", "sum", 32 * Mi, reps=reps, pin=base))
+    ft = oracle.fold_time("double", "sum", 32 * Mi, reps=reps, pin=base)
+    fold = statistics.median(ft)
     out.append({"config": "configs[1]", "call": "local reduce of shmem_double_sum_to_all "
                 "(write_to = write_to + pWrk, the N = 1 GPU step)", "nreduce": 32 * Mi, "PEs": 1,
                 "cores": 1, "cpus": str(base), "ms_per_call": round(fold * 1e3, 4),
-                "per_pe_GiBps": round(32 * Mi * 8 / fold / GiB, 4)})
+                "spread": spread_ms(ft), "per_pe_GiBps": round(32 * Mi * 8 / fold / GiB, 4)})
     for t, op, P, n, cfg in rows:
-        med, cores = cpu_run(oracle, t, op, P, n, reps if n * size[t] >= 1 << 20 else 4 * reps)
+        base = pin_base(P)
+        times, _ = oracle.reduce_fork(t, op, P, 0, 0, P, n, kind=0,
+                                      reps=reps if n * size[t] >= 1 << 20 else 4 * reps, pin_base=base)
+        med = statistics.median(times)
         out.append({"config": cfg, "call": f"shmem_{t}_{op}_to_all", "nreduce": n, "PEs": P,
-                    "cores": P, "cpus": cores, "ms_per_call": round(med * 1e3, 4),
+                    "cores": P, "cpus": f"{base}-{base + P - 1}" if base >= 0 else "unpinned",
+                    "ms_per_call": round(med * 1e3, 4), "spread": spread_ms(times),
                     "per_pe_GiBps": round(n * size[t] / med / GiB, 4)})
     return {"host": f"{cpu_model()}, {os.cpu_count()} logical CPUs, "
                     f"{len(os.sched_getaffinity(0))} usable by this job",
@@ -233,6 +267,8 @@ def config_extras(world, stream, barrier, max_over_ranks, cap=256 * 1024 * 1024)
     scratch = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
     scratch64 = scratch.view(torch.float64)
 
+    detail = {}
+
     def rate(type_name, op, n, elem, steps, cold=None):
         x = (torch.randint(-2**62, 2**62, (n,), dtype=torch.int64, device="cuda", generator=g)
              if elem == 8 and type_name == "long" else
@@ -250,6 +286,13 @@ def config_extras(world, stream, barrier, max_over_ranks, cap=256 * 1024 * 1024)
                   for _ in range(steps)]
             barrier()
             torch.cuda.synchronize()
+            if world == 1:
+                # N = 1: each fold's own duration from the library's kernel
+                # clock (its dispatch's events); the marker events around it
+                # add the launch boundary and their own latency (~5-6 us,
+                # profiles/r04_midsize.txt), which a cold step of a few us
+                # cannot amortise
+                shm.kernel_timing(True)
             with torch.cuda.stream(stream):
                 for k, (e0, e1) in enumerate(ev):
                     if cold == "dirty":
@@ -260,7 +303,17 @@ def config_extras(world, stream, barrier, max_over_ranks, cap=256 * 1024 * 1024)
                     fn()
                     e1.record(stream)
             torch.cuda.synchronize()
-            w = sum(e0.elapsed_time(e1) for e0, e1 in ev) * 1e-3
+            w_ev = sum(e0.elapsed_time(e1) for e0, e1 in ev) * 1e-3
+            w = w_ev
+            if world == 1:
+                kt, _ = shm.kernel_times()
+                shm.kernel_timing(False)
+                kern = [us for kind, us in kt if kind == "fold"]
+                if len(kern) == steps:
+                    w = sum(kern) * 1e-6
+                    detail.setdefault(cold, {})[str(n)] = {
+                        "kernel_us": round(statistics.median(kern), 2),
+                        "event_us": round(w_ev / steps * 1e6, 2)}
         else:
             w, _ = time_region(fn, steps, stream, barrier)
         w = max_over_ranks(w)
@@ -281,8 +334,14 @@ def config_extras(world, stream, barrier, max_over_ranks, cap=256 * 1024 * 1024)
     out["float_sum_GiBps_vs_nreduce"] = cold
     out["float_sum_GiBps_vs_nreduce_note"] = (
         "cold: a 1 GiB scratch is read (read-only sweep: evicts, leaves nothing dirty) before every "
-        "step and only the steps are timed (HIP events on the stream), so every step reads and "
-        "writes HBM; GiB/s = PEs x nreduce x 4 B / step")
+        "step and only the steps are timed, so every step reads and writes HBM; GiB/s = PEs x "
+        "nreduce x 4 B / step.  N = 1: the step is the fold kernel's own duration (the library's "
+        "kernel clock, shmemx_kernel_times: start/stop events of the dispatch itself); "
+        "float_sum_us_vs_nreduce gives it beside the marker-event time around the same launch, whose "
+        "difference is the launch boundary plus the markers' latency, not kernel work.  N > 1: "
+        "marker events around the whole collective")
+    if detail.get("clean"):
+        out["float_sum_us_vs_nreduce"] = detail["clean"]
     out["float_sum_GiBps_vs_nreduce_after_write_flush"] = dirty
     out["float_sum_GiBps_vs_nreduce_after_write_flush_note"] = (
         "the same, but the scratch is REWRITTEN before every step (round 2's flush): up to 256 MiB "
@@ -858,6 +917,34 @@ def fused_twoshot_kb(cells):
     return int((kib[lead - 1] * kib[lead]) ** 0.5)
 
 
+def measured_ceiling(ptrs, nbytes, stream_ptr, reps=20):
+    """The device's measured HBM streaming ceiling beside the spec peak
+    (SURVEY §8d): tools/libceiling.so reads the given arrays (nbytes each)
+    with 16-B non-temporal loads and nothing else, each launch timed by its
+    own dispatch events; the median rate in GB/s.  A read-only stream is the
+    fastest thing HBM does here (6.8-7.1 TB/s; a copy's honest rate is
+    6.1-6.4, profiles/r04_stream_lab_*.txt), so no kernel that also writes
+    can beat it.  None if the helper is not built."""
+    import ctypes
+    path = os.path.join(REPO, "tools", "libceiling.so")
+    if not os.path.exists(path):
+        return None
+    L = ctypes.CDLL(path)
+    dp = ctypes.POINTER(ctypes.c_double)
+    L.ceiling_read.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_size_t,
+                               ctypes.c_void_p, ctypes.c_int, dp, dp]
+    L.ceiling_read.restype = ctypes.c_int
+    arr = (ctypes.c_void_p * len(ptrs))(*ptrs)
+    med, lo = ctypes.c_double(), ctypes.c_double()
+    if L.ceiling_read(arr, len(ptrs), nbytes, stream_ptr, reps, ctypes.byref(med), ctypes.byref(lo)):
+        return None
+    total = len(ptrs) * nbytes
+    return {"kernel": f"read-only stream of {len(ptrs)} x {nbytes >> 20} MiB (the bench's own arrays), "
+                      f"16-B non-temporal loads, 256 lanes x 4 vectors per array (tools/ceiling.hip)",
+            "bytes_per_launch": total, "median_us": round(med.value, 2), "min_us": round(lo.value, 2),
+            "GBps": round(total / med.value / 1e3, 1), "launches": reps}
+
+
 def time_region(fn, steps, stream, barrier):
     """Run fn() `steps` times on `stream`; returns (wall_s, event_s)."""
     barrier()
@@ -944,7 +1031,7 @@ def main():
     # per PE), as the reference's source/target are symmetric objects carved
     # from its heap (memory/symmem.c:168-227).  Heap blocks also give the
     # fold a steady 122 us, where separately allocated torch tensors land on
-    # a slow physical pairing now and then (129 us; profiles/r01_placement_*).
+    # a slow physical pairing now and then (129 us; profiles/archive/r01_placement_*).
     heap_blocks = [shm.malloc(nbytes) for _ in range(2)]
     use_heap = max_over_ranks(0.0 if all(heap_blocks) else 1.0) == 0.0
 
@@ -1033,6 +1120,35 @@ def main():
                     "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
                     "avg_launch_us": round(t_launch * 1e6, 2),
                     "kernel": "fold_kernel<double,SUM,2 inputs>"}
+        # cross-check of avg_launch_us (HIP events over the timed region): K
+        # more launches of the same step, each timed by its own dispatch
+        # events (the library's kernel clock), after the timed region
+        try:
+            torch.cuda.synchronize()
+            shm.kernel_timing(True)
+            for _ in range(a.steps):
+                step()
+            torch.cuda.synchronize()
+            kt, _ = shm.kernel_times()
+            shm.kernel_timing(False)
+            kus = [us for kind, us in kt if kind == "fold"]
+            if kus:
+                roofline["kernel_clock_us"] = {"mean": round(statistics.mean(kus), 2),
+                                               "median": round(statistics.median(kus), 2),
+                                               "min": round(min(kus), 2), "launches": len(kus)}
+        except Exception as e:   # noqa: BLE001 — a cross-check, never the headline
+            roofline["kernel_clock_us"] = f"error: {type(e).__name__}: {e}"
+        # the measured streaming ceiling beside the spec peak:
+        # a read-only stream over the bench's own three 256 MiB arrays
+        try:
+            ptr = lambda x: x if isinstance(x, int) else x.data_ptr()   # noqa: E731
+            mc = measured_ceiling([ptr(acc), ptr(inp), tgt.data_ptr()], nbytes, sp)
+            if mc:
+                roofline["measured_ceiling_GBps"] = mc["GBps"]
+                roofline["frac_of_measured_ceiling"] = round(achieved / mc["GBps"], 4)
+                roofline["measured_ceiling"] = mc
+        except Exception as e:   # noqa: BLE001
+            roofline["measured_ceiling"] = f"error: {type(e).__name__}: {e}"
     else:
         t_call = ev / a.steps
         xgmi_bytes = 2 * (world - 1) / world * nbytes        # per GPU, RS + AG
@@ -1043,22 +1159,27 @@ def main():
                     "alg_bytes_per_launch": int(xgmi_bytes),
                     "avg_launch_us": round(t_call * 1e6, 2),
                     "busbw_GBps": round(achieved, 1),
-                    "peak_basis": "bytes each GPU sends (= receives), RS + AG, over its N-1 "
-                                  "direct links at 153 GB/s per link per direction (the task's "
-                                  "figure; if 153 GB/s is the two-way link rate, frac doubles)",
+                    "peak_basis": XGMI_PEAK_BASIS,
                     "algbw_GiBps": round(nbytes / t_call / GiB, 2)}
 
     cpu = None
-    if world == 1 and rank == 0 and not a.no_cpu_baseline:
+    if rank == 0 and not a.no_cpu_baseline:
+        # the reference's CPU src/reduce on this host, in the same run
+        # (north_star): at N > 1 the line's own config on N PE processes
         stage(rank, "cpu baseline")
-        cpu = cpu_baseline(n, a.cpu_reps)
-        if a.cpu_table:
+        try:
+            cpu = cpu_baseline(n, a.cpu_reps if world == 1 else a.cpu_reps_multi, world)
+        except Exception as e:   # noqa: BLE001 — a reported baseline, never the headline
+            cpu = {"value": None, "error": f"{type(e).__name__}: {e}", "cores": world}
+        if world == 1 and a.cpu_table:
             # every BASELINE.json config on the host cores (BASELINE.md's plan);
             # the P = 1 double-sum row sits beside this N = 1 GPU value
             try:
                 cpu["table"] = cpu_baseline_table()
             except Exception as e:   # noqa: BLE001 — a reported baseline, never the headline
                 cpu["table"] = f"error: {type(e).__name__}: {e}"
+
+    barrier()     # the other ranks wait here while rank 0 times the CPU leg
 
     line = {
         "metric": "GiB/s device-resident shmem_double_sum_to_all, nreduce=32Mi, 1/2/4/8 GPUs",
@@ -1070,7 +1191,8 @@ def main():
                    "algo": algo_used if world == 1 else
                    shm.plan("double", "sum", n, 0, 0, world, rank, world, algo_used).algo,
                    "parallelism": f"one PE per GPU x{world}",
-                   "transport": os.environ.get("SHMEMX_TRANSPORT", "rccl"),
+                   "transport": os.environ.get("SHMEMX_TRANSPORT", "rccl") if world > 1 else
+                   "none (one PE: the step is the local fold, no exchange)",
                    "arrays": "symmetric heap (shmem_malloc, HBM)" if use_heap else "hipMalloc (torch)"},
         "roofline": roofline, "cpu_baseline": cpu, "correct": ok, "extras": extras,
     }
@@ -1146,17 +1268,28 @@ def main():
                     api_step()
                 k2 = max(5, a.steps // 2)
                 w2, e2 = time_region(api_step, k2, stream, barrier)
-                return {"GiBps": round(nbytes * k2 / w2 / GiB, 1),
-                        "hbm_GBps": round(2 * nbytes / (e2 / k2) / 1e9, 1),
-                        "us_per_call": round(e2 / k2 * 1e6, 2)}
+                # and each call's copy kernel by its own dispatch events
+                shm.kernel_timing(True)
+                for _ in range(k2):
+                    api_step()
+                torch.cuda.synchronize()
+                kt, _ = shm.kernel_times()
+                shm.kernel_timing(False)
+                kus = [us for kind, us in kt if kind == "copy"]
+                t_ev = e2 / k2
+                out = {"clock_events": {"us_per_call": round(t_ev * 1e6, 2),
+                                        "GiBps": round(nbytes / t_ev / GiB, 1),
+                                        "hbm_GBps": round(2 * nbytes / t_ev / 1e9, 1)},
+                       "clock_wall": {"us_per_call": round(w2 / k2 * 1e6, 2),
+                                      "GiBps": round(nbytes / (w2 / k2) / GiB, 1)},
+                       "note": "each block's fields come from one clock: HIP events over the timed "
+                               "calls, the host's wall clock, the copy kernel's own dispatch events"}
+                if kus:
+                    ku = statistics.median(kus)
+                    out["clock_kernel"] = {"kernel": "fold_kernel<T,SUM,1 input,8 vectors,nt> (the copy)",
+                                           "us": round(ku, 2), "hbm_GBps": round(2 * nbytes / ku / 1e3, 1)}
+                return out
             guarded("api_pe_size_1", api_pe_size_1)
-            # the same chip's measured streaming ceiling beside the spec peak
-            # ("vs a measured device-copy ceiling"): the PE_size 1
-            # call is one copy kernel over the same 256 MiB (read + write)
-            cp = extras.get("api_pe_size_1")
-            if isinstance(cp, dict) and cp.get("hbm_GBps"):
-                line["roofline"]["measured_copy_GBps"] = cp["hbm_GBps"]
-                line["roofline"]["frac_of_measured_copy"] = round(achieved / cp["hbm_GBps"], 4)
             guarded("host_resident_e2e", lambda: host_e2e(n))
             guarded("configs", lambda: config_extras(world, stream, barrier, max_over_ranks,
                                                      a.extras_max_nreduce))
@@ -1206,6 +1339,13 @@ def main():
         # run makes (the library itself only loads from the peers), after
         # everything the next round's settings are read from
         guarded("xgmi_links", lambda: xgmi_extra(world, rank, sp, stream, barrier, max_over_ranks))
+        xl = extras.get("xgmi_links")
+        if isinstance(xl, dict) and (xl.get("GBps_per_gpu") or {}).get("pull_all"):
+            # the links' measured rate beside the spec peak: a copy kernel
+            # pulling from every peer at once (the all-gather's pattern)
+            meas = xl["GBps_per_gpu"]["pull_all"]
+            line["roofline"]["measured_link_ceiling_GBps"] = meas
+            line["roofline"]["frac_of_measured_links"] = round(achieved / meas, 4)
         guarded("push_allreduce", lambda: push_extra(world, rank, n, sp, stream, barrier, max_over_ranks,
                                                      max(3, a.steps // 4)))
 

@@ -304,6 +304,20 @@ int shmemx_gather_on_stream(const void *const *srcs, void *const *dsts,
  * vectors per lane per input of the 2-input fold (2, 4 or 8; default 4). */
 int shmemx_fold_set_tuning(int max_blocks, int nontemporal, int unroll);
 
+/* The kernel clock: with on != 0, every launch of the fold family (the
+ * 2-input and P-input folds, the copy of a one-member call, the peers fold,
+ * the gather) carries start / stop events of its own dispatch
+ * (hipExtLaunchKernelGGL), i.e. the kernel's execution time alone, with no
+ * launch boundary and no event-marker latency; up to 4096 launches are
+ * timed between reads.  shmemx_kernel_times waits for them and writes up to
+ * max durations in microseconds to us[] and their kinds (0 fold, 1 copy,
+ * 2 peers fold, 3 gather) to kind[] (may be NULL), in launch order, and the
+ * launches past the 4096 that went untimed to *dropped (may be NULL); it
+ * returns how many were written and starts over.  Off by default; timing
+ * does not change what runs. */
+int shmemx_kernel_timing(int on);
+int shmemx_kernel_times(double *us, int *kind, int max, unsigned long long *dropped);
+
 /* Largest DIRECT / SIGNAL two-shot call, in KiB, that runs as one fused
  * launch (default $SHMEMX_FUSED_TWOSHOT_KB, else 4096; 0 = never).  Every
  * member of a set must hold the same value when it calls (the members choose
@@ -358,11 +372,14 @@ void *shmemx_heap_ptr(const void *addr, int pe);
  *                             given a view address (write(2) of a result,
  *                             read(2) into a source) fails with EFAULT on a
  *                             block the library has not opened;
- *   shmemx_mirror_stats       out[0..5] = write faults, read faults, blocks
+ *   shmemx_mirror_stats       out[0..6] = write faults, read faults, blocks
  *                             copied to HBM, blocks copied back, blocks marked
  *                             device-newer, faults that waited for a
- *                             collective being enqueued on their block;
- *                             returns how many were filled.
+ *                             collective writing their block, blocks a
+ *                             blocking call made clean before returning
+ *                             (its result, up to $SHMEMX_MIRROR_SETTLE_KB,
+ *                             default 256 KiB, copied back); returns how
+ *                             many were filled.
  * A host access to a block a collective is writing waits for it (from any
  * thread), then reads the result; a fetch waits only for the streams that
  * wrote the view (the caller's stream of a stream-ordered call, not the whole

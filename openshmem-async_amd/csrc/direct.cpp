@@ -209,7 +209,7 @@ void fence_and_wait(hipStream_t s) {
         // starts only after all earlier work on s: once all kFenceBlocks
         // records are in, that work is complete and every XCD has fenced.
         // Polling the host-coherent records returns ~1.5 us sooner than
-        // hipStreamSynchronize (profiles/r02_sync_lab.txt); after a second
+        // hipStreamSynchronize (profiles/archive/r02_sync_lab.txt); after a second
         // without them the stream wait takes over (and reports any error).
         {
             const auto t0 = std::chrono::steady_clock::now();
@@ -556,7 +556,11 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
                       "SHMEMX_FUSED_TWOSHOT_KB (set member %d: %llu/%llu KiB, member 0: %llu/%llu KiB)",
                       i, (unsigned long long)(desc[i].aux >> 32), (unsigned long long)(desc[i].aux & 0xffffffffu),
                       (unsigned long long)(desc[0].aux >> 32), (unsigned long long)(desc[0].aux & 0xffffffffu));
-                // nobody reads anyone's operands: the call ends here on every member
+                // nobody reads anyone's operands: the call ends here on every
+                // member, after one more barrier, so that no member's next
+                // call overwrites its descriptor before a slower member has
+                // read this call's copy
+                node::barrier(start, step, P);
                 return set_error(SHMEMX_ENOTSUP);
             }
         }

@@ -27,9 +27,92 @@
 //     (-ffp-contract=off), min/max are selects (not v_min_f64, whose NaN / -0
 //     behaviour differs), complex products follow C99 Annex G / libgcc
 //     __muldc3 including its NaN-recovery branch.
+#include <hip/hip_ext.h>
+
+#include <algorithm>
+#include <atomic>
+#include <mutex>
+#include <vector>
+
 #include "fold_ops.h"
 
 namespace shmx {
+
+// ------------------------------------------------------------ kernel clock
+// shmemx_kernel_timing(1): the fold-family launches (2-input and P-input
+// folds, the copy, the peers fold, the gather) go through
+// hipExtLaunchKernelGGL with a start / stop event pair: the dispatch's own
+// timestamps, i.e. the kernel alone, with no launch boundary and no
+// event-marker latency (a marker pair around a 9 us fold reads 14.7 us,
+// rocprofv3 8.6, profiles/r04_midsize.txt).  shmemx_kernel_times() hands
+// the durations back in launch order.  Off (the default), the launches are
+// plain hipLaunchKernelGGL.
+enum KernelKind { kKindFold = 0, kKindCopy = 1, kKindPeers = 2, kKindGather = 3 };
+namespace {
+constexpr size_t kClockPairs = 4096;
+struct KClock {
+    std::mutex mu;
+    std::atomic<bool> on{false};
+    std::vector<hipEvent_t> ev;   // 2 per launch, created on first use
+    std::vector<int> kind;
+    size_t used = 0;              // pairs handed out since the last read
+    size_t dropped = 0;           // launches past the ring, not timed
+} g_kclock;
+
+// a start / stop pair for the next launch, or false (timing off, ring full)
+bool clock_pair(int kind, hipEvent_t *a, hipEvent_t *b) {
+    if (!g_kclock.on.load(std::memory_order_relaxed)) return false;
+    std::lock_guard<std::mutex> lk(g_kclock.mu);
+    if (g_kclock.used >= kClockPairs) {
+        ++g_kclock.dropped;
+        return false;
+    }
+    if (g_kclock.ev.size() < 2 * (g_kclock.used + 1)) {
+        for (int i = 0; i < 2; ++i) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return false;
+            g_kclock.ev.push_back(e);
+        }
+        g_kclock.kind.push_back(0);
+    }
+    *a = g_kclock.ev[2 * g_kclock.used];
+    *b = g_kclock.ev[2 * g_kclock.used + 1];
+    g_kclock.kind[g_kclock.used++] = kind;
+    return true;
+}
+
+template <typename K, typename... Args>
+void launch_k(int kind, K kernel, dim3 grid, dim3 block, hipStream_t s, Args... args) {
+    hipEvent_t a, b;
+    if (clock_pair(kind, &a, &b)) hipExtLaunchKernelGGL(kernel, grid, block, 0, s, a, b, 0, args...);
+    else hipLaunchKernelGGL(kernel, grid, block, 0, s, args...);
+}
+}  // namespace
+
+int kernel_timing(int on) {
+    std::lock_guard<std::mutex> lk(g_kclock.mu);
+    g_kclock.on.store(on != 0);
+    g_kclock.used = 0;
+    g_kclock.dropped = 0;
+    return 0;
+}
+
+int kernel_times(double *us, int *kind, int max, unsigned long long *dropped) {
+    std::lock_guard<std::mutex> lk(g_kclock.mu);
+    const int n = (int)std::min<size_t>(g_kclock.used, max > 0 ? (size_t)max : 0);
+    for (int i = 0; i < n; ++i) {
+        float ms = 0.f;
+        if (hipEventSynchronize(g_kclock.ev[2 * i + 1]) != hipSuccess ||
+            hipEventElapsedTime(&ms, g_kclock.ev[2 * i], g_kclock.ev[2 * i + 1]) != hipSuccess)
+            return -1;
+        us[i] = ms * 1e3;
+        if (kind) kind[i] = g_kclock.kind[i];
+    }
+    if (dropped) *dropped = g_kclock.dropped;
+    g_kclock.used = 0;
+    g_kclock.dropped = 0;
+    return n;
+}
 
 namespace {
 
@@ -289,31 +372,31 @@ hipError_t launch_typed_grid(const FoldArgs &a, hipStream_t stream) {
         // the two-input fold (reduce-op.c:231-235): the hot kernel.  The
         // soft-float long double kernels exist at unroll 4 only.
         if constexpr (std::is_same<T, ld80>::value) {
-            hipLaunchKernelGGL((fold_kernel<T, OP, 2, 4, NT>), dim3((unsigned)grid_for(a, 4)),
-                               dim3(kBlock), 0, stream, a);
+            launch_k(kKindFold, fold_kernel<T, OP, 2, 4, NT>, dim3((unsigned)grid_for(a, 4)), dim3(kBlock),
+                     stream, a);
         } else {
             const int u = fold_tuning().unroll;
             const dim3 grid((unsigned)grid_for(a, u));
             if (u == 2)
-                hipLaunchKernelGGL((fold_kernel<T, OP, 2, 2, NT>), grid, dim3(kBlock), 0, stream, a);
+                launch_k(kKindFold, fold_kernel<T, OP, 2, 2, NT>, grid, dim3(kBlock), stream, a);
             else if (u == 8)
-                hipLaunchKernelGGL((fold_kernel<T, OP, 2, 8, NT>), grid, dim3(kBlock), 0, stream, a);
+                launch_k(kKindFold, fold_kernel<T, OP, 2, 8, NT>, grid, dim3(kBlock), stream, a);
             else
-                hipLaunchKernelGGL((fold_kernel<T, OP, 2, 4, NT>), grid, dim3(kBlock), 0, stream, a);
+                launch_k(kKindFold, fold_kernel<T, OP, 2, 4, NT>, grid, dim3(kBlock), stream, a);
         }
     } else if (a.peers && !kHeavyOp<T, OP> && (NT == 0 || NT == 3)) {
         if (a.nins <= 4)
-            hipLaunchKernelGGL((fold_peers_kernel<T, OP, 4, NT>), dim3((unsigned)grid_for(a, peers_unroll(4))),
-                               dim3(kBlock), 0, stream, a);
+            launch_k(kKindPeers, fold_peers_kernel<T, OP, 4, NT>,
+                     dim3((unsigned)grid_for(a, peers_unroll(4))), dim3(kBlock), stream, a);
         else if (a.nins <= 8)
-            hipLaunchKernelGGL((fold_peers_kernel<T, OP, 8, NT>), dim3((unsigned)grid_for(a, peers_unroll(8))),
-                               dim3(kBlock), 0, stream, a);
+            launch_k(kKindPeers, fold_peers_kernel<T, OP, 8, NT>,
+                     dim3((unsigned)grid_for(a, peers_unroll(8))), dim3(kBlock), stream, a);
         else
-            hipLaunchKernelGGL((fold_peers_kernel<T, OP, 16, NT>), dim3((unsigned)grid_for(a, peers_unroll(16))),
-                               dim3(kBlock), 0, stream, a);
+            launch_k(kKindPeers, fold_peers_kernel<T, OP, 16, NT>,
+                     dim3((unsigned)grid_for(a, peers_unroll(16))), dim3(kBlock), stream, a);
     } else {
-        hipLaunchKernelGGL((fold_kernel<T, OP, 0, kUnrollN, NT>), dim3((unsigned)grid_for(a, kUnrollN)),
-                           dim3(kBlock), 0, stream, a);
+        launch_k(kKindFold, fold_kernel<T, OP, 0, kUnrollN, NT>, dim3((unsigned)grid_for(a, kUnrollN)),
+                 dim3(kBlock), stream, a);
     }
     return hipGetLastError();
 }
@@ -348,6 +431,46 @@ hipError_t launch_nt(const FoldArgs &a, hipStream_t stream) {
         default: return launch_typed<T, OP, 3>(a, stream);
         }
     }
+}
+
+// The copy (nins == 1: reduce-op.c:213-216, the whole PE_size = 1 call, and
+// the private copy of an overlapping source): a compile-time one-input
+// instance of the fold, one chunk of kBlock x kUnrollCopy 16-B vectors per
+// workgroup, non-temporal loads and stores from 32 MiB moved.  A copy moves
+// bits, so it runs on one type per element size (short, int, long, and a
+// 16-byte struct for complex double and long double) with no arithmetic.
+// Measured (tools/stream_lab.hip, profiles/r04_stream_lab_*.txt, 256 and
+// 512 MiB, after a flush, the in-stream cost that also charges deferred
+// write-backs): 8 vectors per lane 6.17-6.42 TB/s, 4 vectors 6.09-6.13, 2
+// or 16 worse, 512/1024-lane blocks and persistent grids worse; default-
+// policy stores look faster by kernel time alone (6.9-7.1) but leave up to
+// 256 MiB dirty in the Infinity Cache for the next kernel to write back
+// (4.9-5.2 TB/s charged), so the stores stay non-temporal.
+constexpr int kUnrollCopy = 8;
+
+template <typename T, int NT>
+hipError_t launch_copy_nt(const FoldArgs &a0, hipStream_t stream) {
+    const size_t blocks = grid_for(a0, kUnrollCopy);
+    // a one-workgroup copy stores the host signal itself (launch_fold_signal);
+    // a larger grid is followed by the marker kernel
+    const bool self_signal = a0.sig_word && blocks == 1;
+    FoldArgs a = a0;
+    if (!self_signal) a.sig_word = nullptr;
+    launch_k(kKindCopy, fold_kernel<T, SHMEMX_OP_SUM, 1, kUnrollCopy, NT>, dim3((unsigned)blocks), dim3(kBlock),
+             stream, a);
+    if (a0.sig_word && !self_signal)
+        hipLaunchKernelGGL(host_signal_kernel, dim3(1), dim3(64), 0, stream, a0.sig_word, a0.sig_value);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_copy(const FoldArgs &a, hipStream_t stream) {
+    int mode = fold_tuning().nontemporal;
+    if (mode < 0) {
+        const size_t n = a.head + a.nvec * (16 / sizeof(T)) + a.tail;
+        mode = 2 * n * sizeof(T) >= kNtThresholdBytes ? 3 : 0;
+    }
+    return mode ? launch_copy_nt<T, 3>(a, stream) : launch_copy_nt<T, 0>(a, stream);
 }
 
 template <typename T>
@@ -448,6 +571,15 @@ hipError_t dispatch(int type, int op, FoldArgs &a, const void *const *ptrs, int 
         a.nvec = 0;
         a.tail = 0;
     }
+    if (a.nins == 1) {   // a copy: bits only, one kernel per element size
+        switch (sz) {
+        case 2: return launch_copy<short>(a, stream);
+        case 4: return launch_copy<int>(a, stream);
+        case 8: return launch_copy<long>(a, stream);
+        case 16: return launch_copy<cplxd>(a, stream);
+        default: return hipErrorInvalidValue;
+        }
+    }
     switch (type) {
     case SHMEMX_TYPE_SHORT: return launch_int_ops<short>(op, a, stream);
     case SHMEMX_TYPE_INT: return launch_int_ops<int>(op, a, stream);
@@ -538,7 +670,7 @@ hipError_t launch_fold_peers(int type, int op, void *out, const void *const *ins
 // kGatherRun blocks take the segments in turn: a resident grid of ~2048
 // blocks still spans every segment (kGatherRun x 7 = 1792), and each run
 // streams 8 MiB contiguous per segment.  Measured on local HBM, 7 x 32 MiB
-// (profiles/r02c_pmc_kernels.json, profiles/r03_peers_gather_lab*.txt):
+// (profiles/archive/r02c_pmc_kernels.json, profiles/r03_peers_gather_lab*.txt):
 // blockIdx.y-major 77.4 us; single blocks in turn (round 2) 80.5, with 2
 // vectors per lane 79.3; runs of 16-64 blocks 82-89; runs of 256 blocks
 // with 8 vectors per lane 72.5 us warm, 74.9 cold (6.48 / 6.27 TB/s), the
@@ -619,7 +751,7 @@ hipError_t launch_gather(const void *const *srcs, void *const *dsts, const size_
     bx = (bx + run - 1) / run * run;
     a.nseg = k;
     a.run = (unsigned)run;
-    hipLaunchKernelGGL(gather_kernel, dim3((unsigned)(bx * k)), dim3(kBlock), 0, stream, a);
+    launch_k(kKindGather, gather_kernel, dim3((unsigned)(bx * k)), dim3(kBlock), stream, a);
     return hipGetLastError();
 }
 

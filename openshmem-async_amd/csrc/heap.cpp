@@ -440,15 +440,24 @@ DeviceWrite::DeviceWrite(void *p, size_t bytes, void *stream)
         bytes > g_heap.arena.capacity() - (uint64_t)(static_cast<const char *>(p) - g_heap.view))
         return;
     const uint64_t off = (uint64_t)(static_cast<const char *>(p) - g_heap.view);
-    mirror::begin_device_write(off, bytes);
+    mirror::begin_device_write(off, bytes, &fresh_);
     dev_ = g_heap.base + off;
+    off_ = off;
+    bytes_ = bytes;
     open_ = true;
 }
 
-DeviceWrite::~DeviceWrite() {
+void DeviceWrite::close() {
     if (!open_) return;
+    open_ = false;
     record_writer(stream_);
-    mirror::end_device_write();
+    mirror::end_device_write(off_, bytes_);
+}
+
+size_t DeviceWrite::settle(size_t limit) {
+    if (!open_ || bytes_ > limit) return 0;
+    close();
+    return mirror::settle(off_, bytes_, fresh_);
 }
 
 bool host_acquire(const void *p, size_t bytes, bool write) {

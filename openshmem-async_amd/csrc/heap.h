@@ -89,15 +89,26 @@ void device_wrote(const void *p, size_t bytes, void *stream);
 class DeviceWrite {
   public:
     DeviceWrite(void *p, size_t bytes, void *stream);
-    ~DeviceWrite();
+    ~DeviceWrite() { close(); }
     DeviceWrite(const DeviceWrite &) = delete;
     DeviceWrite &operator=(const DeviceWrite &) = delete;
     void *ptr() const { return dev_; }
+    // record the writer and end the write in flight (the destructor's work)
+    void close();
+    // After a BLOCKING call's work has completed: if the target is at most
+    // `limit` bytes, close the write and copy the result back into the view
+    // (mirror::settle), so its blocks are CLEAN — readable by system calls
+    // as well as by plain loads — when the call returns.  Larger targets
+    // keep the lazy fetch.  Returns the bytes copied back.
+    size_t settle(size_t limit);
 
   private:
     void *dev_;
     void *stream_;
+    uint64_t off_ = 0;
+    size_t bytes_ = 0;
     bool open_;
+    bool fresh_ = false;
 };
 // The HBM twin of a host-view address (p itself otherwise), with no change
 // of block state.

@@ -156,6 +156,15 @@ constexpr int kChecksumMaxBlocks = 4096;
 hipError_t launch_checksum(int type, const void *ptr, size_t n, unsigned long long *out,
                            unsigned long long epoch, hipStream_t stream);
 
+// The kernel clock (fold_kernels.hip; shmemx_kernel_timing /
+// shmemx_kernel_times): while on, every fold-family launch carries a
+// start / stop event pair of its own dispatch (hipExtLaunchKernelGGL), up to
+// 4096 launches between reads.  kernel_times waits for them and returns
+// their durations (us) and kinds (0 fold, 1 copy, 2 peers fold, 3 gather)
+// in launch order, then starts over.
+int kernel_timing(int on);
+int kernel_times(double *us, int *kind, int max, unsigned long long *dropped);
+
 // Tuning knobs for the fold kernels (initialised from the environment:
 // SHMEMX_FOLD_MAX_BLOCKS, SHMEMX_FOLD_NT, SHMEMX_FOLD_UNROLL; changed at run
 // time by shmemx_fold_set_tuning).

@@ -25,6 +25,8 @@ struct View {
     size_t bytes = 0;
     size_t nblocks = 0;
     uint8_t *state = nullptr;   // one State per block (mmap'd: no allocator in the handler)
+    // device writes in flight per block (begin_device_write .. end_device_write)
+    uint16_t *pending = nullptr;
     Backend be{};
     // the last write fault's run, so a sequential writer unprotects growing
     // runs instead of faulting once per block
@@ -38,10 +40,6 @@ struct View {
 std::atomic_flag g_lock = ATOMIC_FLAG_INIT;
 struct sigaction g_prev_segv;
 bool g_installed = false;
-
-// Device writes in flight (begin_device_write .. end_device_write): a fault
-// on a DEVICE_NEWER block waits for zero before it fetches.
-std::atomic<int> g_pending{0};
 
 // The fault service: one request slot, because the handler holds the lock
 // while it waits.  kIdle -> kAsked (handler) -> kDone (service) -> kIdle.
@@ -138,10 +136,13 @@ bool create(size_t bytes, const Backend &be) {
     void *a = mmap(nullptr, vbytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
     close(fd);   // the mappings keep the pages
     void *s = mmap(nullptr, nblocks, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-    if (p == MAP_FAILED || a == MAP_FAILED || s == MAP_FAILED) {
+    void *w = mmap(nullptr, nblocks * sizeof(uint16_t), PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS,
+                   -1, 0);
+    if (p == MAP_FAILED || a == MAP_FAILED || s == MAP_FAILED || w == MAP_FAILED) {
         if (p != MAP_FAILED) munmap(p, vbytes);
         if (a != MAP_FAILED) munmap(a, vbytes);
         if (s != MAP_FAILED) munmap(s, nblocks);
+        if (w != MAP_FAILED) munmap(w, nblocks * sizeof(uint16_t));
         return false;
     }
     g_view.base = static_cast<char *>(p);
@@ -149,11 +150,11 @@ bool create(size_t bytes, const Backend &be) {
     g_view.bytes = vbytes;
     g_view.nblocks = nblocks;
     g_view.state = static_cast<uint8_t *>(s);   // zero: every block CLEAN
+    g_view.pending = static_cast<uint16_t *>(w);
     g_view.be = be;
     g_view.run_end = g_view.fetch_end = ~size_t(0);
     g_view.run_len = g_view.fetch_len = 0;
     g_view.st = Stats{};
-    g_pending.store(0);
     g_req.store(kIdle);
     g_service_up = pthread_create(&g_service, nullptr, service_main, nullptr) == 0;
     // a forked child has no service thread: its faults copy in place (and
@@ -213,6 +214,7 @@ void destroy() {
     munmap(g_view.base, g_view.bytes);
     munmap(g_view.alias, g_view.bytes);
     munmap(g_view.state, g_view.nblocks);
+    munmap(g_view.pending, g_view.nblocks * sizeof(uint16_t));
     g_view = View{};
 }
 
@@ -284,18 +286,41 @@ size_t flush(uint64_t off, size_t bytes) {
     return flush_locked(off, bytes);
 }
 
-size_t begin_device_write(uint64_t off, size_t bytes) {
+size_t begin_device_write(uint64_t off, size_t bytes, bool *fresh) {
     if (!g_view.base || !bytes) return 0;
     Guard g;
     flush_locked(off, bytes);
     const size_t b0 = block_of(off), b1 = std::min(block_of(off + bytes - 1) + 1, g_view.nblocks);
     const size_t n = mark_device_newer(b0, b1);
-    g_pending.fetch_add(1, std::memory_order_acq_rel);
+    for (size_t b = b0; b < b1; ++b) ++g_view.pending[b];
+    if (fresh) *fresh = n == b1 - b0;
     return n;
 }
 
-void end_device_write() {
-    if (g_pending.load(std::memory_order_acquire) > 0) g_pending.fetch_sub(1, std::memory_order_acq_rel);
+void end_device_write(uint64_t off, size_t bytes) {
+    if (!g_view.base || !bytes) return;
+    Guard g;
+    const size_t b0 = block_of(off), b1 = std::min(block_of(off + bytes - 1) + 1, g_view.nblocks);
+    for (size_t b = b0; b < b1; ++b)
+        if (g_view.pending[b]) --g_view.pending[b];
+}
+
+size_t settle(uint64_t off, size_t bytes, bool fresh) {
+    if (!g_view.base || !bytes) return 0;
+    Guard g;
+    const size_t b0 = block_of(off), b1 = std::min(block_of(off + bytes - 1) + 1, g_view.nblocks);
+    for (size_t b = b0; b < b1; ++b)   // another write in flight, or a block already back
+        if (g_view.pending[b] || g_view.state[b] != DEVICE_NEWER) return 0;
+    if (!fresh) {
+        fetch_run(b0, b1 - b0, false);
+        return (b1 - b0) * kBlock;
+    }
+    // the rest of every block already equals HBM: only the written bytes move
+    g_view.be.to_host(off, bytes, g_view.be.ctx);
+    protect(b0, b1 - b0, PROT_READ);
+    std::memset(g_view.state + b0, CLEAN, b1 - b0);
+    g_view.st.blocks_settled += b1 - b0;
+    return bytes;
 }
 
 size_t device_wrote(uint64_t off, size_t bytes) {
@@ -350,10 +375,11 @@ bool handle_fault(void *addr) {
         const size_t b = block_of(offset_of(addr));
         switch (g_view.state[b]) {
         case DEVICE_NEWER: {
-            if (g_pending.load(std::memory_order_acquire) > 0) {
-                // a collective is being enqueued on blocks of the view: its
-                // result is not recorded yet, so fetching now would read
-                // the old bytes; retry once the write in flight has ended
+            if (g_view.pending[b]) {
+                // a collective writing this block is being enqueued or run:
+                // its result is not recorded yet, so fetching now would read
+                // the old bytes; retry once that write has ended (writes to
+                // other blocks do not hold this fault up)
                 waited = true;
                 continue;
             }

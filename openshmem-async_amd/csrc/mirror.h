@@ -99,15 +99,24 @@ uint64_t offset_of(const void *p);
 size_t flush(uint64_t off, size_t bytes);
 // Before a collective WRITES [off, off + bytes): flush the overlapped
 // HOST_NEWER blocks, then mark every overlapped block DEVICE_NEWER (no host
-// access) and count one device write in flight, all under the lock.  A host
-// access to any of those blocks — the target itself, or a neighbouring
-// object in the same block, from any thread — waits until every write in
-// flight has ended (end_device_write), then fetches the block, whose bytes
-// are then the collective's.  Returns the blocks marked.
-size_t begin_device_write(uint64_t off, size_t bytes);
-// The write begun last is enqueued and its completion is recorded where
-// Backend::to_host waits for it.
-void end_device_write();
+// access) and count one device write in flight on each of them, all under
+// the lock.  A host access to any of those blocks — the target itself, or a
+// neighbouring object in the same block, from any thread — waits until the
+// writes in flight on THAT block have ended (end_device_write), then fetches
+// it, whose bytes are then the collective's; faults on other blocks do not
+// wait.  *fresh (if given): no overlapped block was DEVICE_NEWER before, so
+// all their other bytes equal HBM (settle()).  Returns the blocks marked.
+size_t begin_device_write(uint64_t off, size_t bytes, bool *fresh = nullptr);
+// The write begun on [off, off + bytes) is enqueued and its completion is
+// recorded where Backend::to_host waits for it.
+void end_device_write(uint64_t off, size_t bytes);
+// After a blocking collective that wrote [off, off + bytes) has completed and
+// ended its write: make its blocks CLEAN (readable by host code and system
+// calls alike) instead of leaving them to a fault.  With `fresh` (from
+// begin_device_write) only [off, off + bytes) is copied back; otherwise the
+// blocks whole.  Nothing happens if another write is in flight on them.
+// Returns the bytes copied.
+size_t settle(uint64_t off, size_t bytes, bool fresh);
 // After a collective wrote [off, off + bytes) in HBM without
 // begin_device_write (a collect target, whose length is known only after
 // the exchange): the overlapped blocks become DEVICE_NEWER (call flush on the
@@ -131,6 +140,7 @@ bool handle_fault(void *addr);
 struct Stats {
     uint64_t write_faults, read_faults, blocks_flushed, blocks_fetched, blocks_device_newer;
     uint64_t fault_waits;   // faults that waited for a device write in flight
+    uint64_t blocks_settled;   // made CLEAN by settle() (the written bytes copied back)
 };
 Stats stats(bool reset);
 State state_of(uint64_t off);   // tests

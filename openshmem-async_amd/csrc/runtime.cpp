@@ -206,6 +206,7 @@ static int init_locked(int pe, int npes, int device, const void *uid) {
     SHMX_HIP(hipStreamCreate(&g_state.stream));
     g_state.force_collective = env_int("SHMEMX_FORCE_COLLECTIVE", nullptr, 0) != 0;
     g_state.ipc_only = ipc_transport_env();
+    g_state.node_shared = false;
     if (npes > 1 || g_state.force_collective) {
         ncclUniqueId id;
         if (npes > 1) {
@@ -233,6 +234,7 @@ static int init_locked(int pe, int npes, int device, const void *uid) {
             if (attached && !all) node::detach(false);
             attached = all != 0;
         }
+        g_state.node_shared = attached;
         if (!attached) trace(LOG_INIT, "no intra-node block: the DIRECT algorithm is unavailable");
         // Every PE is attached after a first barrier (it also makes the IPC
         // transport's init collective, like ncclCommInitRank, so a bootstrap
@@ -440,7 +442,7 @@ int make_plan(int type, int op, int nreduce, int start, int logstride,
     if (algo == SHMEMX_ALGO_AUTO && P > 1) {
         const int t = auto_table_algo(world, n * sz);
         const bool rccl_ok = world && rccl_native(type, op) && !g_state.ipc_only;
-        const bool pull_ok = node::up() && P <= kMaxFoldInputs && !t_planning_capture;
+        const bool pull_ok = g_state.node_shared && P <= kMaxFoldInputs && !t_planning_capture;
         if (((t == SHMEMX_ALGO_RCCL || t == SHMEMX_ALGO_ALLREDUCE) && rccl_ok) ||
             (t == SHMEMX_ALGO_A2A && !g_state.ipc_only) || (t == SHMEMX_ALGO_DIRECT && pull_ok) ||
             t == SHMEMX_ALGO_GATHER)
@@ -815,6 +817,11 @@ int reduce_on_stream(int type, int op, void *target, const void *source,
     // blocks waits until the call is enqueued, then for `s` (the writer), and
     // reads the result
     heap::DeviceWrite t(target, bytes, s);
+    // a host-view target whose range runs past the heap: DeviceWrite opened
+    // nothing and ptr() is still the view address, which no kernel may write
+    // 
+    uint64_t voff = 0;
+    if (bytes && t.ptr() == target && heap::view_offset(target, &voff)) return set_error(SHMEMX_EINVAL);
     return reduce_device(type, op, t.ptr(), src, nreduce, start, logstride, size,
                          algo == SHMEMX_ALGO_AUTO ? g_state.algo : algo, s);
 }
@@ -876,6 +883,7 @@ void pshmem_finalize(void) {
     }
     (void)hipStreamDestroy(g_state.stream);
     g_state.stream = nullptr;
+    g_state.node_shared = false;
     g_state.inited = false;
 }
 
@@ -926,9 +934,10 @@ int shmemx_mirror_stats(unsigned long long *out, int nout, int reset) {
     std::lock_guard<std::recursive_mutex> lk(g_mu);
     if (!out || nout < 0) return set_error(SHMEMX_EINVAL);
     const mirror::Stats st = mirror::stats(reset != 0);
-    const unsigned long long all[6] = {st.write_faults, st.read_faults, st.blocks_flushed,
-                                       st.blocks_fetched, st.blocks_device_newer, st.fault_waits};
-    const int k = nout < 6 ? nout : 6;
+    const unsigned long long all[7] = {st.write_faults, st.read_faults, st.blocks_flushed,
+                                       st.blocks_fetched, st.blocks_device_newer, st.fault_waits,
+                                       st.blocks_settled};
+    const int k = nout < 7 ? nout : 7;
     for (int i = 0; i < k; ++i) out[i] = all[i];
     return k;
 }
@@ -1096,6 +1105,15 @@ int shmemx_fold_set_tuning(int max_blocks, int nontemporal, int unroll) {
     t.nontemporal = nontemporal < 0 ? -1 : (nontemporal & 3);
     t.unroll = unroll;
     return SHMEMX_OK;
+}
+
+int shmemx_kernel_timing(int on) { return kernel_timing(on); }
+
+int shmemx_kernel_times(double *us, int *kind, int max, unsigned long long *dropped) {
+    if (!us || max < 0) return set_error(SHMEMX_EINVAL);
+    const int n = kernel_times(us, kind, max, dropped);
+    if (n < 0) fatal("shmemx_kernel_times", "a timed kernel failed");
+    return n;
 }
 
 size_t shmemx_type_size(int type) { return type_size(type); }

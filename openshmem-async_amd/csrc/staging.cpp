@@ -178,6 +178,17 @@ static bool calls_agree(int start, int logstride, int size, size_t ncalls) {
 static void reduce_blocking_impl(int type, int op, void *target, const void *source, int nreduce,
                                  int start, int logstride, int size, bool trace_call);
 
+// A blocking call's host-view target up to this many bytes is copied back
+// into the view before the call returns ($SHMEMX_MIRROR_SETTLE_KB, default
+// 256 KiB, the bounce path's size; 0 = never): its blocks come back CLEAN.
+static size_t mirror_settle_limit() {
+    static const size_t lim = [] {
+        const char *e = std::getenv("SHMEMX_MIRROR_SETTLE_KB");
+        return (e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)256) << 10;
+    }();
+    return lim;
+}
+
 // The blocking entry point body: host- or device-resident arrays.  Operands
 // in the mirrored heap's host view run on their HBM twins (heap.h).
 void reduce_blocking(int type, int op, void *target, const void *source,
@@ -195,6 +206,10 @@ void reduce_blocking(int type, int op, void *target, const void *source,
             // library stream, its recorded writer
             heap::DeviceWrite t(target, bytes, g_state.stream);
             reduce_blocking_impl(type, op, t.ptr(), s, nreduce, start, logstride, size, false);
+            // the call's work is complete: a small result comes back into the
+            // view now, so the caller's system calls can read it (VERDICT r03
+            // #6; larger targets are fetched on first access)
+            t.settle(mirror_settle_limit());
             return;
         }
     }
@@ -334,7 +349,7 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
         // Small messages (the ISx nreduce = 1 case, isx.c:617): latency, not
         // bandwidth.  Bounce through the page-locked buffers; copy kernels on
         // the library stream move them to and from the device (no DMA
-        // command: 25 vs 33 us per call at 32 KiB, profiles/r01_host_latency.txt),
+        // command: 25 vs 33 us per call at 32 KiB, profiles/archive/r01_host_latency.txt),
         // and the host waits once.
         char *bin = static_cast<char *>(g_state.bounce);
         char *bout = bin + kSmallHostBytes;

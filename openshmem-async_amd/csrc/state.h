@@ -27,6 +27,11 @@ struct State {
     // $SHMEMX_TRANSPORT=ipc: no RCCL communicator; every collective runs over
     // the node block and IPC-mapped HBM (node.h, direct.cpp)
     bool ipc_only = false;
+    // every PE of the job has the intra-node block: agreed once at init (an
+    // RCCL all-reduce of each PE's attach result on the RCCL transport; on the
+    // IPC transport a PE without it is fatal).  AUTO's plan reads this, never
+    // per-process state, so every PE plans alike.
+    bool node_shared = false;
     // test hook ($SHMEMX_FORCE_COLLECTIVE=1): a 1-PE job still builds an RCCL
     // communicator and runs the collective schedules, so a one-GPU box can
     // execute every RCCL call of the path

@@ -97,6 +97,11 @@ def lib() -> ctypes.CDLL:
     L.shmemx_set_algo.restype = i
     L.shmemx_fold_set_tuning.argtypes = [i, i, i]
     L.shmemx_fold_set_tuning.restype = i
+    L.shmemx_kernel_timing.argtypes = [i]
+    L.shmemx_kernel_timing.restype = i
+    L.shmemx_kernel_times.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int), i,
+                                      ctypes.POINTER(ctypes.c_ulonglong)]
+    L.shmemx_kernel_times.restype = i
     L.shmemx_set_fused_twoshot_kb.argtypes = [ctypes.c_long]
     L.shmemx_set_fused_twoshot_kb.restype = ctypes.c_long
     L.shmemx_type_size.argtypes = [i]
@@ -319,6 +324,25 @@ def set_fold_tuning(max_blocks: int = 0, nontemporal: int = -1, unroll: int = 4)
     _check(lib().shmemx_fold_set_tuning(max_blocks, nontemporal, unroll), "shmemx_fold_set_tuning")
 
 
+KERNEL_KINDS = ("fold", "copy", "peers_fold", "gather")
+
+
+def kernel_timing(on: bool) -> None:
+    """shmemx_kernel_timing: time every fold-family launch from here on
+    (start/stop events of the dispatch itself, kernel time only)."""
+    lib().shmemx_kernel_timing(1 if on else 0)
+
+
+def kernel_times(max_launches: int = 4096):
+    """shmemx_kernel_times: [(kind, microseconds)] of the launches timed since
+    the last read, in launch order (waits for them), and the untimed count."""
+    us = (ctypes.c_double * max_launches)()
+    kind = (ctypes.c_int * max_launches)()
+    dropped = ctypes.c_ulonglong(0)
+    n = lib().shmemx_kernel_times(us, kind, max_launches, ctypes.byref(dropped))
+    return [(KERNEL_KINDS[kind[i]], us[i]) for i in range(n)], dropped.value
+
+
 def type_size(type_name: str) -> int:
     return lib().shmemx_type_size(TYPES[type_name])
 
@@ -384,7 +408,7 @@ def direct_stats(reset: bool = True) -> dict:
 
 
 MIRROR_STATS = ("write_faults", "read_faults", "blocks_flushed", "blocks_fetched",
-                "blocks_device_newer", "fault_waits")
+                "blocks_device_newer", "fault_waits", "blocks_settled")
 
 
 def mirror_stats(reset: bool = False) -> dict:

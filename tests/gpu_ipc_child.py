@@ -786,6 +786,29 @@ elif scenario == "mirrored":
         if not same_bits(np.frombuffer(f.read(), dtype=np.float64), want[:nb // 8]):
             fails.append("mirrored: write(2) after shmemx_mirror_acquire wrote wrong bytes")
     ncases += 1
+    # a SMALL result (<= $SHMEMX_MIRROR_SETTLE_KB, 256 KiB) comes back into the
+    # view before the blocking call returns: write(2) of it works with no
+    # shmemx_mirror_acquire, the blocks are CLEAN, and the
+    # copy-back moved only the result's bytes
+    for m, t in ((512, "double"), (1, "longlong"), ((256 << 10) // 8, "long")):
+        srcs = oracle.sources(t, 1, npes, m, base_seed=0x727 + m)
+        host_view(HEAP_SRC, oracle.NP_DTYPE[t], m)[:] = srcs[pe]
+        shm.mirror_stats(reset=True)
+        shm.to_all(t, "sum", HEAP_TGT, HEAP_SRC, m, 0, 0, npes)
+        st = shm.mirror_stats(reset=True)
+        ncases += 1
+        with tempfile.TemporaryFile() as f:
+            raw = (ctypes.c_char * (m * 8)).from_address(HEAP_TGT)
+            try:
+                wrote = os.write(f.fileno(), raw)
+            except OSError as e:
+                wrote = f"{e}"
+            f.seek(0)
+            back = np.frombuffer(f.read(), dtype=oracle.NP_DTYPE[t])
+        if wrote != m * 8 or not same_bits(back, oracle.reduce_sim(t, "sum", srcs, 0, 0, npes)[0]):
+            fails.append(f"mirrored: write(2) of a fresh {m * 8}-byte {t} result without acquire: {wrote}")
+        if st["blocks_settled"] < 1 or st["blocks_fetched"] != 0:
+            fails.append(f"mirrored: {m * 8}-byte result not settled by the call: {st}")
     # and read(2) straight into a source: acquired for writing first, then
     # the reduction sees the bytes the system call stored
     m = 50000

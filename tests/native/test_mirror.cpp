@@ -167,13 +167,93 @@ int main(int argc, char **argv) {
             g_dev[base + i] = (unsigned char)(200 + i);
             truth[base + i] = g_dev[base + i];
         }
-        M::end_device_write();
+        M::end_device_write(base, 64);
         other.join();
         truth[base + 100] = 42;
         CHECK(stored.load() == 1);
         for (size_t i = 0; i < 128; ++i) CHECK(h[base + i] == truth[base + i]);
         CHECK(M::state_of(base) == M::HOST_NEWER && M::stats(false).fault_waits >= 1);
         CHECK(M::flush(base, 1) == 1 && g_dev[base + 100] == 42 && g_dev[base + 3] == 203);
+    }
+    // (1b) A write in flight on one block does not hold up a fault on another
+    // (ADVICE r03): block 52 is DEVICE_NEWER from an earlier collective while
+    // a new one is being enqueued on block 51; a load from block 52 fetches
+    // at once.
+    {
+        const size_t w = 51 * M::kBlock, other_blk = 52 * M::kBlock;
+        M::flush(w, 2 * M::kBlock);
+        for (size_t i = other_blk; i < other_blk + 16; ++i) {
+            g_dev[i] = (unsigned char)(i * 7);
+            truth[i] = g_dev[i];
+        }
+        M::device_wrote(other_blk, 16);
+        CHECK(M::begin_device_write(w, 8) == 1);
+        std::atomic<int> loaded{0};
+        std::thread reader([&] {
+            loaded.store(h[other_blk + 3] == truth[other_blk + 3] ? 1 : 2);
+        });
+        for (int k = 0; k < 200 && !loaded.load(); ++k) std::this_thread::sleep_for(std::chrono::milliseconds(5));
+        CHECK(loaded.load() == 1);           // not waiting for block 51's write
+        for (size_t i = 0; i < 8; ++i) {
+            g_dev[w + i] = (unsigned char)(90 + i);
+            truth[w + i] = g_dev[w + i];
+        }
+        M::end_device_write(w, 8);
+        reader.join();
+        CHECK(h[w + 2] == truth[w + 2]);
+    }
+    // (1c) settle(): a blocking call's small result comes back into the view
+    // before the call returns.  A write on CLEAN blocks ("fresh") copies only
+    // its own bytes back and leaves the blocks CLEAN (no fault afterwards, a
+    // system call can read them); a write on a block that was already
+    // DEVICE_NEWER fetches the whole block; a write still in flight on the
+    // block makes settle() leave it alone.
+    {
+        const size_t b = 54 * M::kBlock + 100;
+        M::flush(54 * M::kBlock, 3 * M::kBlock);
+        bool fresh = false;
+        CHECK(M::begin_device_write(b, 40, &fresh) == 1 && fresh);
+        for (size_t i = 0; i < 40; ++i) {
+            g_dev[b + i] = (unsigned char)(17 + i);
+            truth[b + i] = g_dev[b + i];
+        }
+        M::end_device_write(b, 40);
+        const size_t d2h0 = g_d2h;
+        const auto rf0 = M::stats(false).read_faults;
+        CHECK(M::settle(b, 40, fresh) == 40 && g_d2h - d2h0 == 40);
+        CHECK(M::state_of(b) == M::CLEAN);
+        for (size_t i = 54 * M::kBlock; i < 55 * M::kBlock; i += 7) CHECK(h[i] == truth[i]);
+        CHECK(M::stats(false).read_faults == rf0);      // readable without a fault
+        int fds[2];
+        CHECK(pipe(fds) == 0);                          // and by a system call
+        CHECK(write(fds[1], const_cast<unsigned char *>(h + b), 40) == 40);
+        unsigned char got[40];
+        CHECK(read(fds[0], got, 40) == 40 && std::memcmp(got, truth.data() + b, 40) == 0);
+        close(fds[0]);
+        close(fds[1]);
+        // block 55 was DEVICE_NEWER already: not fresh, fetched whole
+        const size_t c = 55 * M::kBlock;
+        for (size_t i = c; i < c + M::kBlock; ++i) {
+            g_dev[i] = (unsigned char)(i * 5);
+            truth[i] = g_dev[i];
+        }
+        M::device_wrote(c, M::kBlock);
+        CHECK(M::begin_device_write(c + 8, 8, &fresh) == 0 && !fresh);
+        M::end_device_write(c + 8, 8);
+        CHECK(M::settle(c + 8, 8, fresh) == M::kBlock && M::state_of(c) == M::CLEAN);
+        CHECK(h[c + 1000] == truth[c + 1000]);
+        // another write in flight on block 56: settle leaves it DEVICE_NEWER
+        const size_t d = 56 * M::kBlock;
+        CHECK(M::begin_device_write(d, 8, &fresh) == 1 && fresh);
+        CHECK(M::begin_device_write(d + 64, 8) == 0);
+        for (size_t i = 0; i < 72; ++i) {
+            g_dev[d + i] = (unsigned char)(3 * i + 1);
+            truth[d + i] = g_dev[d + i];
+        }
+        M::end_device_write(d, 8);
+        CHECK(M::settle(d, 8, fresh) == 0 && M::state_of(d) == M::DEVICE_NEWER);
+        M::end_device_write(d + 64, 8);
+        CHECK(h[d + 65] == truth[d + 65] && M::state_of(d) == M::CLEAN);   // the fault path
     }
     // (2) A store another thread makes while a flush copies its block (after
     // the protection change, before the copy) is not lost: it faults, waits,

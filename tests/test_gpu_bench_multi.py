@@ -76,7 +76,16 @@ def test_bench_multi_rank_line(tmp_path, transport, npes):
     line = json.loads(lines[0])
     assert line["correct"] is True
     assert line["n_gpus"] == npes and line["steps"] == 3 and line["value"] > 0
-    assert line["roofline"]["bound"] == "xgmi" and line["cpu_baseline"] is None
+    roof = line["roofline"]
+    assert roof["bound"] == "xgmi" and "153 GB/s per link in EACH direction" in roof["peak_basis"], roof
+    assert roof["peak"] == (npes - 1) * 153.0
+    # the reference's CPU src/reduce on this host in the same run (north_star):
+    # the line's own config on N PE processes, one core each
+    cpu = line["cpu_baseline"]
+    assert isinstance(cpu, dict) and cpu["cores"] == npes and cpu["value"] > 0, cpu
+    assert cpu["unit"] == "GiB/s" and cpu["kind"] == "port" and f"on {npes} PEs" in cpu["sample"], cpu
+    sp = cpu["spread"]
+    assert sp["min_ms"] <= sp["median_ms"] <= sp["max_ms"] and sp["calls"] >= 3, sp
     extras = line["extras"]
     assert "note" not in extras, extras.get("note")     # no watchdog, no fatal signal
     for algo in ("direct", "signal"):
@@ -88,6 +97,8 @@ def test_bench_multi_rank_line(tmp_path, transport, npes):
     assert isinstance(x, dict) and x["push_visible_after_barrier"] is True, x
     assert set(x["GBps_per_gpu"]) == {"pull_one", "pull_all", "push_one", "push_all"}
     assert all(v > 0 for v in x["GBps_per_gpu"].values()), x
+    assert roof["measured_link_ceiling_GBps"] == x["GBps_per_gpu"]["pull_all"], roof
+    assert roof["frac_of_measured_links"] > 0, roof
     pa = extras["push_allreduce"]      # the store-based exchange, exact integer sums
     assert isinstance(pa, dict) and pa["correct"] is True and pa["GiBps"] > 0, pa
     bad = []

@@ -273,3 +273,52 @@ def test_fold_fuzz_against_oracle(cuda, shm, oracle, peers):
         got = from_dev(outbuf, dt)
         assert same_bits(got[offs[0]:offs[0] + n], want), (case, t, op, P, n, list(offs))
         assert not np.any(got[:offs[0]] != 0) and not np.any(got[offs[0] + n:] != 0), case
+
+
+@pytest.mark.parametrize("t", ["short", "int", "long", "float", "double", "longdouble", "complexd", "complexf"])
+def test_copy_moves_bits_every_size_offset_and_nt_path(cuda, shm, t):
+    """The copy (one input: the PE_size = 1 call, reduce-op.c:213-216) runs one
+    bit-moving kernel per element size (fold_kernels.hip launch_copy): random
+    bytes, NaN payloads and long double padding included, come out identical,
+    at every element offset mod 16 (the scalar head and tail), for lengths
+    around one workgroup's chunk, and above the 32 MiB non-temporal cut; the
+    bytes around the target are untouched."""
+    import torch
+    sz = shm.type_size(t)
+    rng = np.random.default_rng(hash(t) & 0xFFFF)
+    chunk = 256 * 8 * 16 // sz              # one workgroup: 256 lanes x 8 vectors
+    lens = [1, 3, chunk - 1, chunk, chunk + 1, 3 * chunk + 7, (17 << 20) // sz + 5]
+    for n in lens:
+        for off in range(0, 16, sz) if n < 1 << 20 else (0, 16 - sz if sz < 16 else 0):
+            src = torch.from_numpy(rng.integers(0, 256, n * sz + 64, dtype=np.uint8)).cuda()
+            dst = torch.full((n * sz + 64,), 0xA5, dtype=torch.uint8, device="cuda")
+            s_off = off if n % 2 else (off + sz) % 16   # same / different alignment mod 16
+            shm.fold_n(t, "sum", dst[off:off + n * sz], [src[s_off:s_off + n * sz]], n)
+            torch.cuda.synchronize()
+            assert torch.equal(dst[off:off + n * sz], src[s_off:s_off + n * sz]), (t, n, off, s_off)
+            assert bool((dst[:off] == 0xA5).all()) and bool((dst[off + n * sz:] == 0xA5).all()), (t, n, off)
+
+
+def test_kernel_clock_times_fold_and_copy(cuda, shm):
+    """shmemx_kernel_timing / shmemx_kernel_times: every fold-family launch
+    while on is timed by its own dispatch events, in launch order, with its
+    kind; off, nothing is recorded; results are unchanged."""
+    import torch
+    n = 8 << 20
+    a = torch.rand(n, dtype=torch.float64, device="cuda")
+    b = torch.rand(n, dtype=torch.float64, device="cuda")
+    want = a + b
+    shm.kernel_timing(True)
+    shm.fold("double", "sum", a, b, n)                       # a += b: the 2-input fold
+    shm.fold_n("double", "sum", b, [a], n)                   # b = a: the copy
+    shm.fold_n("double", "max", a, [a, b, a], n)             # the P-input fold
+    torch.cuda.synchronize()
+    kt, dropped = shm.kernel_times()
+    shm.kernel_timing(False)
+    assert [k for k, _ in kt] == ["fold", "copy", "fold"] and dropped == 0, kt
+    # 192 / 128 / 256 MiB: tens of microseconds each at HBM speed
+    assert all(5.0 < us < 5000.0 for _, us in kt), kt
+    assert torch.equal(a, want) and torch.equal(b, want)
+    shm.fold("double", "sum", a, b, n)
+    torch.cuda.synchronize()
+    assert shm.kernel_times() == ([], 0)

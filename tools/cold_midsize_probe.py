@@ -16,7 +16,8 @@ launch after its own flush, timed alone with HIP events on the stream:
   fill+read  fill, then the read sweep (the dirty lines are written back
          before the timed launch starts)
   warm   no flush, back to back
-Prints one {"config": ...} line per (flush, n, nt) in launch order, so
+usage: cold_midsize_probe.py [reps] [flush,...] [n,...] [nt,...] (nt -1 = the
+shipped choice).  Prints one {"config": ...} line per (flush, n, nt) in launch order, so
 tools/summarize_pmc.py can attach rocprofv3 FETCH_SIZE / WRITE_SIZE passes
 (run under rocprofv3 with one counter per pass).
 """
@@ -33,6 +34,8 @@ import shmem_mi355x as shm  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 flushes = sys.argv[2].split(",") if len(sys.argv) > 2 else ["fill", "read", "fill+read", "warm"]
+sizes = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [1 << 22, 1 << 24, 1 << 26]
+nts = [int(x) for x in sys.argv[4].split(",")] if len(sys.argv) > 4 else [0, 3]   # -1 = shipped auto
 torch.cuda.set_device(0)
 shm.init_attr(0, 1, 0, None)
 st = torch.cuda.Stream()
@@ -50,10 +53,10 @@ def flush(kind, k):
 
 
 for kind in flushes:
-    for n in (1 << 22, 1 << 24, 1 << 26):
+    for n in sizes:
         acc = torch.rand(n, dtype=torch.float32, device="cuda") + 1
         inp = torch.rand(n, dtype=torch.float32, device="cuda") + 1
-        for nt in (0, 3):
+        for nt in nts:
             shm.set_fold_tuning(0, nt, 4)
             torch.cuda.synchronize()
             times = []

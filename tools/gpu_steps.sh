@@ -1,0 +1,108 @@
+# The one GPU runner: `gpurun -- bash tools/gpu_steps.sh STEP [STEP ...]`.
+# Each step runs under its own time limit and writes under gpurun_out/; the
+# first step that fails (a test failure, a crash, an abort, a time limit)
+# ends the script, so nothing more touches the GPU after trouble.
+#
+#   smoke          __graft_entry__.smoke()
+#   tests          pytest -m gpu (the whole GPU suite; PE logs in gpurun_out/ipclogs)
+#   bench          the driver's default command, python bench.py (N = 1)
+#   bench2         the same again (run-to-run check of value and cpu_baseline)
+#   trace          rocprofv3 --kernel-trace --stats of the driver's command, python3 bench.py
+#   pmc            FETCH_SIZE and WRITE_SIZE of the headline, one rocprofv3 pass each, then
+#                  tools/summarize_prof.py -> gpurun_out/profiles/$TAG_{kernel_stats.csv,pmc.json}
+#   pmc_kernels    every shipped kernel (tools/pmc_kernels.py): trace + FETCH/WRITE passes
+#   soak           the randomized multi-PE soak (tests/gpu_ipc_child.py "soak"),
+#                  $SOAK_SEEDS x $SOAK_ITERS draws
+#   isx_mirror     tools/isx_mirror_latency.py with and without the small-result settle
+# $TAG names the round's files (default r04).
+#   ceiling        tools/stream_lab: copy / read / fill ceilings beside the fold
+#   midsize        the mid-size fold: tools/stream_lab fold shapes and the library's
+#                  fold after a read-only flush (cold_midsize_probe.py), under
+#                  rocprofv3 kernel traces, per size
+#   rehearse2      bench.py N = 2 on the IPC transport, both ranks on this GPU
+#   rehearse8      the same with 8 ranks
+#   rehearse_rccl  bench.py N = 2 on the RCCL transport against the RCCL test double
+set -u
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+export TMPDIR=/tmp
+ulimit -c 0
+O=gpurun_out
+
+run() {   # run <seconds> <log> <cmd...>: one GPU step under its own limit
+    local secs=$1 log=$2; shift 2
+    timeout -k 10 "$secs" "$@" > "$log" 2>&1
+    local rc=$?
+    echo "[$(date +%T)] $* -> rc=$rc"
+    [ $rc -eq 0 ] || { tail -25 "$log"; exit $rc; }
+}
+
+BENCH_HEAD="python3 bench.py --steps 20 --warmup 5 --extras 0 --no-cpu-baseline"
+TAG=${TAG:-r04}
+
+for step in "$@"; do
+    case $step in
+    smoke) run 300 $O/smoke.log python3 -c "import __graft_entry__ as g; g.smoke()"; tail -2 $O/smoke.log ;;
+    tests)
+        export GPU_TEST_LOGDIR=$O/ipclogs
+        run 1100 $O/gpu_tests.log python3 -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread
+        tail -3 $O/gpu_tests.log ;;
+    bench) run 600 $O/bench_n1.json python3 bench.py; grep '"metric"' $O/bench_n1.json | cut -c1-400 ;;
+    bench2) run 600 $O/bench_n1_b.json python3 bench.py; grep '"metric"' $O/bench_n1_b.json | cut -c1-400 ;;
+    trace)
+        run 600 $O/trace.log rocprofv3 --kernel-trace --stats -d $O/trace -o trace --output-format csv -- python3 bench.py
+        grep '"metric"' $O/trace.log | cut -c1-300
+        python3 tools/trace_by_grid.py $O/trace fold > $O/trace_by_grid.txt; cat $O/trace_by_grid.txt ;;
+    pmc)
+        run 200 $O/pmc_fetch.log timeout -s KILL 180 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o fetch --output-format csv -- $BENCH_HEAD
+        run 200 $O/pmc_write.log timeout -s KILL 180 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o write --output-format csv -- $BENCH_HEAD
+        PROFILES_OUT=$O/profiles python3 tools/summarize_prof.py $O/trace $O/pmc_fetch $O/pmc_write $TAG > $O/prof_summary.json 2>&1
+        head -40 $O/prof_summary.json ;;
+    pmc_kernels)
+        run 300 $O/pmc_kernels.log python3 tools/pmc_kernels.py
+        run 300 $O/pk_trace.log rocprofv3 --kernel-trace --stats -d $O/pk_trace -o trace --output-format csv -- python3 tools/pmc_kernels.py
+        run 320 $O/pk_fetch.log timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $O/pk_fetch -o fetch --output-format csv -- python3 tools/pmc_kernels.py
+        run 320 $O/pk_write.log timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $O/pk_write -o write --output-format csv -- python3 tools/pmc_kernels.py
+        python3 tools/summarize_pmc.py $O/pmc_kernels.log $O/pk_trace $O/pk_fetch $O/pk_write $O/${TAG}_pmc_kernels.json > $O/pk_summary.txt 2>&1
+        cp $O/pk_trace/*/*kernel_stats.csv $O/${TAG}_pmc_kernels_stats.csv 2>/dev/null || cp $O/pk_trace/*kernel_stats.csv $O/${TAG}_pmc_kernels_stats.csv
+        head -80 $O/pk_summary.txt ;;
+    soak)
+        for seed in ${SOAK_SEEDS:-51}; do
+            SOAK_ITERS=${SOAK_ITERS:-1000} SOAK_SEED=$seed GPU_TEST_LOGDIR=$O/soak_logs_$seed run 600 $O/soak_$seed.log \
+                python3 -u -m pytest tests/test_gpu_ipc.py -k soak -x -v --timeout 580 --timeout-method thread
+            grep -E "PASSED|FAILED|passed|failed" $O/soak_$seed.log | tail -6
+        done ;;
+    isx_mirror)
+        SHMEMX_MIRROR_SETTLE_KB=0 run 120 $O/isx_mirror_before.json python3 tools/isx_mirror_latency.py 3000
+        run 120 $O/isx_mirror_after.json python3 tools/isx_mirror_latency.py 3000
+        SHMEMX_FORCE_COLLECTIVE=1 SHMEMX_MIRROR_SETTLE_KB=0 run 120 $O/isx_mirror_coll_before.json python3 tools/isx_mirror_latency.py 2000
+        SHMEMX_FORCE_COLLECTIVE=1 run 120 $O/isx_mirror_coll_after.json python3 tools/isx_mirror_latency.py 2000
+        cat $O/isx_mirror_*.json ;;
+    ceiling)
+        for nd in 33554432 67108864; do
+            run 300 $O/stream_lab_ceiling_$nd.txt ./tools/stream_lab $nd 3 10 ceiling
+            cut -c1-260 $O/stream_lab_ceiling_$nd.txt
+        done ;;
+    midsize)
+        for nd in 524288 2097152 8388608; do
+            run 300 $O/midsize_lab_$nd.txt rocprofv3 --kernel-trace --stats -d $O/midsize_lab_$nd -o t \
+                --output-format csv -- ./tools/stream_lab $nd 3 20 fold
+            python3 tools/trace_by_grid.py $O/midsize_lab_$nd > $O/midsize_lab_${nd}_trace.txt
+        done
+        run 300 $O/midsize_probe.txt rocprofv3 --kernel-trace --stats -d $O/midsize_probe -o t --output-format csv \
+            -- python3 tools/cold_midsize_probe.py 20 read,warm 1048576,4194304,16777216 -1
+        python3 tools/trace_by_grid.py $O/midsize_probe fold_kernel > $O/midsize_probe_trace.txt
+        cat $O/midsize_probe.txt | grep config; cat $O/midsize_probe_trace.txt ;;
+    rehearse2|rehearse8)
+        np=${step#rehearse}
+        SHMEMX_TRANSPORT=ipc SHMEMX_SHARE_GPU=1 run 900 $O/rehearse_ipc_n$np.json python3 -m torch.distributed.run \
+            --nnodes=1 --nproc-per-node $np --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus $np \
+            --steps 10 --warmup 3
+        grep '"metric"' $O/rehearse_ipc_n$np.json | cut -c1-600 ;;
+    rehearse_rccl)
+        FAKE_RCCL=$PWD/tests/native/libfake_rccl.so SHMEMX_SHARE_GPU=1 run 900 $O/rehearse_rccl_n2.json \
+            python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+            --master-port 29512 bench.py --gpus 2 --steps 10 --warmup 3
+        grep '"metric"' $O/rehearse_rccl_n2.json | cut -c1-600 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+    esac
+done

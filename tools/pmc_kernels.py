@@ -1,6 +1,6 @@
 """Every shipped kernel of the path, launched through the C ABI at the sizes
 VERDICT r01 asks counters for, for rocprofv3 passes (kernel trace, then
-FETCH_SIZE and WRITE_SIZE in separate --pmc runs; tools/gpu_pmc_all.sh):
+FETCH_SIZE and WRITE_SIZE in separate --pmc runs; tools/gpu_steps.sh pmc_kernels):
 
   fold2_double_sum   fold_kernel, 2 inputs, acc += in, 32 Mi doubles (headline)
   fold2_long_{and,or,xor}   2 inputs, 64 Mi longs (configs[3]'s fold)

@@ -1,0 +1,312 @@
+// Experiment harness (not part of the library): the chip's streaming
+// ceilings on gfx950, next to the library's 2-input fold, so the bench's
+// "measured ceiling" is a kernel the fold does not beat.
+//
+//   copy   out[i] = in[i]            1 read : 1 write (the PE_size = 1 call)
+//   read   x ^= in[i] over 1..3 arrays  reads only (no store per element)
+//   fill   out[i] = c                writes only
+//   fold   acc[i] += in[i]           2 reads : 1 write (the headline kernel)
+//   dma    hipMemcpyAsync D2D        the runtime's own copy
+//
+// Block size B, U 16-B vectors per lane, NT bit 0 = non-temporal loads,
+// bit 1 = non-temporal stores.  Every variant runs `rounds` interleaved
+// rounds of `reps` launches, each launch timed alone with HIP events, warm
+// (back to back) and cold (a default-policy read of a 1 GiB scratch before
+// every launch); kernel-only durations from hipExtLaunchKernelGGL's events,
+// and for cold also the in-stream cost including deferred write-backs (see
+// main).  Prints medians in us and TB/s of algorithmic bytes.
+//
+// usage: stream_lab [doubles per array] [rounds] [reps] [ceiling|fold]
+// Build: hipcc --offload-arch=gfx950 -O3 tools/stream_lab.hip -o tools/stream_lab
+#include <hip/hip_ext.h>
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+#define CK(x)                                                                  \
+    do {                                                                     \
+        hipError_t e = (x);                                                  \
+        if (e != hipSuccess) {                                               \
+            printf("%s: %s\n", #x, hipGetErrorString(e));                    \
+            exit(1);                                                         \
+        }                                                                    \
+    } while (0)
+
+template <int NT>
+__device__ __forceinline__ u32x4 ld(const u32x4 *p) {
+    if constexpr (NT & 1) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <int NT>
+__device__ __forceinline__ void st(u32x4 *p, u32x4 v) {
+    if constexpr (NT & 2) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+// one chunk of B*U vectors per block (the library's shape), nvec a multiple
+template <int B, int U, int NT>
+__global__ __launch_bounds__(B) void k_copy(u32x4 *out, const u32x4 *in, size_t nvec) {
+    const size_t base = (size_t)blockIdx.x * B * U + threadIdx.x;
+    u32x4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = ld<NT>(in + base + u * B);
+#pragma unroll
+    for (int u = 0; u < U; ++u) st<NT>(out + base + u * B, x[u]);
+}
+
+// grid-stride copy with a fixed grid (persistent), loads of step k+1 issued
+// before the stores of step k
+template <int B, int U, int NT>
+__global__ __launch_bounds__(B) void k_copy_pers(u32x4 *out, const u32x4 *in, size_t nvec) {
+    const size_t step = (size_t)gridDim.x * B * U;
+    size_t base = (size_t)blockIdx.x * B * U + threadIdx.x;
+    u32x4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = ld<NT>(in + base + u * B);
+    for (; base + step < nvec; base += step) {
+        u32x4 y[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) y[u] = ld<NT>(in + base + step + u * B);
+#pragma unroll
+        for (int u = 0; u < U; ++u) st<NT>(out + base + u * B, x[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = y[u];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) st<NT>(out + base + u * B, x[u]);
+}
+
+template <int B, int U, int NT, int NARR>
+__global__ __launch_bounds__(B) void k_read(const u32x4 *a, const u32x4 *b, const u32x4 *c, size_t nvec,
+                                            unsigned *sink) {
+    const size_t base = (size_t)blockIdx.x * B * U + threadIdx.x;
+    u32x4 x[NARR][U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[0][u] = ld<NT>(a + base + u * B);
+    if constexpr (NARR > 1) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[1][u] = ld<NT>(b + base + u * B);
+    }
+    if constexpr (NARR > 2) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[NARR - 1][u] = ld<NT>(c + base + u * B);
+    }
+    unsigned r = 0;
+#pragma unroll
+    for (int k = 0; k < NARR; ++k)
+#pragma unroll
+        for (int u = 0; u < U; ++u) r ^= x[k][u].x ^ x[k][u].y ^ x[k][u].z ^ x[k][u].w;
+    if (r == 0x9E3779B9u) sink[0] = r;   // never true for the lab's data; keeps the loads
+}
+
+template <int B, int U, int NT>
+__global__ __launch_bounds__(B) void k_fill(u32x4 *out, size_t nvec, unsigned c) {
+    const size_t base = (size_t)blockIdx.x * B * U + threadIdx.x;
+    u32x4 v = {c, c, c, c};
+#pragma unroll
+    for (int u = 0; u < U; ++u) st<NT>(out + base + u * B, v);
+}
+
+template <int B, int U, int NT>
+__global__ __launch_bounds__(B) void k_fold(u32x4 *acc, const u32x4 *in, size_t nvec) {
+    typedef double f64x2 __attribute__((ext_vector_type(2)));
+    const size_t base = (size_t)blockIdx.x * B * U + threadIdx.x;
+    u32x4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) a[u] = ld<NT>(acc + base + u * B);
+#pragma unroll
+    for (int u = 0; u < U; ++u) b[u] = ld<NT>(in + base + u * B);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        f64x2 s = __builtin_bit_cast(f64x2, a[u]) + __builtin_bit_cast(f64x2, b[u]);
+        st<NT>(acc + base + u * B, __builtin_bit_cast(u32x4, s));
+    }
+}
+
+// persistent grid-stride fold, fixed grid G
+template <int B, int U, int NT>
+__global__ __launch_bounds__(B) void k_fold_pers(u32x4 *acc, const u32x4 *in, size_t nvec) {
+    typedef double f64x2 __attribute__((ext_vector_type(2)));
+    for (size_t base = (size_t)blockIdx.x * B * U + threadIdx.x; base < nvec; base += (size_t)gridDim.x * B * U) {
+        u32x4 a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) a[u] = ld<NT>(acc + base + u * B);
+#pragma unroll
+        for (int u = 0; u < U; ++u) b[u] = ld<NT>(in + base + u * B);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            f64x2 s = __builtin_bit_cast(f64x2, a[u]) + __builtin_bit_cast(f64x2, b[u]);
+            st<NT>(acc + base + u * B, __builtin_bit_cast(u32x4, s));
+        }
+    }
+}
+
+__global__ void k_flush(const u32x4 *p, size_t nvec, unsigned *sink) {
+    unsigned r = 0;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
+        u32x4 v = p[i];
+        r ^= v.x ^ v.w;
+    }
+    if (r == 0x9E3779B9u) sink[1] = r;
+}
+
+struct Variant {
+    std::string name;
+    double bytes;
+    // launch on the stream; with events, as hipExtLaunchKernelGGL's start /
+    // stop events (the dispatch's own timestamps: kernel time only)
+    std::function<void(hipStream_t, hipEvent_t, hipEvent_t)> run;
+};
+
+int main(int argc, char **argv) {
+    const size_t n_dbl = argc > 1 ? strtoull(argv[1], 0, 0) : (size_t)32 << 20;   // doubles per array
+    const int rounds = argc > 2 ? atoi(argv[2]) : 5;
+    const int reps = argc > 3 ? atoi(argv[3]) : 10;
+    const size_t bytes = n_dbl * 8, nvec = bytes / 16;
+    if (nvec % 4096) { printf("n must be a multiple of 8192 doubles\n"); return 1; }
+    u32x4 *a, *b, *c, *scratch;
+    unsigned *sink;
+    CK(hipMalloc(&a, bytes));
+    CK(hipMalloc(&b, bytes));
+    CK(hipMalloc(&c, bytes));
+    const size_t sbytes = (size_t)1 << 30;
+    CK(hipMalloc(&scratch, sbytes));
+    CK(hipMalloc(&sink, 64));
+    CK(hipMemset(a, 0x11, bytes));
+    CK(hipMemset(b, 0x22, bytes));
+    CK(hipMemset(c, 0x33, bytes));
+    CK(hipMemset(scratch, 0x44, sbytes));
+    hipStream_t s;
+    CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+
+    std::vector<Variant> vs;
+#define GRID(B, U) dim3((unsigned)(nvec / ((B) * (U))))
+#define COPY(B, U, NT)                                                                        \
+    vs.push_back({"copy B" #B " U" #U " nt" #NT, 2.0 * bytes, [=](hipStream_t st, hipEvent_t k0, hipEvent_t k1) {           \
+        hipExtLaunchKernelGGL((k_copy<B, U, NT>), GRID(B, U), dim3(B), 0, st, k0, k1, 0, c, b, nvec); }})
+#define COPYP(B, U, NT, G)                                                                    \
+    vs.push_back({"copy_pers B" #B " U" #U " nt" #NT " G" #G, 2.0 * bytes, [=](hipStream_t st, hipEvent_t k0, hipEvent_t k1) { \
+        hipExtLaunchKernelGGL((k_copy_pers<B, U, NT>), dim3(G), dim3(B), 0, st, k0, k1, 0, c, b, nvec); }})
+#define READ(B, U, NT, K)                                                                     \
+    vs.push_back({"read" #K " B" #B " U" #U " nt" #NT, (double)K * bytes, [=](hipStream_t st, hipEvent_t k0, hipEvent_t k1) { \
+        hipExtLaunchKernelGGL((k_read<B, U, NT, K>), GRID(B, U), dim3(B), 0, st, k0, k1, 0, a, b, c, nvec, sink); }})
+#define FILL(B, U, NT)                                                                        \
+    vs.push_back({"fill B" #B " U" #U " nt" #NT, 1.0 * bytes, [=](hipStream_t st, hipEvent_t k0, hipEvent_t k1) {           \
+        hipExtLaunchKernelGGL((k_fill<B, U, NT>), GRID(B, U), dim3(B), 0, st, k0, k1, 0, c, nvec, 7u); }})
+#define FOLD(B, U, NT)                                                                        \
+    vs.push_back({"fold B" #B " U" #U " nt" #NT, 3.0 * bytes, [=](hipStream_t st, hipEvent_t k0, hipEvent_t k1) {           \
+        hipExtLaunchKernelGGL((k_fold<B, U, NT>), GRID(B, U), dim3(B), 0, st, k0, k1, 0, a, b, nvec); }})
+
+    const std::string set = argc > 4 ? argv[4] : "ceiling";
+#define FOLDP(B, U, NT, G)                                                                    \
+    vs.push_back({"fold_pers B" #B " U" #U " nt" #NT " G" #G, 3.0 * bytes, [=](hipStream_t st, hipEvent_t k0, hipEvent_t k1) { \
+        hipExtLaunchKernelGGL((k_fold_pers<B, U, NT>), dim3(G), dim3(B), 0, st, k0, k1, 0, a, b, nvec); }})
+    if (set == "fold") {   // the mid-size fold's shapes
+        FOLD(256, 4, 3);
+        FOLD(256, 4, 0);
+        FOLD(256, 2, 3);
+        FOLD(256, 2, 0);
+        FOLD(256, 1, 3);
+        FOLD(256, 1, 0);
+        FOLD(512, 2, 3);
+        FOLD(128, 4, 3);
+        FOLDP(256, 2, 3, 512);
+        FOLDP(256, 2, 3, 1024);
+        FOLDP(256, 1, 3, 2048);
+        COPY(256, 4, 3);
+        READ(256, 4, 1, 2);
+    } else {
+    FOLD(256, 4, 3);
+    FOLD(256, 4, 0);
+    COPY(256, 4, 3);
+    COPY(256, 4, 0);
+    COPY(256, 4, 1);
+    COPY(256, 4, 2);
+    COPY(256, 8, 3);
+    COPY(256, 2, 3);
+    COPY(256, 16, 3);
+    COPY(512, 4, 3);
+    COPY(1024, 4, 3);
+    COPYP(256, 4, 3, 2048);
+    COPYP(256, 4, 3, 4096);
+    COPYP(256, 8, 3, 2048);
+    READ(256, 4, 1, 1);
+    READ(256, 4, 0, 1);
+    READ(256, 4, 1, 2);
+    READ(256, 4, 1, 3);
+    READ(256, 8, 1, 2);
+    READ(256, 4, 0, 3);
+    FILL(256, 4, 2);
+    FILL(256, 4, 0);
+    vs.push_back({"dma hipMemcpyAsync D2D", 2.0 * bytes,
+                  [=](hipStream_t st, hipEvent_t k0, hipEvent_t k1) {
+                      if (k0) CK(hipEventRecord(k0, st));
+                      CK(hipMemcpyAsync(c, b, bytes, hipMemcpyDeviceToDevice, st));
+                      if (k1) CK(hipEventRecord(k1, st));
+                  }});
+    }
+
+    // warm: back to back; cold: a default-policy read of a 1 GiB scratch
+    // before every launch.  Per launch: the kernel's own duration (ext-launch
+    // events) and, for cold, the in-stream cost = (flush + kernel) - flush
+    // over `reps` pairs with events at the ends only: it also charges the
+    // write-back of dirty lines the kernel left in the Infinity Cache, which
+    // the next flush pays (a deferred write is not bandwidth).
+    auto flush = [&](hipStream_t st) {
+        hipLaunchKernelGGL(k_flush, dim3(4096), dim3(256), 0, st, scratch, sbytes / 16, sink);
+    };
+    for (int cold = 0; cold < 2; ++cold) {
+        std::vector<std::vector<float>> t(vs.size()), d(vs.size());
+        for (auto &v : vs) { v.run(s, nullptr, nullptr); v.run(s, nullptr, nullptr); }
+        CK(hipStreamSynchronize(s));
+        for (int r = 0; r < rounds; ++r)
+            for (size_t i = 0; i < vs.size(); ++i) {
+                for (int k = 0; k < reps; ++k) {
+                    if (cold) flush(s);
+                    vs[i].run(s, e0, e1);
+                    CK(hipEventSynchronize(e1));
+                    float ms;
+                    CK(hipEventElapsedTime(&ms, e0, e1));
+                    t[i].push_back(ms);
+                }
+                if (cold) {
+                    float pair, alone;
+                    CK(hipEventRecord(e0, s));
+                    for (int k = 0; k < reps; ++k) { flush(s); vs[i].run(s, nullptr, nullptr); }
+                    flush(s);
+                    CK(hipEventRecord(e1, s));
+                    CK(hipEventSynchronize(e1));
+                    CK(hipEventElapsedTime(&pair, e0, e1));
+                    CK(hipEventRecord(e0, s));
+                    for (int k = 0; k <= reps; ++k) flush(s);
+                    CK(hipEventRecord(e1, s));
+                    CK(hipEventSynchronize(e1));
+                    CK(hipEventElapsedTime(&alone, e0, e1));
+                    d[i].push_back((pair - alone) / reps);
+                }
+            }
+        for (size_t i = 0; i < vs.size(); ++i) {
+            std::sort(t[i].begin(), t[i].end());
+            std::sort(d[i].begin(), d[i].end());
+            const double med = t[i][t[i].size() / 2] * 1e-3, lo = t[i].front() * 1e-3;
+            const double dm = cold ? d[i][d[i].size() / 2] * 1e-3 : 0;
+            printf("{\"variant\": \"%s\", \"mode\": \"%s\", \"MiB_per_array\": %zu, \"kernel_median_us\": %.2f, "
+                   "\"kernel_min_us\": %.2f, \"TBps\": %.3f, \"TBps_best\": %.3f, \"in_stream_us\": %.2f, "
+                   "\"in_stream_TBps\": %.3f}\n",
+                   vs[i].name.c_str(), cold ? "cold" : "warm", bytes >> 20, med * 1e6, lo * 1e6,
+                   vs[i].bytes / med / 1e12, vs[i].bytes / lo / 1e12, dm * 1e6, dm > 0 ? vs[i].bytes / dm / 1e12 : 0.0);
+        }
+        fflush(stdout);
+    }
+    return 0;
+}

@@ -74,7 +74,7 @@ def main():
                       "traffic_over_alg": round(hbm / c["alg_bytes"], 4)})
         out.append(e)
     with open(dst, "w") as fh:
-        json.dump({"source": "tools/pmc_kernels.py + rocprofv3 (tools/gpu_pmc_all.sh)",
+        json.dump({"source": "tools/pmc_kernels.py + rocprofv3 (tools/gpu_steps.sh pmc_kernels)",
                    "configs": out}, fh, indent=1)
     print(json.dumps(out, indent=1))
 

@@ -37,7 +37,8 @@ def counter_values(d, counter):
 
 def main():
     trace, fetch, write, tag = sys.argv[1:5]
-    out = os.path.join(REPO, "profiles")
+    # on the GPU box: $PROFILES_OUT under gpurun_out/ (merged back), else profiles/
+    out = os.environ.get("PROFILES_OUT") or os.path.join(REPO, "profiles")
     os.makedirs(out, exist_ok=True)
     stats = find(trace, "*kernel_stats.csv")
     summary = {}
