@@ -89,10 +89,10 @@ int main(void)
         if (pSync[i] != SHMEM_SYNC_VALUE) { printf("PE %d: pSync[%d] changed\n", me, i); fail = 1; }
     if (shmemx_reduce_last_error()) { printf("PE %d: last error %d\n", me, shmemx_reduce_last_error()); fail = 1; }
     if (heap && heap[0] == '1') {
-        unsigned long long st[5] = {0, 0, 0, 0, 0};
-        shmemx_mirror_stats(st, 5, 0);
-        printf("PE %d: mirror write faults %llu read faults %llu flushed %llu fetched %llu blocks\n", me,
-               st[0], st[1], st[2], st[3]);
+        unsigned long long st[7] = {0, 0, 0, 0, 0, 0, 0};
+        shmemx_mirror_stats(st, 7, 0);
+        printf("PE %d: mirror write faults %llu read faults %llu flushed %llu fetched %llu settled %llu blocks\n",
+               me, st[0], st[1], st[2], st[3], st[6]);
     }
     const long long total = total_num_keys;
     shmem_finalize();

@@ -1,8 +1,10 @@
 #!/bin/bash
 # TEST INFRASTRUCTURE ONLY: compiles the part of the reference's hot path that
 # builds on its own -- the element operations of reduce-op.c (:71-150) -- from
-# the source where it lies, into oracle/_ref/libref_ops.so (git-ignored; the
-# .so travels to the GPU box with the tree, the reference text never does).
+# the source where it lies, into oracle/_ref/libref_ops.so.  It stays in this
+# container: git-ignored, and listed in .gpurunignore so that neither the
+# reference's text nor an object built from it ever reaches the GPU box (the
+# GPU tests read tests/golden/ref_element_ops.json, the outputs it computed).
 #
 # The text is read between two markers and piped straight into gcc after
 # <complex.h>, followed by oracle/ref_ops_harness.c (the exported wrapper);

@@ -930,6 +930,37 @@ elif scenario == "mixed":
             fails.append(f"mixed kinds n={n} (one call either way): error {err} / wrong result")
         # the same call with matching kinds right after
         run_case("double", "sum", n, (0, 0, npes), "auto", "device", 0x77 + n)
+elif scenario == "limits":
+    # DIRECT members whose size limits differ: every member returns ENOTSUP
+    # with its target untouched, the member that differed aligns at once, and
+    # the next call is correct everywhere.  20 rounds back to back: the ENOTSUP
+    # path ends with a barrier, so a member that retries at once
+    # cannot overwrite its descriptor before a slower member has read it.
+    import time
+    default_kb = shm.set_fused_twoshot_kb(4096)
+    shm.set_fused_twoshot_kb(default_kb)
+    for rep in range(20):
+        n = (100003, 7, 300001)[rep % 3]
+        if pe == rep % npes:
+            shm.set_fused_twoshot_kb(default_kb + 1024)
+        srcs = oracle.sources("double", 1, npes, n, base_seed=0x11B0 + rep)
+        s = to_dev(torch, np.ascontiguousarray(srcs[pe]))
+        d = to_dev(torch, np.zeros(n))
+        torch.cuda.synchronize()
+        t0 = time.time()
+        try:
+            shm.reduce_on_stream("double", "sum", d, s, n, 0, 0, npes, "direct")
+            err = 0
+        except shm.ShmemError as e:
+            err = e.code
+        torch.cuda.synchronize()
+        ncases += 1
+        if err != 3 or time.time() - t0 > 30 or bool(d.abs().sum().item()):
+            fails.append(f"limits rep {rep}: error {err} after {time.time() - t0:.1f} s, want ENOTSUP, "
+                         "target untouched")
+        if pe == rep % npes:
+            shm.set_fused_twoshot_kb(default_kb)
+        run_case("double", "sum", n, (0, 0, npes), "direct", "device", 0x11C0 + rep)
 elif scenario == "signal_timeout":
     # one SIGNAL call together (maps and votes), then PE 0 calls again alone:
     # its device barrier must give up after $SHMEMX_SIGNAL_TIMEOUT seconds and

@@ -126,3 +126,17 @@ def test_oracle_matches_reference_on_random_bits(oracle, t):
         tg = oracle.reduce_sim(t, op, np.stack([a, b]), 0, 0, 2)
         assert _value_bytes(tg[0]) == _value_bytes(_ref_apply(L, oracle, t, op, a, b)), (t, op)
         assert _value_bytes(tg[1]) == _value_bytes(_ref_apply(L, oracle, t, op, b, a)), (t, op)
+
+
+def test_reference_build_stays_in_this_container():
+    """oracle/_ref (an object compiled from the reference's text) never travels
+    to the GPU box: .gpurunignore lists it (SURVEY.md "neither source nor
+    objects ship"), and no GPU test loads it (they read the golden fixture)."""
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(repo, ".gpurunignore")) as f:
+        pats = [ln.strip() for ln in f if ln.strip() and not ln.startswith("#")]
+    assert "./oracle/_ref" in pats, pats
+    for name in os.listdir(os.path.join(repo, "tests")):
+        if name.startswith("test_gpu") and name.endswith(".py"):
+            with open(os.path.join(repo, "tests", name)) as f:
+                assert "libref_ops" not in f.read(), name
