@@ -282,38 +282,44 @@ def config_extras(world, stream, barrier, max_over_ranks, cap=256 * 1024 * 1024)
         for _ in range(2):
             fn()
         if cold:
-            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                  for _ in range(steps)]
-            barrier()
-            torch.cuda.synchronize()
-            if world == 1:
-                # N = 1: each fold's own duration from the library's kernel
-                # clock (its dispatch's events); the marker events around it
-                # add the launch boundary and their own latency (~5-6 us,
-                # profiles/r04_midsize.txt), which a cold step of a few us
-                # cannot amortise
-                shm.kernel_timing(True)
-            with torch.cuda.stream(stream):
-                for k, (e0, e1) in enumerate(ev):
-                    if cold == "dirty":
-                        scratch.fill_(k & 0xFF)
-                    else:
-                        scratch64.sum()
-                    e0.record(stream)
-                    fn()
-                    e1.record(stream)
-            torch.cuda.synchronize()
-            w_ev = sum(e0.elapsed_time(e1) for e0, e1 in ev) * 1e-3
+            def cold_pass(clock):
+                """`steps` flushed steps; marker-event seconds, and with the
+                kernel clock on each fold's own duration (us list)"""
+                ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                      for _ in range(steps)]
+                barrier()
+                torch.cuda.synchronize()
+                if clock:
+                    shm.kernel_timing(True)
+                with torch.cuda.stream(stream):
+                    for k, (e0, e1) in enumerate(ev):
+                        if cold == "dirty":
+                            scratch.fill_(k & 0xFF)
+                        else:
+                            scratch64.sum()
+                        e0.record(stream)
+                        fn()
+                        e1.record(stream)
+                torch.cuda.synchronize()
+                kern = None
+                if clock:
+                    kt, _ = shm.kernel_times()
+                    shm.kernel_timing(False)
+                    kern = [us for kind, us in kt if kind == "fold"]
+                return sum(e0.elapsed_time(e1) for e0, e1 in ev) * 1e-3, kern
+            w_ev, _ = cold_pass(False)
             w = w_ev
             if world == 1:
-                kt, _ = shm.kernel_times()
-                shm.kernel_timing(False)
-                kern = [us for kind, us in kt if kind == "fold"]
-                if len(kern) == steps:
+                # N = 1: each fold's own duration from the library's kernel
+                # clock (its dispatch's events), in a pass of its own; the
+                # marker events of the pass above add the launch boundary and
+                # their own latency, which a step of a few us cannot amortise
+                _, kern = cold_pass(True)
+                if kern and len(kern) == steps:
                     w = sum(kern) * 1e-6
                     detail.setdefault(cold, {})[str(n)] = {
                         "kernel_us": round(statistics.median(kern), 2),
-                        "event_us": round(w_ev / steps * 1e6, 2)}
+                        "marker_event_us": round(w_ev / steps * 1e6, 2)}
         else:
             w, _ = time_region(fn, steps, stream, barrier)
         w = max_over_ranks(w)
@@ -337,8 +343,8 @@ def config_extras(world, stream, barrier, max_over_ranks, cap=256 * 1024 * 1024)
         "step and only the steps are timed, so every step reads and writes HBM; GiB/s = PEs x "
         "nreduce x 4 B / step.  N = 1: the step is the fold kernel's own duration (the library's "
         "kernel clock, shmemx_kernel_times: start/stop events of the dispatch itself); "
-        "float_sum_us_vs_nreduce gives it beside the marker-event time around the same launch, whose "
-        "difference is the launch boundary plus the markers' latency, not kernel work.  N > 1: "
+        "float_sum_us_vs_nreduce gives it beside the marker-event time around each launch (a separate "
+        "pass), whose difference is the launch boundary plus the markers' latency, not kernel work.  N > 1: "
         "marker events around the whole collective")
     if detail.get("clean"):
         out["float_sum_us_vs_nreduce"] = detail["clean"]

@@ -226,8 +226,19 @@ void mir_to_device(uint64_t off, size_t bytes, void *) {
     });
 }
 
+void mir_copy_to_host(uint64_t off, size_t bytes);
+
 void mir_to_host(uint64_t off, size_t bytes, void *) {
     wait_writers();
+    mir_copy_to_host(off, bytes);
+}
+
+// settle(): a blocking call's result, whose work has completed (its host
+// signal arrived), so no writer event is waited for (~half of the copy-back's
+// cost, profiles/r04_isx_mirror.txt)
+void mir_to_host_done(uint64_t off, size_t bytes, void *) { mir_copy_to_host(off, bytes); }
+
+void mir_copy_to_host(uint64_t off, size_t bytes) {
     const hipStream_t fs = mir_fetch_stream();
     mir_by_region(off, bytes, [fs](uint64_t o, size_t len, bool locked) {
         char *dst = mirror::alias_base() + o;
@@ -291,7 +302,8 @@ bool ensure_segment() {
         node::publish(node::kHeap, p, bytes);   // peers map it after the allocation's barrier
         if (mirrored()) {
             if (!mirror::create(g_heap.arena.capacity(), mirror::Backend{mir_to_device, mir_to_host,
-                                                                        mir_drain, nullptr}))
+                                                                        mir_drain, nullptr,
+                                                                        mir_to_host_done}))
                 fatal("shmem_malloc", "cannot reserve the host view of the mirrored heap");
             g_heap.view = mirror::host_base();
         }

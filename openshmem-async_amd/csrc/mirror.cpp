@@ -315,8 +315,9 @@ size_t settle(uint64_t off, size_t bytes, bool fresh) {
         fetch_run(b0, b1 - b0, false);
         return (b1 - b0) * kBlock;
     }
-    // the rest of every block already equals HBM: only the written bytes move
-    g_view.be.to_host(off, bytes, g_view.be.ctx);
+    // the rest of every block already equals HBM: only the written bytes
+    // move, and their writer has completed (the caller's contract)
+    (g_view.be.to_host_done ? g_view.be.to_host_done : g_view.be.to_host)(off, bytes, g_view.be.ctx);
     protect(b0, b1 - b0, PROT_READ);
     std::memset(g_view.state + b0, CLEAN, b1 - b0);
     g_view.st.blocks_settled += b1 - b0;

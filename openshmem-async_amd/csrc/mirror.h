@@ -64,6 +64,10 @@ struct Backend {
     // every to_device issued so far has landed
     void (*drain)(void *ctx);
     void *ctx;
+    // settle()'s copy: as to_host, for bytes whose writer is known to have
+    // completed (a blocking call that has returned), so it waits for no
+    // writer; nullptr = to_host
+    void (*to_host_done)(uint64_t off, size_t bytes, void *ctx) = nullptr;
 };
 
 // Reserve a host view of `bytes` (rounded up to kBlock) and its alias, every

@@ -5,6 +5,7 @@
 #
 #   smoke          __graft_entry__.smoke()
 #   tests          pytest -m gpu (the whole GPU suite; PE logs in gpurun_out/ipclogs)
+#   tests_k        the GPU tests matching $TESTS_K (pytest -k)
 #   bench          the driver's default command, python bench.py (N = 1)
 #   bench2         the same again (run-to-run check of value and cpu_baseline)
 #   trace          rocprofv3 --kernel-trace --stats of the driver's command, python3 bench.py
@@ -46,6 +47,10 @@ for step in "$@"; do
         export GPU_TEST_LOGDIR=$O/ipclogs
         run 1100 $O/gpu_tests.log python3 -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread
         tail -3 $O/gpu_tests.log ;;
+    tests_k)   # a subset: TESTS_K="expr" (pytest -k)
+        export GPU_TEST_LOGDIR=$O/ipclogs
+        run 900 $O/gpu_tests_k.log python3 -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread -k "$TESTS_K"
+        tail -3 $O/gpu_tests_k.log ;;
     bench) run 600 $O/bench_n1.json python3 bench.py; grep '"metric"' $O/bench_n1.json | cut -c1-400 ;;
     bench2) run 600 $O/bench_n1_b.json python3 bench.py; grep '"metric"' $O/bench_n1_b.json | cut -c1-400 ;;
     trace)
