@@ -81,11 +81,20 @@ bool clock_pair(int kind, hipEvent_t *a, hipEvent_t *b) {
     return true;
 }
 
+// launches captured into a hipGraph are never timed (their events would
+// belong to the capture, not to a run)
+bool capturing(hipStream_t s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
 template <typename K, typename... Args>
 void launch_k(int kind, K kernel, dim3 grid, dim3 block, hipStream_t s, Args... args) {
     hipEvent_t a, b;
-    if (clock_pair(kind, &a, &b)) hipExtLaunchKernelGGL(kernel, grid, block, 0, s, a, b, 0, args...);
-    else hipLaunchKernelGGL(kernel, grid, block, 0, s, args...);
+    if (g_kclock.on.load(std::memory_order_relaxed) && !capturing(s) && clock_pair(kind, &a, &b))
+        hipExtLaunchKernelGGL(kernel, grid, block, 0, s, a, b, 0, args...);
+    else
+        hipLaunchKernelGGL(kernel, grid, block, 0, s, args...);
 }
 }  // namespace
 
