@@ -104,3 +104,29 @@ def test_fused_twoshot_recommendation(bench):
     rec = bench.auto_recommendation({"us_per_call": us, "correct": ok,
                                      "twoshot_fused_vs_unfused_us": cells((40, 50, 100), (40, 50, 80))}, {})
     assert rec["env"]["SHMEMX_FUSED_TWOSHOT_KB"] == "4096"
+
+
+def test_pin_base_takes_the_last_consecutive_cpus(bench, monkeypatch):
+    """The CPU baseline pins to the LAST P consecutive CPUs of the job's set
+    (CPU 0 of a share also takes interrupts and runtime threads)."""
+    monkeypatch.setattr(bench.os, "sched_getaffinity", lambda _pid: {0, 1, 2, 3, 8, 9, 10, 11})
+    assert bench.pin_base(1) == 11
+    assert bench.pin_base(4) == 8
+    assert bench.pin_base(5) == -1          # no 5 consecutive CPUs: unpinned
+    monkeypatch.setattr(bench.os, "sched_getaffinity", lambda _pid: set(range(16)))
+    assert bench.pin_base(8) == 8
+
+
+@pytest.mark.parametrize("world", [1, 3])
+def test_cpu_baseline_fields(bench, world):
+    """cpu_baseline at N = 1 (the local fold on one core) and N > 1 (the line's
+    config on N PE processes): GiB/s of the whole job, cores = N, the CPUs,
+    min <= median <= max of the timed calls and the wall time."""
+    n = 1 << 16
+    c = bench.cpu_baseline(n, 3, world)
+    assert c["unit"] == "GiB/s" and c["kind"] == "port" and c["cores"] == world
+    assert c["value"] > 0 and c["wall_s"] >= 0
+    sp = c["spread"]
+    assert sp["calls"] == 3 and sp["min_ms"] <= sp["median_ms"] <= sp["max_ms"]
+    assert abs(c["value"] - world * n * 8 / (sp["median_ms"] * 1e-3) / (1 << 30)) < 0.01 * c["value"] + 1e-3
+    assert ("on %d PEs" % world in c["sample"]) == (world > 1)
