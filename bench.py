@@ -348,6 +348,17 @@ def config_extras(world, stream, barrier, max_over_ranks, cap=256 * 1024 * 1024)
         "marker events around the whole collective")
     if detail.get("clean"):
         out["float_sum_us_vs_nreduce"] = detail["clean"]
+    if world > 1:
+        # algbw = S / t per PE and busbw = algbw x
+        # 2(P-1)/P (the bytes each GPU moves over xGMI in RS + AG), GB/s,
+        # from the same cold timings (t = max over ranks per step)
+        algbw, busbw = {}, {}
+        for k, v in cold.items():
+            t = world * int(k) * 4 / (v * GiB)          # seconds per step
+            algbw[k] = round(int(k) * 4 / t / 1e9, 2)
+            busbw[k] = round(algbw[k] * 2 * (world - 1) / world, 2)
+        out["float_sum_algbw_GBps_vs_nreduce"] = algbw
+        out["float_sum_busbw_GBps_vs_nreduce"] = busbw
     out["float_sum_GiBps_vs_nreduce_after_write_flush"] = dirty
     out["float_sum_GiBps_vs_nreduce_after_write_flush_note"] = (
         "the same, but the scratch is REWRITTEN before every step (round 2's flush): up to 256 MiB "

@@ -99,6 +99,10 @@ def test_bench_multi_rank_line(tmp_path, transport, npes):
     assert all(v > 0 for v in x["GBps_per_gpu"].values()), x
     assert roof["measured_link_ceiling_GBps"] == x["GBps_per_gpu"]["pull_all"], roof
     assert roof["frac_of_measured_links"] > 0, roof
+    cfg = extras["configs"]            # config 5's curve: algbw and busbw per size
+    assert set(cfg["float_sum_busbw_GBps_vs_nreduce"]) == set(cfg["float_sum_GiBps_vs_nreduce"]), cfg
+    for k, a in cfg["float_sum_algbw_GBps_vs_nreduce"].items():
+        assert a > 0 and abs(cfg["float_sum_busbw_GBps_vs_nreduce"][k] - a * 2 * (npes - 1) / npes) < 0.02, (k, a)
     pa = extras["push_allreduce"]      # the store-based exchange, exact integer sums
     assert isinstance(pa, dict) and pa["correct"] is True and pa["GiBps"] > 0, pa
     bad = []
