@@ -390,7 +390,10 @@ bool handle_fault(void *addr) {
             size_t want = 1;
             if (b == g_view.fetch_end) want = std::min(kMaxFetchRun, 2 * g_view.fetch_len);
             size_t e = b;
-            while (e < g_view.nblocks && e - b < want && g_view.state[e] == DEVICE_NEWER) ++e;
+            // the run stops at a block with a write in flight: its bytes in
+            // HBM are not the collective's yet
+            while (e < g_view.nblocks && e - b < want && g_view.state[e] == DEVICE_NEWER && !g_view.pending[e])
+                ++e;
             fetch_run(b, e - b, true);
             g_view.fetch_end = e;
             g_view.fetch_len = e - b;

@@ -202,6 +202,27 @@ int main(int argc, char **argv) {
         reader.join();
         CHECK(h[w + 2] == truth[w + 2]);
     }
+    // (1b') A sequential reader's fetch run stops at a block with a write in
+    // flight: block 59 is being written while 57 and 58 are read in turn (the
+    // second fault would fetch a run of two), so 59 stays DEVICE_NEWER until
+    // its write ends, and then reads the collective's bytes.
+    {
+        const size_t b57 = 57 * M::kBlock, b59 = 59 * M::kBlock;
+        M::flush(b57, 3 * M::kBlock);
+        for (size_t i = b57; i < b57 + 3 * M::kBlock; i += 4096) {
+            g_dev[i] = (unsigned char)(i / 4096 + 11);
+            truth[i] = g_dev[i];
+        }
+        M::device_wrote(b57, 2 * M::kBlock);
+        CHECK(M::begin_device_write(b59, 16) == 1);
+        CHECK(h[b57] == truth[b57]);                        // first fault: block 57 alone
+        CHECK(h[b57 + M::kBlock] == truth[b57 + M::kBlock]);  // sequential: would take 58 and 59
+        CHECK(M::state_of(b59) == M::DEVICE_NEWER);          // 59 is not fetched while being written
+        g_dev[b59] = 0x3C;
+        truth[b59] = 0x3C;
+        M::end_device_write(b59, 16);
+        CHECK(h[b59] == 0x3C);
+    }
     // (1c) settle(): a blocking call's small result comes back into the view
     // before the call returns.  A write on CLEAN blocks ("fresh") copies only
     // its own bytes back and leaves the blocks CLEAN (no fault afterwards, a

@@ -99,7 +99,8 @@ for step in "$@"; do
         cat $O/midsize_probe.txt | grep config; cat $O/midsize_probe_trace.txt ;;
     rehearse2|rehearse8)
         np=${step#rehearse}
-        SHMEMX_TRANSPORT=ipc SHMEMX_SHARE_GPU=1 run 900 $O/rehearse_ipc_n$np.json python3 -m torch.distributed.run \
+        q=4; [ "$np" -gt 4 ] && q=2     # 8 processes' queues on one GPU (tests/test_gpu_ipc.py)
+        GPU_MAX_HW_QUEUES=$q SHMEMX_TRANSPORT=ipc SHMEMX_SHARE_GPU=1 run 900 $O/rehearse_ipc_n$np.json python3 -m torch.distributed.run \
             --nnodes=1 --nproc-per-node $np --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus $np \
             --steps 10 --warmup 3
         grep '"metric"' $O/rehearse_ipc_n$np.json | cut -c1-600 ;;
