@@ -43,6 +43,8 @@ def lib() -> ctypes.CDLL:
         vp, i = ctypes.c_void_p, ctypes.c_int
         L.oracle_reduce_sim.argtypes = [i, i, i, i, i, i, i, vp, vp]
         L.oracle_reduce_sim.restype = i
+        L.oracle_reduce_one.argtypes = [i, i, i, i, i, i, i, vp, i, vp]
+        L.oracle_reduce_one.restype = i
         L.oracle_reduce_fork.argtypes = [i, i, i, i, i, i, i, i, ctypes.c_uint64, i, i,
                                          ctypes.POINTER(ctypes.c_double),
                                          ctypes.POINTER(ctypes.c_uint64)]
@@ -164,6 +166,21 @@ def reduce_sim(type_name: str, op: str, srcs: np.ndarray, PE_start: int, logPE_s
         raise ValueError(f"oracle_reduce_sim rejected {type_name} {op} set "
                          f"({PE_start},{logPE_stride},{PE_size}) npes={npes} n={n}")
     return targets
+
+
+def reduce_one(type_name: str, op: str, srcs: np.ndarray, PE_start: int, logPE_stride: int,
+               PE_size: int, pe: int) -> np.ndarray:
+    """PE `pe`'s target after shmem_<type>_<op>_to_all (srcs: [npes, n]),
+    without simulating the other members: full-size checks."""
+    srcs = np.ascontiguousarray(srcs, dtype=NP_DTYPE[type_name])
+    npes, n = srcs.shape
+    out = np.empty(n, dtype=NP_DTYPE[type_name])
+    rc = lib().oracle_reduce_one(TYPES[type_name], OPS[op], npes, PE_start, logPE_stride, PE_size,
+                                 n, srcs.ctypes.data, pe, out.ctypes.data)
+    if rc != 0:
+        raise ValueError(f"oracle_reduce_one rejected {type_name} {op} set "
+                         f"({PE_start},{logPE_stride},{PE_size}) pe={pe}")
+    return out
 
 
 def reduce_fork(type_name: str, op: str, npes: int, PE_start: int, logPE_stride: int,

@@ -270,6 +270,30 @@ int oracle_reduce_sim(int type, int op, int npes, int PE_start,
     return 0;
 }
 
+/* One PE's target only (PE `pe`, a member of the set): the same loop as
+ * oracle_reduce_sim for that PE alone (reduce-op.c:213-248), so a test can
+ * check a full-size array without simulating every member.               */
+int oracle_reduce_one(int type, int op, int npes, int PE_start, int logPE_stride,
+                      int PE_size, int nreduce, const void *sources, int pe, void *target)
+{
+    orc_kernel_t k;
+    if (orc_kernel(type, op, &k) ||
+        orc_check_set(npes, PE_start, logPE_stride, PE_size, nreduce))
+        return -1;
+    int member = 0;
+    for (int m = 0; m < PE_size; ++m) member |= orc_member(PE_start, logPE_stride, m) == pe;
+    if (!member) return -1;
+    const size_t stride = oracle_type_size(type) * (size_t)nreduce;
+    const char *src = (const char *)sources;
+    k.copy(target, src + (size_t)pe * stride, nreduce);                /* :213-216 */
+    for (int i = 0; i < PE_size; ++i) {                                /* :219-248 */
+        const int q = orc_member(PE_start, logPE_stride, i);
+        if (q == pe) continue;
+        k.fold(k.fn, target, src + (size_t)q * stride, nreduce);
+    }
+    return 0;
+}
+
 /* ------------------------------------------- neighbouring collectives ---- */
 
 int oracle_broadcast_sim(size_t esize, int npes, int PE_root, int PE_start,

@@ -44,6 +44,10 @@ int oracle_op_valid(int type, int op);
 int oracle_reduce_sim(int type, int op, int npes, int PE_start,
                       int logPE_stride, int PE_size, int nreduce,
                       const void *sources, void *targets);
+/* PE `pe`'s target alone (a member of the set), as oracle_reduce_sim
+ * computes it. */
+int oracle_reduce_one(int type, int op, int npes, int PE_start, int logPE_stride,
+                      int PE_size, int nreduce, const void *sources, int pe, void *target);
 
 /*
  * The same algorithm run as one forked process per PE over MAP_SHARED

@@ -701,13 +701,25 @@ elif scenario == "configs8":
         if not torch.equal(got.view(iv), want.view(iv)):
             bad = int((got.view(iv) != want.view(iv)).sum())
             fails.append(f"configs8 {t} n={n} {algo}: {bad} elements differ")
-        # up to 64 Ki sampled elements against the oracle itself (each PE's
-        # own order for GATHER, PE_start's otherwise)
-        smp = torch.arange(0, n, max(1, n // 65536), device="cuda")
-        srcs = np.stack([gen(t, q, n, salt)[smp].cpu().numpy() for q in range(npes)])
-        ref = oracle.reduce_sim(t, "sum", srcs, 0, 0, npes)[pe if algo == "gather" else 0]
-        if not same_bits(got[smp].cpu().numpy(), ref):
-            fails.append(f"configs8 {t} n={n} {algo}: sampled elements differ from the oracle")
+        # against the oracle itself (each PE's own order for GATHER,
+        # PE_start's otherwise): every element up to 256 MiB per PE
+        # (configs[2] whole: 32 Mi doubles; oracle_reduce_one folds this PE's
+        # target alone, ~2 GiB of host memory per PE), 64 Ki sampled
+        # elements above that
+        if n * sz <= 256 << 20:
+            srcs = np.stack([gen(t, q, n, salt).cpu().numpy() for q in range(npes)])
+            ref = oracle.reduce_one(t, "sum", srcs, 0, 0, npes, pe if algo == "gather" else 0)
+            if not same_bits(got.cpu().numpy(), ref):
+                fails.append(f"configs8 {t} n={n} {algo}: elements differ from the oracle (full size)")
+            extra.setdefault("oracle_full_elements", 0)
+            extra["oracle_full_elements"] += n
+        else:
+            smp = torch.arange(0, n, max(1, n // 65536), device="cuda")
+            srcs = np.stack([gen(t, q, n, salt)[smp].cpu().numpy() for q in range(npes)])
+            ref = oracle.reduce_sim(t, "sum", srcs, 0, 0, npes)[pe if algo == "gather" else 0]
+            if not same_bits(got[smp].cpu().numpy(), ref):
+                fails.append(f"configs8 {t} n={n} {algo}: sampled elements differ from the oracle")
+        del srcs
         if algo != "gather" and not shm.verify(t, BIG_TGT, n, 0, 0, npes):
             fails.append(f"configs8 {t} n={n} {algo}: targets differ across PEs")
         del got, want

@@ -203,11 +203,15 @@ def test_ipc_eight_pe_baseline_configs(tmp_path):
     and own-order GATHER, and configs[4] (float sum sweep 4 Ki .. 256 Mi, 8
     PEs), as 8 PE processes sharing the GPU through the blocking drop-in entry
     points: bit-exact against torch's fold of the regenerated sources in the
-    reference's order, identical across PEs, every fence on every XCD."""
+    reference's order, identical across PEs, every fence on every XCD; and
+    against the oracle restatement itself on every element of every case up
+    to 256 MiB per PE (configs[2] whole), 64 Ki samples of the 1 GiB one."""
     reports = run_pes(tmp_path, 8, "configs8", timeout=900)
     for r in reports:
         assert r["ncases"] == 14
         assert not r["fails"], f"PE {r['pe']}: {r['fails']}"
+        assert r["oracle_full_elements"] == 3 * (32 << 20) + sum(4096 * 4 ** k for k in range(8)) + (16 << 20) + 5 \
+            + 4096 + 3, r.get("oracle_full_elements")
     fences_checked(reports)
     fences_checked(reports, device=True)
 

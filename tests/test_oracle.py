@@ -227,3 +227,23 @@ def test_fold_time_is_the_local_reduce(oracle):
     assert len(t) == 3 and all(x > 0 for x in t)
     with pytest.raises(RuntimeError):
         oracle.fold_time("double", "xor", 10, reps=1)
+
+
+def test_reduce_one_matches_reduce_sim():
+    """oracle_reduce_one (one PE's target, for full-size GPU checks) is the
+    same loop as oracle_reduce_sim: every pair, several active sets, every
+    member, value bytes equal (long double padding is unspecified)."""
+    import oracle as O
+    cases = 0
+    for t in O.TYPES:
+        for op in O.OPS:
+            if not O.op_valid(t, op):
+                continue
+            srcs = O.sources(t, 1, 5, 1001)
+            for st in ((0, 0, 5), (1, 1, 2), (2, 0, 3), (4, 0, 1)):
+                ref = O.reduce_sim(t, op, srcs, *st)
+                for m in range(st[2]):
+                    pe = st[0] + m * (1 << st[1])
+                    assert O.value_hash(t, ref[pe]) == O.value_hash(t, O.reduce_one(t, op, srcs, *st, pe))
+                    cases += 1
+    assert cases == 484
