@@ -635,13 +635,15 @@ elif scenario == "configs":
         if not torch.equal(got.view(torch.int64), want.view(torch.int64)):
             bad = int((got.view(torch.int64) != want.view(torch.int64)).sum())
             fails.append(f"config {t} {op} n={n}: {bad} elements differ")
-        # and 64 Ki sampled elements against the oracle itself (the restated
-        # reduce-op.c fold, PE_start's order), not only torch's fold
-        smp = torch.arange(0, n, n // 65536, device="cuda")
-        srcs = np.stack([gen(t, q, n, salt)[smp].cpu().numpy() for q in range(npes)])
-        ref = oracle.reduce_sim(t, op, srcs, 0, 0, npes)[0]
-        if not same_bits(got[smp].cpu().numpy(), ref):
-            fails.append(f"config {t} {op} n={n}: sampled elements differ from the oracle")
+        # and against the oracle itself on every element (the restated
+        # reduce-op.c fold in PE_start's order, this PE's target alone:
+        # oracle_reduce_one), not only torch's fold
+        srcs = np.stack([gen(t, q, n, salt).cpu().numpy() for q in range(npes)])
+        ref = oracle.reduce_one(t, op, srcs, 0, 0, npes, 0)
+        del srcs
+        if not same_bits(got.cpu().numpy(), ref):
+            fails.append(f"config {t} {op} n={n}: elements differ from the oracle (full size)")
+        extra["oracle_full_elements"] = extra.get("oracle_full_elements", 0) + n
         if not shm.verify(t, BIG_TGT, n, 0, 0, npes):
             fails.append(f"config {t} {op} n={n}: targets differ across PEs")
         del got, want

@@ -259,11 +259,13 @@ def test_ipc_baseline_configs_full_size(tmp_path):
     """BASELINE.json configs[3] (long and/or/xor, 64 Mi, 4 PEs) and configs[2]'s
     double sum over 32 Mi, as 4 PE processes through the blocking drop-in
     entry points: bit-exact against torch's fold of all regenerated sources in
-    PE_start order, and identical on every PE."""
+    PE_start order and against the oracle restatement on every element, and
+    identical on every PE."""
     reports = run_pes(tmp_path, 4, "configs", timeout=600)
     for r in reports:
         assert r["ncases"] == 4
         assert not r["fails"], f"PE {r['pe']}: {r['fails']}"
+        assert r["oracle_full_elements"] == 3 * (64 << 20) + (32 << 20), r.get("oracle_full_elements")
 
 
 @pytest.mark.gpu
