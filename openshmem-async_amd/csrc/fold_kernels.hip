@@ -623,6 +623,19 @@ hipError_t launch_fold(int type, int op, void *out, const void *const *ins,
     return dispatch(type, op, a, ptrs, nins + 1, n, stream);
 }
 
+bool copy_one_workgroup(int type, const void *dst, const void *src, size_t n) {
+    const size_t sz = type_size(type);
+    if (!sz || !n || fold_tuning().max_blocks < 0) return false;
+    const uintptr_t off = reinterpret_cast<uintptr_t>(dst) & 15u;
+    if (off % sz != 0 || (reinterpret_cast<uintptr_t>(src) & 15u) != off)
+        return n <= (size_t)kBlock;                    // all scalar: ceil(n / kBlock) blocks
+    size_t head = ((16 - off) & 15u) / sz;
+    if (head > n) head = n;
+    const size_t E = 16 / sz, nvec = (n - head) / E, tail = n - head - nvec * E;
+    if (nvec == 0) return head + tail <= (size_t)kBlock;
+    return nvec <= (size_t)kBlock * kUnrollCopy;       // grid_for: one chunk per block
+}
+
 hipError_t launch_fold_signal(int type, int op, void *out, const void *const *ins, int nins, size_t n,
                               hipStream_t stream, const HostSignal &sig) {
     if (!op_on_device(type, op) || nins < 1 || nins > kMaxFoldInputs || !out || !sig.word)

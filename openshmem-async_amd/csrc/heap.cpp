@@ -108,6 +108,7 @@ struct MirStage {
     int next = 0;
     hipStream_t fetch = nullptr;   // the fetches' own stream (non-blocking)
     std::vector<uint8_t> region;   // 0 untried, 1 page-locked, 2 refused
+    std::vector<char *> region_dev;   // device address of a page-locked region
 } g_mst;
 
 // The streams collectives on view operands ran on, each with an event
@@ -190,6 +191,23 @@ bool mir_locked(uint64_t off) {
               ok ? "page-locked" : "not page-locked (bounce buffer)");
     }
     return g_mst.region[r] == 1;
+}
+
+// Device address of alias bytes [off, off + bytes) (inside one page-locked
+// region), or nullptr: kernels may store a small result there directly.
+char *mir_alias_device(uint64_t off, size_t bytes) {
+    const size_t r = (size_t)(off / kMirRegion);
+    if (!bytes || (off + bytes - 1) / kMirRegion != r || !mir_locked(off)) return nullptr;
+    if (g_mst.region_dev.size() <= r) g_mst.region_dev.resize(r + 1, nullptr);
+    if (!g_mst.region_dev[r]) {
+        void *d = nullptr;
+        if (hipHostGetDevicePointer(&d, mirror::alias_base() + r * kMirRegion, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            return nullptr;
+        }
+        g_mst.region_dev[r] = static_cast<char *>(d);
+    }
+    return g_mst.region_dev[r] + (off - r * kMirRegion);
 }
 
 // [off, off + bytes) cut at region boundaries
@@ -466,10 +484,15 @@ void DeviceWrite::close() {
     mirror::end_device_write(off_, bytes_);
 }
 
-size_t DeviceWrite::settle(size_t limit) {
+size_t DeviceWrite::settle(size_t limit, bool copied) {
     if (!open_ || bytes_ > limit) return 0;
     close();
-    return mirror::settle(off_, bytes_, fresh_);
+    return mirror::settle(off_, bytes_, fresh_, copied && fresh_);
+}
+
+void *DeviceWrite::settle_dst(size_t limit) const {
+    if (!open_ || !fresh_ || bytes_ > limit) return nullptr;
+    return mir_alias_device(off_, bytes_);
 }
 
 bool host_acquire(const void *p, size_t bytes, bool write) {

@@ -100,7 +100,13 @@ class DeviceWrite {
     // (mirror::settle), so its blocks are CLEAN — readable by system calls
     // as well as by plain loads — when the call returns.  Larger targets
     // keep the lazy fetch.  Returns the bytes copied back.
-    size_t settle(size_t limit);
+    size_t settle(size_t limit, bool copied = false);
+    // Where the call's own stream may store the result for settle(limit,
+    // true): the device address of the view's page-locked alias at the
+    // target's offset, when the target is at most `limit` bytes, its blocks
+    // were current before the call (only the result's bytes differ), and the
+    // alias region is page-locked; else nullptr.
+    void *settle_dst(size_t limit) const;
 
   private:
     void *dev_;

@@ -49,6 +49,11 @@ void wait_host_signal(const HostSignal &sig, hipStream_t s);
 // one-thread marker kernel right after it.
 hipError_t launch_fold_signal(int type, int op, void *out, const void *const *ins, int nins, size_t n,
                               hipStream_t stream, const HostSignal &sig);
+// Does a copy (launch_fold with nins == 1) of n elements of `type` from
+// src to dst run as ONE workgroup (so launch_fold_signal's workgroup stores
+// the signal itself, after its own stores drained and a system-scope
+// release)?
+bool copy_one_workgroup(int type, const void *dst, const void *src, size_t n);
 // The one-thread marker kernel alone: stores sig once everything enqueued
 // before it on the stream has completed.
 hipError_t launch_host_signal(const HostSignal &sig, hipStream_t stream);

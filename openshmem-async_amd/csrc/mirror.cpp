@@ -305,7 +305,7 @@ void end_device_write(uint64_t off, size_t bytes) {
         if (g_view.pending[b]) --g_view.pending[b];
 }
 
-size_t settle(uint64_t off, size_t bytes, bool fresh) {
+size_t settle(uint64_t off, size_t bytes, bool fresh, bool copied) {
     if (!g_view.base || !bytes) return 0;
     Guard g;
     const size_t b0 = block_of(off), b1 = std::min(block_of(off + bytes - 1) + 1, g_view.nblocks);
@@ -316,12 +316,14 @@ size_t settle(uint64_t off, size_t bytes, bool fresh) {
         return (b1 - b0) * kBlock;
     }
     // the rest of every block already equals HBM: only the written bytes
-    // move, and their writer has completed (the caller's contract)
-    (g_view.be.to_host_done ? g_view.be.to_host_done : g_view.be.to_host)(off, bytes, g_view.be.ctx);
+    // move, and their writer has completed (the caller's contract); with
+    // `copied` the call's stream has put them into the alias already
+    if (!copied)
+        (g_view.be.to_host_done ? g_view.be.to_host_done : g_view.be.to_host)(off, bytes, g_view.be.ctx);
     protect(b0, b1 - b0, PROT_READ);
     std::memset(g_view.state + b0, CLEAN, b1 - b0);
     g_view.st.blocks_settled += b1 - b0;
-    return bytes;
+    return copied ? 0 : bytes;
 }
 
 size_t device_wrote(uint64_t off, size_t bytes) {

@@ -119,8 +119,10 @@ void end_device_write(uint64_t off, size_t bytes);
 // calls alike) instead of leaving them to a fault.  With `fresh` (from
 // begin_device_write) only [off, off + bytes) is copied back; otherwise the
 // blocks whole.  Nothing happens if another write is in flight on them.
-// Returns the bytes copied.
-size_t settle(uint64_t off, size_t bytes, bool fresh);
+// `copied` (with `fresh`): the call's own stream already wrote the result
+// into the alias (a copy kernel before its host signal), so only the block
+// states and protections change.  Returns the bytes copied here.
+size_t settle(uint64_t off, size_t bytes, bool fresh, bool copied = false);
 // After a collective wrote [off, off + bytes) in HBM without
 // begin_device_write (a collect target, whose length is known only after
 // the exchange): the overlapped blocks become DEVICE_NEWER (call flush on the

@@ -205,11 +205,22 @@ void reduce_blocking(int type, int op, void *target, const void *source,
             // (host accesses wait for it); the blocking call completes on the
             // library stream, its recorded writer
             heap::DeviceWrite t(target, bytes, g_state.stream);
+            // a small result also goes straight into the view's page-locked
+            // alias: the call's last kernel stores it there before the host
+            // signal (one workgroup, so its own drained stores and
+            // system-scope release precede the signal)
+            void *dst = t.settle_dst(mirror_settle_limit());
+            if (dst && !copy_one_workgroup(type, dst, t.ptr(), (size_t)nreduce)) dst = nullptr;
+            g_state.settle_dst = dst;
+            g_state.settled = false;
             reduce_blocking_impl(type, op, t.ptr(), s, nreduce, start, logstride, size, false);
-            // the call's work is complete: a small result comes back into the
-            // view now, so the caller's system calls can read it (VERDICT r03
-            // #6; larger targets are fetched on first access)
-            t.settle(mirror_settle_limit());
+            const bool copied = g_state.settled;
+            g_state.settle_dst = nullptr;
+            g_state.settled = false;
+            // the call's work is complete: a small result is back in the view
+            // (copied above, or now), so the caller's system calls can read
+            // it (larger targets are fetched on first access)
+            t.settle(mirror_settle_limit(), copied);
             return;
         }
     }
@@ -272,8 +283,17 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
             // a marker kernel otherwise): no stream wait
             const HostSignal sig = next_host_signal();
             const void *in[1] = {source};
-            SHMX_HIP(launch_fold_signal(type, op, target, in, 1, (size_t)nreduce, s, sig));
+            if (g_state.settle_dst) {
+                // a small mirrored target: the copy, then the result into the
+                // view's alias by the workgroup that signals
+                const void *res[1] = {target};
+                SHMX_HIP(launch_fold(type, op, target, in, 1, (size_t)nreduce, s));
+                SHMX_HIP(launch_fold_signal(type, op, g_state.settle_dst, res, 1, (size_t)nreduce, s, sig));
+            } else {
+                SHMX_HIP(launch_fold_signal(type, op, target, in, 1, (size_t)nreduce, s, sig));
+            }
             wait_host_signal(sig, s);
+            if (g_state.settle_dst) g_state.settled = true;
             return;
         }
         const int rc = reduce_device(type, op, target, source, nreduce, start, logstride, size,
@@ -286,10 +306,18 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
         // with a marker the host spins on.
         const bool waits_itself = collective && (plan.algo == SHMEMX_ALGO_DIRECT ||
                                                  (plan.algo == SHMEMX_ALGO_GATHER && g_state.ipc_only));
-        if (rc == SHMEMX_OK && !waits_itself) {
+        if (rc == SHMEMX_OK && (!waits_itself || g_state.settle_dst)) {
             const HostSignal sig = next_host_signal();
-            SHMX_HIP(launch_host_signal(sig, s));
+            if (g_state.settle_dst) {
+                // a small mirrored target: the result into the view's alias,
+                // by the one workgroup that then signals
+                const void *res[1] = {target};
+                SHMX_HIP(launch_fold_signal(type, op, g_state.settle_dst, res, 1, (size_t)nreduce, s, sig));
+            } else {
+                SHMX_HIP(launch_host_signal(sig, s));
+            }
             wait_host_signal(sig, s);
+            if (g_state.settle_dst) g_state.settled = true;
         } else if (rc != SHMEMX_OK) {
             SHMX_HIP(hipStreamSynchronize(s));
         }

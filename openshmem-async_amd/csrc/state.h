@@ -39,6 +39,12 @@ struct State {
     // inside a blocking entry point: wait_host_signal returns as soon as the
     // work's host signal arrives, without seeing the stream idle
     bool return_on_signal = false;
+    // inside a blocking call on a small host-view target (staging.cpp): the
+    // device address where the call's last kernel also stores the result (the
+    // view's page-locked alias, heap.h DeviceWrite::settle_dst), and whether
+    // it did, before the host signal
+    void *settle_dst = nullptr;
+    bool settled = false;
     // grow-only device workspaces
     void *ws = nullptr;        // A2A shard receive area / GATHER sources
     size_t ws_bytes = 0;

@@ -275,6 +275,21 @@ int main(int argc, char **argv) {
         CHECK(M::settle(d, 8, fresh) == 0 && M::state_of(d) == M::DEVICE_NEWER);
         M::end_device_write(d + 64, 8);
         CHECK(h[d + 65] == truth[d + 65] && M::state_of(d) == M::CLEAN);   // the fault path
+        // the call's own stream already stored the result into the alias
+        // (settle with `copied`): nothing more moves, the block is CLEAN
+        const size_t e = 53 * M::kBlock + 40;
+        M::flush(53 * M::kBlock, M::kBlock);
+        CHECK(M::begin_device_write(e, 8, &fresh) == 1 && fresh);
+        for (size_t i = 0; i < 8; ++i) {
+            g_dev[e + i] = (unsigned char)(0xE0 + i);
+            M::alias_base()[e + i] = (char)(0xE0 + i);     // the in-stream copy
+            truth[e + i] = g_dev[e + i];
+        }
+        M::end_device_write(e, 8);
+        const size_t d2h1 = g_d2h;
+        const auto rf1 = M::stats(false).read_faults;
+        CHECK(M::settle(e, 8, fresh, true) == 0 && g_d2h == d2h1 && M::state_of(e) == M::CLEAN);
+        CHECK(h[e + 3] == truth[e + 3] && M::stats(false).read_faults == rf1);
     }
     // (2) A store another thread makes while a flush copies its block (after
     // the protection change, before the copy) is not lost: it faults, waits,
