@@ -315,6 +315,14 @@ int shmemx_fold_set_tuning(int max_blocks, int nontemporal, int unroll);
  * launches past the 4096 that went untimed to *dropped (may be NULL); it
  * returns how many were written and starts over.  Off by default; timing
  * does not change what runs. */
+/* Register (on != 0) or deregister the symmetric heap's HBM segment with
+ * the library's RCCL communicator (ncclCommRegister), so RCCL may use
+ * collectives' heap operands in place instead of staging them through its
+ * own buffers.  Off by default: the N > 1 bench times the RCCL algorithms
+ * both ways (extras.rccl_registered) before it is adopted.  Every PE should
+ * call it alike.  ENOTSUP without an RCCL communicator or an HBM segment. */
+int shmemx_rccl_register_heap(int on);
+
 int shmemx_kernel_timing(int on);
 int shmemx_kernel_times(double *us, int *kind, int max, unsigned long long *dropped);
 

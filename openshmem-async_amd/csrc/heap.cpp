@@ -512,6 +512,13 @@ bool view_offset(const void *p, uint64_t *off) {
     return true;
 }
 
+bool segment(void **base, size_t *bytes) {
+    if (!g_heap.base || host_kind()) return false;
+    *base = g_heap.base;
+    *bytes = g_heap.arena.capacity();
+    return true;
+}
+
 void release_all() {
     if (g_heap.view) {
         for (size_t r = 0; r < g_mst.region.size(); ++r)

@@ -128,6 +128,9 @@ void flush_view();
 // Offset of a host-view address in the segment; false if not in the view.
 bool view_offset(const void *p, uint64_t *off);
 void release_all();                             // shmem_finalize
+// The HBM segment (base and bytes, the signal area excluded), or false if
+// there is none yet (no shmem_malloc) or it is host memory.
+bool segment(void **base, size_t *bytes);
 
 }  // namespace heap
 }  // namespace shmx

@@ -855,6 +855,8 @@ void pshmem_finalize(void) {
     (void)hipStreamSynchronize(g_state.stream);
     // collective: no PE frees memory its peers may still be reading
     if (node::up()) node::barrier(0, 1, g_state.npes);
+    if (g_state.comm && g_state.rccl_reg) (void)ncclCommDeregister(g_state.comm, g_state.rccl_reg);
+    g_state.rccl_reg = nullptr;
     heap::release_all();
     direct_release();
     node::detach(g_state.pe == 0);
@@ -1104,6 +1106,29 @@ int shmemx_fold_set_tuning(int max_blocks, int nontemporal, int unroll) {
     t.max_blocks = max_blocks;
     t.nontemporal = nontemporal < 0 ? -1 : (nontemporal & 3);
     t.unroll = unroll;
+    return SHMEMX_OK;
+}
+
+int shmemx_rccl_register_heap(int on) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    if (int rc = ensure_init()) return rc;
+    if (!g_state.comm) return set_error(SHMEMX_ENOTSUP);
+    if (on && !g_state.rccl_reg) {
+        void *base = nullptr;
+        size_t bytes = 0;
+        if (!heap::segment(&base, &bytes)) return set_error(SHMEMX_ENOTSUP);
+        SHMX_HIP(hipStreamSynchronize(g_state.stream));
+        if (ncclCommRegister(g_state.comm, base, bytes, &g_state.rccl_reg) != ncclSuccess) {
+            g_state.rccl_reg = nullptr;
+            trace(LOG_INFO, "ncclCommRegister of the heap segment (%zu bytes) failed", bytes);
+            return set_error(SHMEMX_ENOTSUP);
+        }
+        trace(LOG_INFO, "heap segment %p (%zu bytes) registered with the RCCL communicator", base, bytes);
+    } else if (!on && g_state.rccl_reg) {
+        SHMX_HIP(hipStreamSynchronize(g_state.stream));
+        (void)ncclCommDeregister(g_state.comm, g_state.rccl_reg);
+        g_state.rccl_reg = nullptr;
+    }
     return SHMEMX_OK;
 }
 

@@ -32,6 +32,9 @@ struct State {
     // IPC transport a PE without it is fatal).  AUTO's plan reads this, never
     // per-process state, so every PE plans alike.
     bool node_shared = false;
+    // the heap segment registered with the RCCL communicator
+    // (shmemx_rccl_register_heap), or nullptr
+    void *rccl_reg = nullptr;
     // test hook ($SHMEMX_FORCE_COLLECTIVE=1): a 1-PE job still builds an RCCL
     // communicator and runs the collective schedules, so a one-GPU box can
     // execute every RCCL call of the path

@@ -97,6 +97,8 @@ def lib() -> ctypes.CDLL:
     L.shmemx_set_algo.restype = i
     L.shmemx_fold_set_tuning.argtypes = [i, i, i]
     L.shmemx_fold_set_tuning.restype = i
+    L.shmemx_rccl_register_heap.argtypes = [i]
+    L.shmemx_rccl_register_heap.restype = i
     L.shmemx_kernel_timing.argtypes = [i]
     L.shmemx_kernel_timing.restype = i
     L.shmemx_kernel_times.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int), i,
@@ -322,6 +324,11 @@ def plan(type_name: str, op: str, nreduce: int, PE_start: int, logPE_stride: int
 def set_fold_tuning(max_blocks: int = 0, nontemporal: int = -1, unroll: int = 4) -> None:
     """Launch shape of the fold kernels (grid cap, nt loads/stores, unroll)."""
     _check(lib().shmemx_fold_set_tuning(max_blocks, nontemporal, unroll), "shmemx_fold_set_tuning")
+
+
+def rccl_register_heap(on: bool) -> None:
+    """shmemx_rccl_register_heap: the heap segment (de)registered with RCCL."""
+    _check(lib().shmemx_rccl_register_heap(1 if on else 0), "shmemx_rccl_register_heap")
 
 
 KERNEL_KINDS = ("fold", "copy", "peers_fold", "gather")

@@ -329,6 +329,16 @@ ncclResult_t ncclCommDestroy(ncclComm_t c) {
     return ncclSuccess;
 }
 
+// buffer registration: the double moves data through its own mailboxes
+// whatever is registered; it records nothing
+ncclResult_t ncclCommRegister(const ncclComm_t, void *, size_t, void **handle) {
+    static int token;
+    *handle = &token;
+    return ncclSuccess;
+}
+
+ncclResult_t ncclCommDeregister(const ncclComm_t, void *) { return ncclSuccess; }
+
 ncclResult_t ncclGroupStart() {
     ++g_depth;
     return ncclSuccess;

@@ -99,6 +99,12 @@ def test_bench_multi_rank_line(tmp_path, transport, npes):
     assert all(v > 0 for v in x["GBps_per_gpu"].values()), x
     assert roof["measured_link_ceiling_GBps"] == x["GBps_per_gpu"]["pull_all"], roof
     assert roof["frac_of_measured_links"] > 0, roof
+    if transport == "rccl":           # the RCCL algorithms with the heap registered with RCCL
+        rr = extras["rccl_registered"]
+        assert isinstance(rr, dict) and rr["algo_rccl_correct"] is True and rr["algo_allreduce_correct"] is True, rr
+        assert rr["algo_rccl_GiBps"] > 0 and rr["algo_allreduce_GiBps"] > 0, rr
+    else:
+        assert "rccl_registered" not in extras
     cfg = extras["configs"]            # config 5's curve: algbw and busbw per size
     assert set(cfg["float_sum_busbw_GBps_vs_nreduce"]) == set(cfg["float_sum_GiBps_vs_nreduce"]), cfg
     for k, a in cfg["float_sum_algbw_GBps_vs_nreduce"].items():
