@@ -1352,6 +1352,11 @@ def main():
                 finally:
                     shm.rccl_register_heap(False)
                 res["headline_unregistered_GiBps"] = round(value, 2)
+                # adopt it (an environment change) only where it is correct and
+                # at least 3 % faster than the unregistered headline
+                best = max(res["algo_rccl_GiBps"] if res["algo_rccl_correct"] else 0.0,
+                           res["algo_allreduce_GiBps"] if res["algo_allreduce_correct"] else 0.0)
+                res["recommend_env"] = {"SHMEMX_RCCL_REGISTER": "1"} if best > 1.03 * value else {}
                 return res
             guarded("rccl_registered", rccl_registered)
         guarded("configs", lambda: config_extras(world, stream, barrier, max_over_ranks,

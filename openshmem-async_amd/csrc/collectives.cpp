@@ -389,6 +389,18 @@ void *heap_alloc(size_t alignment, size_t bytes) {
     void *p = heap::alloc(alignment, bytes);
     if (!p) set_error(SHMEMX_ENOMEM);
     trace(LOG_MEMORY, "shmem_malloc(%zu bytes, align %zu) = %p (HBM)", bytes, alignment, p);
+    // $SHMEMX_RCCL_REGISTER=1: the segment is registered with RCCL as soon as
+    // it exists (shmemx_rccl_register_heap; adopted from the N > 1 bench's
+    // extras.rccl_registered); every PE allocates alike, so every PE registers
+    static const bool reg = [] {
+        const char *e = std::getenv("SHMEMX_RCCL_REGISTER");
+        return e && *e == '1';
+    }();
+    if (p && reg && g_state.comm && !g_state.rccl_reg) {
+        const int err = shmemx_reduce_last_error();
+        (void)shmemx_rccl_register_heap(1);
+        set_error(err);   // a refused registration is not the allocation's error
+    }
     return p;
 }
 
