@@ -229,7 +229,10 @@ def test_rccl_transport_with_rccl_double(tmp_path, npes):
     order)."""
     fake = os.path.join(HERE, "native", "libfake_rccl.so")
     assert os.path.exists(fake), "tests/native/libfake_rccl.so not built (make -C tests/native)"
-    reports = run_pes(tmp_path, npes, "rccl", {"SHMEMX_TRANSPORT": "rccl", "FAKE_RCCL": fake},
+    # at 3 PEs with the heap segment registered with RCCL at its first
+    # allocation (SHMEMX_RCCL_REGISTER=1): the same results
+    reports = run_pes(tmp_path, npes, "rccl", {"SHMEMX_TRANSPORT": "rccl", "FAKE_RCCL": fake,
+                                               "SHMEMX_RCCL_REGISTER": "1" if npes == 3 else "0"},
                       timeout=600)
     for r in reports:
         assert r["ncases"] > 0
