@@ -17,6 +17,8 @@
 #   isx_mirror     tools/isx_mirror_latency.py with and without the small-result settle
 # $TAG names the round's files (default r04).
 #   ceiling        tools/stream_lab: copy / read / fill ceilings beside the fold
+#   write          tools/stream_lab: write-only shapes (what bounds the fold's stores)
+#   fold2          tools/stream_lab: fold shapes the write-only lab suggests
 #   midsize        the mid-size fold: tools/stream_lab fold shapes and the library's
 #                  fold after a read-only flush (cold_midsize_probe.py), under
 #                  rocprofv3 kernel traces, per size
@@ -86,6 +88,11 @@ for step in "$@"; do
         for nd in 33554432 67108864; do
             run 300 $O/stream_lab_ceiling_$nd.txt ./tools/stream_lab $nd 3 10 ceiling
             cut -c1-260 $O/stream_lab_ceiling_$nd.txt
+        done ;;
+    write|fold2)
+        for nd in 33554432 67108864; do
+            run 300 $O/stream_lab_${step}_$nd.txt ./tools/stream_lab $nd 3 10 $step
+            cut -c1-260 $O/stream_lab_${step}_$nd.txt
         done ;;
     midsize)
         for nd in 524288 2097152 8388608; do

@@ -16,7 +16,7 @@
 // and for cold also the in-stream cost including deferred write-backs (see
 // main).  Prints medians in us and TB/s of algorithmic bytes.
 //
-// usage: stream_lab [doubles per array] [rounds] [reps] [ceiling|fold]
+// usage: stream_lab [doubles per array] [rounds] [reps] [ceiling|fold|write|fold2]
 // Build: hipcc --offload-arch=gfx950 -O3 tools/stream_lab.hip -o tools/stream_lab
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
@@ -130,6 +130,35 @@ __global__ __launch_bounds__(B) void k_fold(u32x4 *acc, const u32x4 *in, size_t 
     }
 }
 
+// the fold with a wave-contiguous layout: each 64-lane wave owns U x 1 KiB
+// adjacent (its U instructions cover one contiguous U KiB), instead of the
+// block-strided layout where a wave's U instructions sit B x 16 B apart
+template <int B, int U, int NT>
+__global__ __launch_bounds__(B) void k_fold_wc(u32x4 *acc, const u32x4 *in, size_t nvec) {
+    typedef double f64x2 __attribute__((ext_vector_type(2)));
+    const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const size_t base = (size_t)blockIdx.x * B * U + (size_t)wave * 64 * U + lane;
+    u32x4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) a[u] = ld<NT>(acc + base + u * 64);
+#pragma unroll
+    for (int u = 0; u < U; ++u) b[u] = ld<NT>(in + base + u * 64);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        f64x2 s = __builtin_bit_cast(f64x2, a[u]) + __builtin_bit_cast(f64x2, b[u]);
+        st<NT>(acc + base + u * 64, __builtin_bit_cast(u32x4, s));
+    }
+}
+
+template <int B, int U, int NT>
+__global__ __launch_bounds__(B) void k_fill_wc(u32x4 *out, size_t nvec, unsigned c) {
+    const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const size_t base = (size_t)blockIdx.x * B * U + (size_t)wave * 64 * U + lane;
+    u32x4 v = {c, c, c, c};
+#pragma unroll
+    for (int u = 0; u < U; ++u) st<NT>(out + base + u * 64, v);
+}
+
 // persistent grid-stride fold, fixed grid G
 template <int B, int U, int NT>
 __global__ __launch_bounds__(B) void k_fold_pers(u32x4 *acc, const u32x4 *in, size_t nvec) {
@@ -211,7 +240,42 @@ int main(int argc, char **argv) {
 #define FOLDP(B, U, NT, G)                                                                    \
     vs.push_back({"fold_pers B" #B " U" #U " nt" #NT " G" #G, 3.0 * bytes, [=](hipStream_t st, hipEvent_t k0, hipEvent_t k1) { \
         hipExtLaunchKernelGGL((k_fold_pers<B, U, NT>), dim3(G), dim3(B), 0, st, k0, k1, 0, a, b, nvec); }})
-    if (set == "fold") {   // the mid-size fold's shapes
+#define FOLDWC(B, U, NT)                                                                      \
+    vs.push_back({"fold_wc B" #B " U" #U " nt" #NT, 3.0 * bytes, [=](hipStream_t st, hipEvent_t k0, hipEvent_t k1) { \
+        hipExtLaunchKernelGGL((k_fold_wc<B, U, NT>), GRID(B, U), dim3(B), 0, st, k0, k1, 0, a, b, nvec); }})
+#define FILLWC(B, U, NT)                                                                      \
+    vs.push_back({"fill_wc B" #B " U" #U " nt" #NT, 1.0 * bytes, [=](hipStream_t st, hipEvent_t k0, hipEvent_t k1) { \
+        hipExtLaunchKernelGGL((k_fill_wc<B, U, NT>), GRID(B, U), dim3(B), 0, st, k0, k1, 0, c, nvec, 7u); }})
+    if (set == "fold2") {   // fold shapes suggested by the write-only lab (round 4)
+        FOLD(256, 4, 3);
+        FOLD(64, 4, 3);
+        FOLD(64, 8, 3);
+        FOLD(64, 16, 3);
+        FOLD(128, 4, 3);
+        FOLD(256, 1, 3);
+        FOLD(256, 2, 3);
+        FOLDWC(256, 4, 3);
+        FOLDWC(256, 8, 3);
+        FOLDWC(512, 4, 3);
+        FILLWC(256, 4, 2);
+        FILL(64, 4, 2);
+        FILL(256, 1, 2);
+        READ(256, 4, 1, 2);
+        READ(64, 4, 1, 2);
+    } else if (set == "write") {   // the write direction alone: what bounds the fold's stores (round 4)
+        FILL(256, 1, 2);
+        FILL(256, 2, 2);
+        FILL(256, 4, 2);
+        FILL(256, 8, 2);
+        FILL(256, 16, 2);
+        FILL(512, 4, 2);
+        FILL(1024, 4, 2);
+        FILL(64, 4, 2);
+        FILL(256, 4, 0);
+        COPY(256, 8, 3);
+        FOLD(256, 4, 3);
+        READ(256, 4, 1, 1);
+    } else if (set == "fold") {   // the mid-size fold's shapes
         FOLD(256, 4, 3);
         FOLD(256, 4, 0);
         FOLD(256, 2, 3);
