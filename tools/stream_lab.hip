@@ -16,7 +16,7 @@
 // and for cold also the in-stream cost including deferred write-backs (see
 // main).  Prints medians in us and TB/s of algorithmic bytes.
 //
-// usage: stream_lab [doubles per array] [rounds] [reps] [ceiling|fold|write|fold2]
+// usage: stream_lab [doubles per array] [rounds] [reps] [ceiling|fold|write|fold2|copy2]
 // Build: hipcc --offload-arch=gfx950 -O3 tools/stream_lab.hip -o tools/stream_lab
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
@@ -159,6 +159,17 @@ __global__ __launch_bounds__(B) void k_fill_wc(u32x4 *out, size_t nvec, unsigned
     for (int u = 0; u < U; ++u) st<NT>(out + base + u * 64, v);
 }
 
+template <int B, int U, int NT>
+__global__ __launch_bounds__(B) void k_copy_wc(u32x4 *out, const u32x4 *in, size_t nvec) {
+    const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const size_t base = (size_t)blockIdx.x * B * U + (size_t)wave * 64 * U + lane;
+    u32x4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = ld<NT>(in + base + u * 64);
+#pragma unroll
+    for (int u = 0; u < U; ++u) st<NT>(out + base + u * 64, x[u]);
+}
+
 // persistent grid-stride fold, fixed grid G
 template <int B, int U, int NT>
 __global__ __launch_bounds__(B) void k_fold_pers(u32x4 *acc, const u32x4 *in, size_t nvec) {
@@ -246,7 +257,24 @@ int main(int argc, char **argv) {
 #define FILLWC(B, U, NT)                                                                      \
     vs.push_back({"fill_wc B" #B " U" #U " nt" #NT, 1.0 * bytes, [=](hipStream_t st, hipEvent_t k0, hipEvent_t k1) { \
         hipExtLaunchKernelGGL((k_fill_wc<B, U, NT>), GRID(B, U), dim3(B), 0, st, k0, k1, 0, c, nvec, 7u); }})
-    if (set == "fold2") {   // fold shapes suggested by the write-only lab (round 4)
+#define COPYWC(B, U, NT)                                                                      \
+    vs.push_back({"copy_wc B" #B " U" #U " nt" #NT, 2.0 * bytes, [=](hipStream_t st, hipEvent_t k0, hipEvent_t k1) { \
+        hipExtLaunchKernelGGL((k_copy_wc<B, U, NT>), GRID(B, U), dim3(B), 0, st, k0, k1, 0, c, b, nvec); }})
+    if (set == "copy2") {   // copy shapes suggested by the write-only lab (round 4)
+        COPY(256, 8, 3);
+        COPY(256, 4, 3);
+        COPY(256, 1, 3);
+        COPY(256, 2, 3);
+        COPY(64, 4, 3);
+        COPY(64, 8, 3);
+        COPY(64, 16, 3);
+        COPY(128, 8, 3);
+        COPYWC(256, 4, 3);
+        COPYWC(256, 8, 3);
+        COPYWC(256, 16, 3);
+        FILL(256, 1, 2);
+        READ(256, 4, 1, 1);
+    } else if (set == "fold2") {   // fold shapes suggested by the write-only lab (round 4)
         FOLD(256, 4, 3);
         FOLD(64, 4, 3);
         FOLD(64, 8, 3);
