@@ -444,29 +444,39 @@ hipError_t launch_nt(const FoldArgs &a, hipStream_t stream) {
 
 // The copy (nins == 1: reduce-op.c:213-216, the whole PE_size = 1 call, and
 // the private copy of an overlapping source): a compile-time one-input
-// instance of the fold, one chunk of kBlock x kUnrollCopy 16-B vectors per
-// workgroup, non-temporal loads and stores from 32 MiB moved.  A copy moves
-// bits, so it runs on one type per element size (short, int, long, and a
-// 16-byte struct for complex double and long double) with no arithmetic.
-// Measured (tools/stream_lab.hip, profiles/r04_stream_lab_*.txt, 256 and
-// 512 MiB, after a flush, the in-stream cost that also charges deferred
-// write-backs): 8 vectors per lane 6.17-6.42 TB/s, 4 vectors 6.09-6.13, 2
-// or 16 worse, 512/1024-lane blocks and persistent grids worse; default-
-// policy stores look faster by kernel time alone (6.9-7.1) but leave up to
-// 256 MiB dirty in the Infinity Cache for the next kernel to write back
+// instance of the fold, non-temporal loads and stores from 32 MiB moved.  A
+// copy moves bits, so it runs on one type per element size (short, int,
+// long, and a 16-byte struct for complex double and long double) with no
+// arithmetic.  Shape: ONE 16-B vector per lane, 4 KiB per workgroup, for
+// large copies; up to 32 KiB, 8 vectors per lane, so the copy is one
+// workgroup that can store the host signal itself (launch_fold_signal).
+// Measured (tools/stream_lab.hip, profiles/r04_stream_lab_copy2_*.txt, in-stream
+// cost after a flush, which also charges deferred write-backs; 256 / 512
+// MiB): 1 vector per lane 6.44 / 6.55 TB/s, 8 vectors 6.38 / 6.18, 4 vectors
+// 6.09 / 6.04, 64- or 128-lane blocks and wave-contiguous layouts 6.1-6.35;
+// stores of 4 KiB per workgroup are the fast write shape
+// (profiles/r04_stream_lab_write_*.txt: 6.7-6.9 against 6.0 at 16 KiB).
+// Default-policy stores look faster by kernel time alone (6.9-7.1) but leave
+// up to 256 MiB dirty in the Infinity Cache for the next kernel to write back
 // (4.9-5.2 TB/s charged), so the stores stay non-temporal.
-constexpr int kUnrollCopy = 8;
+constexpr int kUnrollCopy = 8;       // small copies: one workgroup up to 32 KiB
+constexpr int kUnrollCopyLarge = 1;  // large copies: 4 KiB per workgroup
 
 template <typename T, int NT>
 hipError_t launch_copy_nt(const FoldArgs &a0, hipStream_t stream) {
-    const size_t blocks = grid_for(a0, kUnrollCopy);
+    const bool small = a0.nvec <= (size_t)kBlock * kUnrollCopy;
+    const size_t blocks = grid_for(a0, small ? kUnrollCopy : kUnrollCopyLarge);
     // a one-workgroup copy stores the host signal itself (launch_fold_signal);
     // a larger grid is followed by the marker kernel
     const bool self_signal = a0.sig_word && blocks == 1;
     FoldArgs a = a0;
     if (!self_signal) a.sig_word = nullptr;
-    launch_k(kKindCopy, fold_kernel<T, SHMEMX_OP_SUM, 1, kUnrollCopy, NT>, dim3((unsigned)blocks), dim3(kBlock),
-             stream, a);
+    if (small)
+        launch_k(kKindCopy, fold_kernel<T, SHMEMX_OP_SUM, 1, kUnrollCopy, NT>, dim3((unsigned)blocks), dim3(kBlock),
+                 stream, a);
+    else
+        launch_k(kKindCopy, fold_kernel<T, SHMEMX_OP_SUM, 1, kUnrollCopyLarge, NT>, dim3((unsigned)blocks),
+                 dim3(kBlock), stream, a);
     if (a0.sig_word && !self_signal)
         hipLaunchKernelGGL(host_signal_kernel, dim3(1), dim3(64), 0, stream, a0.sig_word, a0.sig_value);
     return hipGetLastError();
