@@ -1306,7 +1306,7 @@ def main():
                                "calls, the host's wall clock, the copy kernel's own dispatch events"}
                 if kus:
                     ku = statistics.median(kus)
-                    out["clock_kernel"] = {"kernel": "fold_kernel<T,SUM,1 input,8 vectors,nt> (the copy)",
+                    out["clock_kernel"] = {"kernel": "fold_kernel<T,SUM,1 input,1 vector,nt> (the copy)",
                                            "us": round(ku, 2), "hbm_GBps": round(2 * nbytes / ku / 1e3, 1)}
                 return out
             guarded("api_pe_size_1", api_pe_size_1)

@@ -456,6 +456,8 @@ hipError_t launch_nt(const FoldArgs &a, hipStream_t stream) {
 // 6.09 / 6.04, 64- or 128-lane blocks and wave-contiguous layouts 6.1-6.35;
 // stores of 4 KiB per workgroup are the fast write shape
 // (profiles/r04_stream_lab_write_*.txt: 6.7-6.9 against 6.0 at 16 KiB).
+// Through the library (tools/copy_probe.py, profiles/r04_copy_probe.txt):
+// 83.7 us at 256 MiB, 166.6 us at 512 MiB (6.41-6.44 TB/s).
 // Default-policy stores look faster by kernel time alone (6.9-7.1) but leave
 // up to 256 MiB dirty in the Infinity Cache for the next kernel to write back
 // (4.9-5.2 TB/s charged), so the stores stay non-temporal.

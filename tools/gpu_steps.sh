@@ -19,6 +19,7 @@
 #   ceiling        tools/stream_lab: copy / read / fill ceilings beside the fold
 #   write          tools/stream_lab: write-only shapes (what bounds the fold's stores)
 #   fold2, copy2   tools/stream_lab: fold / copy shapes the write-only lab suggests
+#   copy           tools/copy_probe.py under a rocprofv3 kernel trace: the library's copy kernel
 #   midsize        the mid-size fold: tools/stream_lab fold shapes and the library's
 #                  fold after a read-only flush (cold_midsize_probe.py), under
 #                  rocprofv3 kernel traces, per size
@@ -94,6 +95,10 @@ for step in "$@"; do
             run 300 $O/stream_lab_${step}_$nd.txt ./tools/stream_lab $nd 3 10 $step
             cut -c1-260 $O/stream_lab_${step}_$nd.txt
         done ;;
+    copy)
+        run 300 $O/copy_probe.txt rocprofv3 --kernel-trace --stats -d $O/copy_probe -o t --output-format csv \
+            -- python3 tools/copy_probe.py
+        grep copy $O/copy_probe.txt; python3 tools/trace_by_grid.py $O/copy_probe fold_kernel ;;
     midsize)
         for nd in 524288 2097152 8388608; do
             run 300 $O/midsize_lab_$nd.txt rocprofv3 --kernel-trace --stats -d $O/midsize_lab_$nd -o t \
