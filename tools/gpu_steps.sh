@@ -18,7 +18,7 @@
 # $TAG names the round's files (default r04).
 #   ceiling        tools/stream_lab: copy / read / fill ceilings beside the fold
 #   write          tools/stream_lab: write-only shapes (what bounds the fold's stores)
-#   fold2, copy2   tools/stream_lab: fold / copy shapes the write-only lab suggests
+#   fold2, copy2, gs  tools/stream_lab: fold / copy shapes the write-only lab suggests
 #   copy           tools/copy_probe.py under a rocprofv3 kernel trace: the library's copy kernel
 #   midsize        the mid-size fold: tools/stream_lab fold shapes and the library's
 #                  fold after a read-only flush (cold_midsize_probe.py), under
@@ -90,7 +90,7 @@ for step in "$@"; do
             run 300 $O/stream_lab_ceiling_$nd.txt ./tools/stream_lab $nd 3 10 ceiling
             cut -c1-260 $O/stream_lab_ceiling_$nd.txt
         done ;;
-    write|fold2|copy2)
+    write|fold2|copy2|gs)
         for nd in 33554432 67108864; do
             run 300 $O/stream_lab_${step}_$nd.txt ./tools/stream_lab $nd 3 10 $step
             cut -c1-260 $O/stream_lab_${step}_$nd.txt

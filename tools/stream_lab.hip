@@ -16,7 +16,7 @@
 // and for cold also the in-stream cost including deferred write-backs (see
 // main).  Prints medians in us and TB/s of algorithmic bytes.
 //
-// usage: stream_lab [doubles per array] [rounds] [reps] [ceiling|fold|write|fold2|copy2]
+// usage: stream_lab [doubles per array] [rounds] [reps] [ceiling|fold|write|fold2|copy2|gs]
 // Build: hipcc --offload-arch=gfx950 -O3 tools/stream_lab.hip -o tools/stream_lab
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
@@ -170,6 +170,36 @@ __global__ __launch_bounds__(B) void k_copy_wc(u32x4 *out, const u32x4 *in, size
     for (int u = 0; u < U; ++u) st<NT>(out + base + u * 64, x[u]);
 }
 
+// U vectors per lane but each 4 KiB block-slice a grid apart: consecutive
+// 4 KiB of every array are read and written by consecutive workgroups (the
+// write-friendly spread of 1 vector per lane) while each lane still keeps U
+// loads in flight per array
+template <int B, int U, int NT>
+__global__ __launch_bounds__(B) void k_fold_gs(u32x4 *acc, const u32x4 *in, size_t nvec) {
+    typedef double f64x2 __attribute__((ext_vector_type(2)));
+    const size_t base = (size_t)blockIdx.x * B + threadIdx.x, stride = (size_t)gridDim.x * B;
+    u32x4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) a[u] = ld<NT>(acc + base + u * stride);
+#pragma unroll
+    for (int u = 0; u < U; ++u) b[u] = ld<NT>(in + base + u * stride);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        f64x2 s = __builtin_bit_cast(f64x2, a[u]) + __builtin_bit_cast(f64x2, b[u]);
+        st<NT>(acc + base + u * stride, __builtin_bit_cast(u32x4, s));
+    }
+}
+
+template <int B, int U, int NT>
+__global__ __launch_bounds__(B) void k_copy_gs(u32x4 *out, const u32x4 *in, size_t nvec) {
+    const size_t base = (size_t)blockIdx.x * B + threadIdx.x, stride = (size_t)gridDim.x * B;
+    u32x4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = ld<NT>(in + base + u * stride);
+#pragma unroll
+    for (int u = 0; u < U; ++u) st<NT>(out + base + u * stride, x[u]);
+}
+
 // persistent grid-stride fold, fixed grid G
 template <int B, int U, int NT>
 __global__ __launch_bounds__(B) void k_fold_pers(u32x4 *acc, const u32x4 *in, size_t nvec) {
@@ -260,7 +290,25 @@ int main(int argc, char **argv) {
 #define COPYWC(B, U, NT)                                                                      \
     vs.push_back({"copy_wc B" #B " U" #U " nt" #NT, 2.0 * bytes, [=](hipStream_t st, hipEvent_t k0, hipEvent_t k1) { \
         hipExtLaunchKernelGGL((k_copy_wc<B, U, NT>), GRID(B, U), dim3(B), 0, st, k0, k1, 0, c, b, nvec); }})
-    if (set == "copy2") {   // copy shapes suggested by the write-only lab (round 4)
+#define FOLDGS(B, U, NT)                                                                      \
+    vs.push_back({"fold_gs B" #B " U" #U " nt" #NT, 3.0 * bytes, [=](hipStream_t st, hipEvent_t k0, hipEvent_t k1) { \
+        hipExtLaunchKernelGGL((k_fold_gs<B, U, NT>), GRID(B, U), dim3(B), 0, st, k0, k1, 0, a, b, nvec); }})
+#define COPYGS(B, U, NT)                                                                      \
+    vs.push_back({"copy_gs B" #B " U" #U " nt" #NT, 2.0 * bytes, [=](hipStream_t st, hipEvent_t k0, hipEvent_t k1) { \
+        hipExtLaunchKernelGGL((k_copy_gs<B, U, NT>), GRID(B, U), dim3(B), 0, st, k0, k1, 0, c, b, nvec); }})
+    if (set == "gs") {   // grid-strided unroll: the write-friendly spread with loads in flight (round 4)
+        FOLD(256, 4, 3);
+        FOLDGS(256, 2, 3);
+        FOLDGS(256, 4, 3);
+        FOLDGS(256, 8, 3);
+        FOLDGS(64, 4, 3);
+        FOLDGS(128, 4, 3);
+        COPY(256, 1, 3);
+        COPYGS(256, 4, 3);
+        COPYGS(256, 8, 3);
+        READ(256, 4, 1, 2);
+        FILL(256, 1, 2);
+    } else if (set == "copy2") {   // copy shapes suggested by the write-only lab (round 4)
         COPY(256, 8, 3);
         COPY(256, 4, 3);
         COPY(256, 1, 3);
