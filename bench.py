@@ -163,7 +163,10 @@ def cpu_baseline(n: int, reps: int, world: int = 1):
                       f"{len(os.sched_getaffinity(0))} usable CPUs); median of {len(times)} warm calls "
                       f"({med * 1e3:.1f} ms/call, {wall:.1f} s wall); host: {cpu_model()}, "
                       f"{os.cpu_count()} logical CPUs",
-            "cpus": cpus, "spread": spread_ms(times), "wall_s": round(wall, 2)}
+            "cpus": cpus, "spread": spread_ms(times), "wall_s": round(wall, 2),
+            # SURVEY §8(d) timing method: per-PE algbw, the host, the cores used
+            "per_pe_GiBps": round(n * 8 / med / GiB, 4), "cpu_model": cpu_model(),
+            "host_cpus": os.cpu_count(), "usable_cpus": len(os.sched_getaffinity(0))}
 
 
 def cpu_baseline_table(reps: int = 3):
