@@ -287,7 +287,13 @@ void mir_copy_to_host(uint64_t off, size_t bytes) {
         g_mst.used[0] = g_mst.used[1] = false;   // every DMA has landed
     });
 }
-void mir_drain(void *) { SHMX_HIP(hipStreamSynchronize(g_state.stream)); }
+// Set by SameStreamFlush: the flushed blocks' consumer is the library stream
+// itself, which the copies are enqueued on, so nothing needs to wait here.
+thread_local bool t_same_stream_flush = false;
+
+void mir_drain(void *) {
+    if (!t_same_stream_flush) SHMX_HIP(hipStreamSynchronize(g_state.stream));
+}
 
 bool ensure_segment() {
     if (g_heap.base) return true;
@@ -511,6 +517,9 @@ bool view_offset(const void *p, uint64_t *off) {
     *off = (uint64_t)(static_cast<const char *>(p) - g_heap.view);
     return true;
 }
+
+SameStreamFlush::SameStreamFlush() : prev_(t_same_stream_flush) { t_same_stream_flush = true; }
+SameStreamFlush::~SameStreamFlush() { t_same_stream_flush = prev_; }
 
 bool segment(void **base, size_t *bytes) {
     if (!g_heap.base || host_kind()) return false;

@@ -116,6 +116,22 @@ class DeviceWrite {
     bool open_;
     bool fresh_ = false;
 };
+// While one lives (a blocking call, whose every kernel and copy runs on the
+// library stream): flushes of host-view blocks to HBM are enqueued on that
+// stream without the host waiting for them; the call's own work follows
+// them in stream order, and the call waits for its work anyway.  A host
+// store racing with the call on its source is the program's race, as in the
+// reference (the source must not change during the collective).
+class SameStreamFlush {
+  public:
+    SameStreamFlush();
+    ~SameStreamFlush();
+    SameStreamFlush(const SameStreamFlush &) = delete;
+    SameStreamFlush &operator=(const SameStreamFlush &) = delete;
+
+  private:
+    bool prev_;
+};
 // The HBM twin of a host-view address (p itself otherwise), with no change
 // of block state.
 void *twin(const void *p);

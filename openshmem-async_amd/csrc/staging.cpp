@@ -199,6 +199,11 @@ void reduce_blocking(int type, int op, void *target, const void *source,
     if (nreduce > 0 && sz && target && source && op_valid(type, op)) {
         const size_t bytes = sz * (size_t)nreduce;
         if (heap::twin(target) != target || heap::twin(source) != source) {
+            // the host's stores to the operands' blocks go up on the library
+            // stream, ahead of the call's own work there: no host wait for
+            // them (the DIRECT / SIGNAL peers read this PE's HBM only after a
+            // barrier that waits for the stream, or in stream order)
+            heap::SameStreamFlush same_stream;
             const void *s = heap::device_operand(source, bytes);
             trace_reference_overlap(target, source, bytes);   // the caller's addresses
             // blocks of a host-view target: DEVICE_NEWER from before the call
