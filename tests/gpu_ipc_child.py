@@ -502,9 +502,13 @@ elif scenario == "soak":
             n = min(n, 40000)
         st = rng.choice(sets)
         algo = rng.choice(algos)
-        mode = rng.choice(("heap", "device", "inplace", "overlap", "host", "heapoff"))
+        # on the mirrored heap also "hostheap": host stores into the view, the
+        # blocking call on the view addresses, host loads of the result
+        # (the small-result copy-back, the same-stream flush, lazy fetches)
+        extra_modes = ("hostheap",) if MIRRORED else ()
+        mode = rng.choice(("heap", "device", "inplace", "overlap", "host", "heapoff") + extra_modes)
         if algo == "signal":
-            mode = rng.choice(("heap", "inplace", "heapoff"))     # symmetric operands only
+            mode = rng.choice(("heap", "inplace", "heapoff") + extra_modes)     # symmetric operands only
         if (n + 3) * 16 > CAP:
             n = CAP // 16 - 3
         try:

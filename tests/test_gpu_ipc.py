@@ -240,15 +240,18 @@ def test_rccl_transport_with_rccl_double(tmp_path, npes):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("transport,npes", [("ipc", 3), ("rccl", 4), ("ipc", 8), ("rccl", 8)])
-def test_soak_random_calls(tmp_path, transport, npes):
+@pytest.mark.parametrize("transport,npes,heap", [("ipc", 3, "device"), ("rccl", 4, "device"), ("ipc", 8, "device"),
+                                                ("rccl", 8, "device"), ("ipc", 3, "mirrored"),
+                                                ("rccl", 4, "mirrored")])
+def test_soak_random_calls(tmp_path, transport, npes, heap):
     """Random collective calls, the same seeded sequence on every PE: any
     reference pair, size (edges favoured), active set, algorithm the transport
     offers and operand placement, each against the oracle.  The RCCL
-    transport runs on the RCCL test double.  $SOAK_ITERS / $SOAK_SEED make
-    longer or different runs."""
+    transport runs on the RCCL test double.  On the mirrored heap the draw
+    also includes blocking calls on host-view operands the host writes and
+    reads.  $SOAK_ITERS / $SOAK_SEED make longer or different runs."""
     env = {"SHMEMX_TRANSPORT": transport, "SOAK_ITERS": os.environ.get("SOAK_ITERS", "60"),
-           "SOAK_SEED": os.environ.get("SOAK_SEED", "7")}
+           "SOAK_SEED": os.environ.get("SOAK_SEED", "7"), "SHMEMX_HEAP_MEMORY": heap}
     if transport == "rccl":
         env["FAKE_RCCL"] = os.path.join(HERE, "native", "libfake_rccl.so")
     reports = run_pes(tmp_path, npes, "soak", env, timeout=900)
