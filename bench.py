@@ -80,7 +80,7 @@ def parse():
 
 def pmc_traffic(kernel_key: str):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if any
-    (profiles/*pmc*.json written by tools/profile_pmc.py)."""
+    (profiles/*pmc*.json, newest round first, written by tools/summarize_prof.py)."""
     pdir = os.path.join(REPO, "profiles")
     if not os.path.isdir(pdir):
         return None

@@ -40,6 +40,10 @@ run() {   # run <seconds> <log> <cmd...>: one GPU step under its own limit
     [ $rc -eq 0 ] || { tail -25 "$log"; exit $rc; }
 }
 
+json_line() {   # json_line <log> <json>: the bench line alone, as a JSON file
+    grep '^{"metric"' "$1" > "$2" && cut -c1-400 "$2"
+}
+
 BENCH_HEAD="python3 bench.py --steps 20 --warmup 5 --extras 0 --no-cpu-baseline"
 TAG=${TAG:-r04}
 
@@ -54,8 +58,9 @@ for step in "$@"; do
         export GPU_TEST_LOGDIR=$O/ipclogs
         run 900 $O/gpu_tests_k.log python3 -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread -k "$TESTS_K"
         tail -3 $O/gpu_tests_k.log ;;
-    bench) run 600 $O/bench_n1.json python3 bench.py; grep '"metric"' $O/bench_n1.json | cut -c1-400 ;;
-    bench2) run 600 $O/bench_n1_b.json python3 bench.py; grep '"metric"' $O/bench_n1_b.json | cut -c1-400 ;;
+    bench|bench2)   # the log keeps rank 0's progress lines; the .json holds the one bench line
+        b=bench_n1; [ $step = bench2 ] && b=bench_n1_b
+        run 600 $O/$b.log python3 bench.py; json_line $O/$b.log $O/$b.json ;;
     trace)
         run 600 $O/trace.log rocprofv3 --kernel-trace --stats -d $O/trace -o trace --output-format csv -- python3 bench.py
         grep '"metric"' $O/trace.log | cut -c1-300
@@ -112,15 +117,15 @@ for step in "$@"; do
     rehearse2|rehearse8)
         np=${step#rehearse}
         q=4; [ "$np" -gt 4 ] && q=2     # 8 processes' queues on one GPU (tests/test_gpu_ipc.py)
-        GPU_MAX_HW_QUEUES=$q SHMEMX_TRANSPORT=ipc SHMEMX_SHARE_GPU=1 run 900 $O/rehearse_ipc_n$np.json python3 -m torch.distributed.run \
+        GPU_MAX_HW_QUEUES=$q SHMEMX_TRANSPORT=ipc SHMEMX_SHARE_GPU=1 run 900 $O/rehearse_ipc_n$np.log python3 -m torch.distributed.run \
             --nnodes=1 --nproc-per-node $np --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus $np \
             --steps 10 --warmup 3
-        grep '"metric"' $O/rehearse_ipc_n$np.json | cut -c1-600 ;;
+        json_line $O/rehearse_ipc_n$np.log $O/rehearse_ipc_n$np.json ;;
     rehearse_rccl)
-        FAKE_RCCL=$PWD/tests/native/libfake_rccl.so SHMEMX_SHARE_GPU=1 run 900 $O/rehearse_rccl_n2.json \
+        FAKE_RCCL=$PWD/tests/native/libfake_rccl.so SHMEMX_SHARE_GPU=1 run 900 $O/rehearse_rccl_n2.log \
             python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
             --master-port 29512 bench.py --gpus 2 --steps 10 --warmup 3
-        grep '"metric"' $O/rehearse_rccl_n2.json | cut -c1-600 ;;
+        json_line $O/rehearse_rccl_n2.log $O/rehearse_rccl_n2.json ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
 done
