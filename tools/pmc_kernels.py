@@ -12,7 +12,12 @@ FETCH_SIZE and WRITE_SIZE in separate --pmc runs; tools/gpu_steps.sh pmc_kernels
                      contiguous in one block (the A2A workspace layout)
   gather7            gather_kernel, 7 segments of 4 Mi doubles (DIRECT's
                      all-gather at P = 8, 32 Mi doubles)
+  copy64Mi           the PE_size = 1 call (shmemx_reduce_on_stream, a copy:
+                     reduce-op.c:213-216) over 64 Mi doubles, 512 MiB: the copy
+                     kernel fold_kernel<long,SUM,1 input,1 vector,nt>
   checksum           checksum_kernel over 32 Mi doubles
+  verify             shmemx_verify at one PE (the same checksum kernel: its
+                     launches join checksum's run in the trace)
 
 Prints one JSON line per config: launches, HIP-event average launch time on
 the launch stream, algorithmic bytes per launch and the rate.
@@ -34,9 +39,11 @@ s = torch.cuda.Stream()
 Mi = 1024 * 1024
 
 
-def timed(name, fn, alg_bytes, grid_hint, blocking=False):
+def timed(name, fn, alg_bytes, grid_hint, blocking=False, shares_run=False):
     """blocking: the call synchronises itself (shmemx_checksum), so it is timed
-    on the host clock, launch + wait included."""
+    on the host clock, launch + wait included.  shares_run: this config
+    launches the same kernel at the same grid as the one before it, so
+    tools/summarize_pmc.py finds its launches in that config's run."""
     fn()
     torch.cuda.synchronize()
     if blocking:
@@ -55,7 +62,7 @@ def timed(name, fn, alg_bytes, grid_hint, blocking=False):
         us = e0.elapsed_time(e1) / REPS * 1e3
     print(json.dumps({"config": name, "launches": REPS + 1, "avg_us": round(us, 2),
                       "alg_bytes": alg_bytes, "GBps": round(alg_bytes / us / 1e3, 1),
-                      "grid_hint": grid_hint}), flush=True)
+                      "grid_hint": grid_hint, "shares_run": shares_run}), flush=True)
 
 
 def blocks(nvec, unroll=4):
@@ -122,7 +129,19 @@ timed("gather7", lambda: shm.gather([x for x, _ in segs], [y for _, y in segs], 
 assert torch.equal(dst[sl:], src[sl:]), "gather copied wrong bytes"
 del dst
 
+# configs[1]'s literal drop-in call at PE_size = 1: a copy (reduce-op.c:213-216)
+n2 = 64 * Mi
+csrc = torch.rand(n2, dtype=torch.float64, device="cuda")
+cdst = torch.empty(n2, dtype=torch.float64, device="cuda")
+timed("copy64Mi", lambda: shm.reduce_on_stream("double", "sum", cdst, csrc, n2, 0, 0, 1, "auto",
+                                               s.cuda_stream),
+      2 * 8 * n2, n2 // 2)
+torch.cuda.synchronize()
+assert torch.equal(cdst, csrc), "the PE_size = 1 call copied wrong bytes"
+del csrc, cdst
+
 timed("checksum", lambda: shm.checksum("double", src, n), 8 * n, None, blocking=True)
 # shmemx_verify at one PE: the checksum launch, the stream wait and the
 # (here empty) exchange — the whole call on the host clock
-timed("verify", lambda: shm.verify("double", src, n, 0, 0, 1), 8 * n, None, blocking=True)
+timed("verify", lambda: shm.verify("double", src, n, 0, 0, 1), 8 * n, None, blocking=True,
+      shares_run=True)

@@ -5,7 +5,9 @@ usage: summarize_pmc.py <pmc_kernels.log> <trace_dir> <fetch_dir> <write_dir> <o
 Dispatches of the library's kernels (names under shmx::) are taken in
 dispatch order and cut into runs of consecutive launches of one (kernel, grid
 size); run i belongs to the i-th config line of the log (the script launches
-each config's kernel back to back).  HBM bytes per launch = 2 * FETCH_SIZE +
+each config's kernel back to back), except that a config marked
+"shares_run" (the same kernel and grid as the config before it) takes the
+previous config's run.  HBM bytes per launch = 2 * FETCH_SIZE +
 WRITE_SIZE (KiB; FETCH_SIZE doubled per MI355X_MICROARCH.md "HBM": gfx950
 counts half of a wide streaming read), compared with the algorithmic bytes.
 """
@@ -59,8 +61,11 @@ def main():
     cfgs = [json.loads(line) for line in open(log) if line.startswith('{"config"')]
     fr, wr, tr = runs(fetch, "FETCH_SIZE"), runs(write, "WRITE_SIZE"), trace_runs(trace)
     out = []
-    for i, c in enumerate(cfgs):
+    i = -1
+    for c in cfgs:
         e = dict(c)
+        if not (c.get("shares_run") and i >= 0):
+            i += 1
         if i < len(tr):
             (name, grid), us = tr[i]
             e["kernel"] = name[:200]
