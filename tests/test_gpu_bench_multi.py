@@ -109,6 +109,9 @@ def test_bench_multi_rank_line(tmp_path, transport, npes):
     assert set(cfg["float_sum_busbw_GBps_vs_nreduce"]) == set(cfg["float_sum_GiBps_vs_nreduce"]), cfg
     for k, a in cfg["float_sum_algbw_GBps_vs_nreduce"].items():
         assert a > 0 and abs(cfg["float_sum_busbw_GBps_vs_nreduce"][k] - a * 2 * (npes - 1) / npes) < 0.02, (k, a)
+    he = extras["host_resident_e2e"]   # host-resident operands on every PE, exact sums
+    assert isinstance(he, dict) and he["correct"] is True and he["last_error"] == 0 and he["GiBps"] > 0, he
+    assert he["nreduce"] == 1 << 20, he
     pa = extras["push_allreduce"]      # the store-based exchange, exact integer sums
     assert isinstance(pa, dict) and pa["correct"] is True and pa["GiBps"] > 0, pa
     bad = []
