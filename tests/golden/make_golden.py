@@ -31,7 +31,7 @@ sys.path.insert(0, os.path.join(HERE, "..", "..", "oracle"))
 import oracle as O  # noqa: E402
 
 NPES = 8
-SIZES = [0, 1, 63, 64, 65, 127, 1000, 4103]
+SIZES = [0, 1, 63, 64, 65, 127, 128, 1000, 4103, 65536 + 13]   # SURVEY.md §8c grid
 SETS = [(0, 0, 1), (0, 0, 2), (0, 0, 3), (0, 0, 4), (0, 0, 8), (1, 0, 3), (0, 1, 4), (1, 1, 3),
         (2, 0, 5), (0, 2, 2)]
 ALL_OPS = ["sum", "prod", "and", "or", "xor", "min", "max"]
