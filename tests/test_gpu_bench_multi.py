@@ -46,7 +46,7 @@ def strings(x, path=""):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("transport,npes", [("rccl", 2), ("ipc", 2), ("rccl", 8), ("ipc", 8)])
+@pytest.mark.parametrize("transport,npes", [("rccl", 2), ("ipc", 2), ("rccl", 4), ("ipc", 4), ("rccl", 8), ("ipc", 8)])
 def test_bench_multi_rank_line(tmp_path, transport, npes):
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     env.update(SHMEMX_SHARE_GPU="1", SHMEMX_BARRIER_TIMEOUT="120", PYTHONUNBUFFERED="1")
