@@ -979,6 +979,64 @@ elif scenario == "limits":
         if pe == rep % npes:
             shm.set_fused_twoshot_kb(default_kb)
         run_case("double", "sum", n, (0, 0, npes), "direct", "device", 0x11C0 + rep)
+elif scenario == "big":
+    # Arrays past 2 GiB per PE through the multi-PE paths.  The reference
+    # computes its byte count as an int (reduce-op.c:180) and stops at 2 GiB;
+    # every offset, shard, slice and count here is 64-bit.  long xor and long
+    # sum (wrapping) over 2.5 GiB + 40 B per PE (an odd length: scalar tails
+    # at the far end), on the heap, through each algorithm in $BIG_ALGOS;
+    # against torch's fold of every PE's regenerated source (integer results:
+    # any order is exact) on every element, 64 Ki sampled elements against
+    # the oracle, and identical on every PE.
+    n = (1 << 28) + (1 << 26) + 5
+    nbytes = n * 8
+    BIG_SRC, BIG_TGT = shm.malloc(nbytes), shm.malloc(nbytes)
+    assert BIG_SRC and BIG_TGT, "shmem_malloc of the 2.5 GiB operands failed"
+
+    def gen(q, salt):
+        g = torch.Generator(device="cuda")
+        g.manual_seed(0xB16 + 131 * q + salt)
+        return torch.randint(-2**63, 2**63 - 1, (n,), dtype=torch.int64, device="cuda", generator=g)
+
+    smp = torch.arange(0, n, n // 65536, device="cuda")
+    smp = torch.cat([smp, torch.arange(n - 7, n, device="cuda")])   # the tail too
+    salt = 0
+    for op in ("xor", "sum"):
+        for algo in os.environ.get("BIG_ALGOS", "auto").split(","):
+            salt += 1
+            ncases += 1
+            print(f"big long {op} n={n} algo={algo}", flush=True)
+            heap_write(BIG_SRC, gen(pe, salt), nbytes)
+            heap_write(BIG_TGT, torch.zeros(n, dtype=torch.int64, device="cuda"), nbytes)
+            torch.cuda.synchronize()
+            shm.set_algo(algo)
+            shm.to_all("long", op, BIG_TGT, BIG_SRC, n, 0, 0, npes)
+            shm.set_algo("auto")
+            if shm.last_error():
+                fails.append(f"big {op} {algo}: last_error {shm.last_error()}")
+                continue
+            got = torch.empty(n, dtype=torch.int64, device="cuda")
+            shm.memcpy(got, twin(BIG_TGT), nbytes)
+            f = torch.bitwise_xor if op == "xor" else torch.add
+            want = gen(0, salt)
+            for q in range(1, npes):
+                want = f(want, gen(q, salt))
+            torch.cuda.synchronize()
+            if not torch.equal(got, want):
+                bad = int((got != want).sum())
+                first = int((got != want).nonzero()[0])
+                fails.append(f"big {op} {algo}: {bad} elements differ, the first at {first}")
+            del want
+            srcs = np.stack([gen(q, salt)[smp].cpu().numpy() for q in range(npes)])
+            ref = oracle.reduce_sim("long", op, srcs, 0, 0, npes)[0]
+            if not same_bits(got[smp].cpu().numpy(), ref):
+                fails.append(f"big {op} {algo}: sampled elements differ from the oracle")
+            del got
+            if not shm.verify("long", BIG_TGT, n, 0, 0, npes):
+                fails.append(f"big {op} {algo}: targets differ across PEs")
+    extra["big_bytes_per_pe"] = nbytes
+    shm.free(BIG_TGT)
+    shm.free(BIG_SRC)
 elif scenario == "signal_timeout":
     # one SIGNAL call together (maps and votes), then PE 0 calls again alone:
     # its device barrier must give up after $SHMEMX_SIGNAL_TIMEOUT seconds and

@@ -275,6 +275,25 @@ def test_ipc_baseline_configs_full_size(tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("transport,algos", [("ipc", "auto,signal,gather"), ("rccl", "auto,gather")])
+def test_beyond_2gib_per_pe_multi_pe(tmp_path, transport, algos):
+    """2.5 GiB per PE (past the reference's int byte count, reduce-op.c:180)
+    through the multi-PE paths, 2 PE processes: DIRECT (auto on IPC), SIGNAL
+    and GATHER over IPC; A2A (auto for xor) and RCCL reduce-scatter +
+    all-gather (auto for sum) and GATHER over the RCCL test double.  Every
+    element checked, identical on both PEs."""
+    env = {"SHMEMX_TRANSPORT": transport, "SHMEM_SYMMETRIC_HEAP_SIZE": "8G", "BIG_ALGOS": algos,
+           "SHMEMX_HEAP_MEMORY": "device"}
+    if transport == "rccl":
+        env["FAKE_RCCL"] = os.path.join(HERE, "native", "libfake_rccl.so")
+    reports = run_pes(tmp_path, 2, "big", env, timeout=600)
+    for r in reports:
+        assert r["ncases"] == 2 * len(algos.split(","))
+        assert not r["fails"], f"PE {r['pe']}: {r['fails']}"
+        assert r["big_bytes_per_pe"] > 2 << 30
+
+
+@pytest.mark.gpu
 def test_ipc_direct_staged_in_chunks(tmp_path):
     # a 1 MiB scratch: every staged operand crosses several chunks per call
     reports = run_pes(tmp_path, 3, "chunk", {"SHMEMX_DIRECT_SCRATCH_MB": "1"})
