@@ -242,7 +242,7 @@ def test_rccl_transport_with_rccl_double(tmp_path, npes):
 @pytest.mark.gpu
 @pytest.mark.parametrize("transport,npes,heap", [("ipc", 3, "device"), ("rccl", 4, "device"), ("ipc", 8, "device"),
                                                 ("rccl", 8, "device"), ("ipc", 3, "mirrored"),
-                                                ("rccl", 4, "mirrored")])
+                                                ("rccl", 4, "mirrored"), ("ipc", 8, "mirrored")])
 def test_soak_random_calls(tmp_path, transport, npes, heap):
     """Random collective calls, the same seeded sequence on every PE: any
     reference pair, size (edges favoured), active set, algorithm the transport
