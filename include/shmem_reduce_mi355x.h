@@ -381,13 +381,14 @@ void *shmemx_heap_ptr(const void *addr, int pe);
  *                             read(2) into a source) fails with EFAULT on a
  *                             block the library has not opened;
  *   shmemx_mirror_stats       out[0..6] = write faults, read faults, blocks
- *                             copied to HBM, blocks copied back, blocks marked
- *                             device-newer, faults that waited for a
- *                             collective writing their block, blocks a
- *                             blocking call made clean before returning
- *                             (its result, up to $SHMEMX_MIRROR_SETTLE_KB,
- *                             default 256 KiB, copied back); returns how
- *                             many were filled.
+ *                             copied to HBM (whole, or a small operand's own
+ *                             bytes of them), blocks copied back, blocks
+ *                             marked device-newer, faults that waited for a
+ *                             collective writing their block, blocks whose
+ *                             result a blocking call put into the view
+ *                             before returning (up to
+ *                             $SHMEMX_MIRROR_SETTLE_KB, default 256 KiB);
+ *                             returns how many were filled.
  * A host access to a block a collective is writing waits for it (from any
  * thread), then reads the result; a fetch waits only for the streams that
  * wrote the view (the caller's stream of a stream-ordered call, not the whole

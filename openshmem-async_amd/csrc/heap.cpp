@@ -453,6 +453,21 @@ void *device_operand(const void *p, size_t bytes) {
     return g_heap.base + off;
 }
 
+const void *device_operand_bytes(const void *p, size_t bytes) {
+    if (!in_view(p) || bytes > g_heap.arena.capacity() - (uint64_t)(static_cast<const char *>(p) - g_heap.view))
+        return p;
+    const uint64_t off = (uint64_t)(static_cast<const char *>(p) - g_heap.view);
+    mirror::flush_bytes(off, bytes);
+    return g_heap.base + off;
+}
+
+void *alias_device(const void *p, size_t bytes) {
+    if (!bytes || !in_view(p) ||
+        bytes > g_heap.arena.capacity() - (uint64_t)(static_cast<const char *>(p) - g_heap.view))
+        return nullptr;
+    return mir_alias_device((uint64_t)(static_cast<const char *>(p) - g_heap.view), bytes);
+}
+
 void *device_operand_open(const void *p) {
     if (!in_view(p)) return const_cast<void *>(p);
     const uint64_t off = (uint64_t)(static_cast<const char *>(p) - g_heap.view);
@@ -470,34 +485,42 @@ void *twin(const void *p) {
     return in_view(p) ? g_heap.base + (static_cast<const char *>(p) - g_heap.view) : const_cast<void *>(p);
 }
 
-DeviceWrite::DeviceWrite(void *p, size_t bytes, void *stream)
+DeviceWrite::DeviceWrite(void *p, size_t bytes, void *stream, bool light)
     : dev_(p), stream_(stream), open_(false) {
     if (!bytes || !in_view(p) ||
         bytes > g_heap.arena.capacity() - (uint64_t)(static_cast<const char *>(p) - g_heap.view))
         return;
     const uint64_t off = (uint64_t)(static_cast<const char *>(p) - g_heap.view);
-    mirror::begin_device_write(off, bytes, &fresh_);
+    light_ = light && mirror::begin_light_write(off, bytes);
+    if (light_) fresh_ = true;
+    else mirror::begin_device_write(off, bytes, &fresh_);
     dev_ = g_heap.base + off;
     off_ = off;
     bytes_ = bytes;
     open_ = true;
 }
 
-void DeviceWrite::close() {
+void DeviceWrite::close(bool copied) {
     if (!open_) return;
     open_ = false;
     record_writer(stream_);
-    mirror::end_device_write(off_, bytes_);
+    if (light_) mirror::end_light_write(off_, bytes_, copied);
+    else mirror::end_device_write(off_, bytes_);
 }
 
 size_t DeviceWrite::settle(size_t limit, bool copied) {
-    if (!open_ || bytes_ > limit) return 0;
+    if (!open_) return 0;
+    if (light_) {
+        close(copied);
+        return copied ? 0 : bytes_;
+    }
+    if (bytes_ > limit) return 0;
     close();
     return mirror::settle(off_, bytes_, fresh_, copied && fresh_);
 }
 
 void *DeviceWrite::settle_dst(size_t limit) const {
-    if (!open_ || !fresh_ || bytes_ > limit) return nullptr;
+    if (!open_ || !fresh_ || (bytes_ > limit && !light_)) return nullptr;
     return mir_alias_device(off_, bytes_);
 }
 

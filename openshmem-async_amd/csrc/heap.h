@@ -88,13 +88,19 @@ void device_wrote(const void *p, size_t bytes, void *stream);
 // HBM twin of a host-view address, p itself otherwise.
 class DeviceWrite {
   public:
-    DeviceWrite(void *p, size_t bytes, void *stream);
+    // light: a BLOCKING call's small target whose result the call's stream
+    // also stores into the view's alias (settle_dst): no block state or
+    // protection changes (mirror::begin_light_write); taken only if the
+    // blocks allow it, else the ordinary DEVICE_NEWER marking
+    DeviceWrite(void *p, size_t bytes, void *stream, bool light = false);
     ~DeviceWrite() { close(); }
     DeviceWrite(const DeviceWrite &) = delete;
     DeviceWrite &operator=(const DeviceWrite &) = delete;
     void *ptr() const { return dev_; }
-    // record the writer and end the write in flight (the destructor's work)
-    void close();
+    bool light() const { return light_; }
+    // record the writer and end the write in flight (the destructor's work);
+    // a light write's result goes into the view here unless `copied`
+    void close(bool copied = false);
     // After a BLOCKING call's work has completed: if the target is at most
     // `limit` bytes, close the write and copy the result back into the view
     // (mirror::settle), so its blocks are CLEAN — readable by system calls
@@ -115,6 +121,7 @@ class DeviceWrite {
     size_t bytes_ = 0;
     bool open_;
     bool fresh_ = false;
+    bool light_ = false;
 };
 // While one lives (a blocking call, whose every kernel and copy runs on the
 // library stream): flushes of host-view blocks to HBM are enqueued on that
@@ -132,6 +139,12 @@ class SameStreamFlush {
   private:
     bool prev_;
 };
+// A blocking call's small source: only its own bytes that the host wrote go
+// to HBM (mirror::flush_bytes), no state change; returns the HBM twin.
+const void *device_operand_bytes(const void *p, size_t bytes);
+// The device address of the view's page-locked alias at host-view address
+// p (bytes inside one alias region), or nullptr.
+void *alias_device(const void *p, size_t bytes);
 // The HBM twin of a host-view address (p itself otherwise), with no change
 // of block state.
 void *twin(const void *p);

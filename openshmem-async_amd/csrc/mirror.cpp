@@ -326,6 +326,55 @@ size_t settle(uint64_t off, size_t bytes, bool fresh, bool copied) {
     return copied ? 0 : bytes;
 }
 
+size_t flush_bytes(uint64_t off, size_t bytes) {
+    if (!g_view.base || !bytes) return 0;
+    Guard g;
+    const size_t b0 = block_of(off), b1 = std::min(block_of(off + bytes - 1) + 1, g_view.nblocks);
+    const uint64_t end = off + bytes;
+    size_t touched = 0;
+    for (size_t b = b0; b < b1;) {
+        if (g_view.state[b] != HOST_NEWER) {
+            ++b;
+            continue;
+        }
+        size_t e = b;
+        while (e < b1 && g_view.state[e] == HOST_NEWER) ++e;
+        // the operand's bytes inside blocks [b, e)
+        const uint64_t lo = std::max<uint64_t>(off, (uint64_t)b * kBlock);
+        const uint64_t hi = std::min<uint64_t>(end, (uint64_t)e * kBlock);
+        g_view.be.to_device(lo, hi - lo, g_view.be.ctx);
+        touched += e - b;
+        b = e;
+    }
+    if (touched) g_view.be.drain(g_view.be.ctx);
+    g_view.st.blocks_flushed += touched;
+    return touched;
+}
+
+bool begin_light_write(uint64_t off, size_t bytes) {
+    if (!g_view.base || !bytes) return false;
+    Guard g;
+    const size_t b0 = block_of(off), b1 = std::min(block_of(off + bytes - 1) + 1, g_view.nblocks);
+    for (size_t b = b0; b < b1; ++b)
+        if (g_view.state[b] == DEVICE_NEWER || g_view.pending[b]) return false;
+    for (size_t b = b0; b < b1; ++b) ++g_view.pending[b];
+    return true;
+}
+
+size_t end_light_write(uint64_t off, size_t bytes, bool copied) {
+    if (!g_view.base || !bytes) return 0;
+    Guard g;
+    const size_t b0 = block_of(off), b1 = std::min(block_of(off + bytes - 1) + 1, g_view.nblocks);
+    // the result's bytes into the alias first (if the call's stream did not),
+    // then the write ends: a block another writer marked DEVICE_NEWER in the
+    // meantime is fetched only after this (its fault waits for pending)
+    if (!copied) g_view.be.to_host(off, bytes, g_view.be.ctx);
+    for (size_t b = b0; b < b1; ++b)
+        if (g_view.pending[b]) --g_view.pending[b];
+    g_view.st.blocks_settled += b1 - b0;
+    return copied ? 0 : bytes;
+}
+
 size_t device_wrote(uint64_t off, size_t bytes) {
     if (!g_view.base || !bytes) return 0;
     Guard g;

@@ -123,6 +123,27 @@ void end_device_write(uint64_t off, size_t bytes);
 // into the alias (a copy kernel before its host signal), so only the block
 // states and protections change.  Returns the bytes copied here.
 size_t settle(uint64_t off, size_t bytes, bool fresh, bool copied = false);
+// The light path of a BLOCKING call on small operands (heap.h DeviceWrite,
+// staging.cpp), which changes no block state and no page protection:
+// flush_bytes() sends the part of a small source [off, off + bytes) that lies
+// in HOST_NEWER blocks to HBM and leaves those blocks HOST_NEWER (writable:
+// the host's next store takes no fault; the next call that needs the whole
+// block flushes it whole).  Returns the blocks touched (counted as flushed).
+// The copy's drain follows Backend::drain (a blocking call's work follows it
+// on the same stream).
+size_t flush_bytes(uint64_t off, size_t bytes);
+// begin_light_write(): a small target whose blocks are CLEAN or HOST_NEWER
+// with no write in flight counts one write in flight on each and keeps its
+// state: the call's own stream stores the result into HBM AND into the alias
+// (the view's bytes), so the blocks stay what they were — CLEAN blocks equal
+// HBM again, HOST_NEWER ones are flushed whole later, the result included.
+// False (nothing changed) if a block is DEVICE_NEWER or has a write in flight:
+// the caller takes begin_device_write instead.
+bool begin_light_write(uint64_t off, size_t bytes);
+// The light write has ended and its work completed: `copied` = the call's
+// stream stored the result into the alias; otherwise it is copied back here
+// (Backend::to_host).  Counts the blocks as settled; returns bytes copied.
+size_t end_light_write(uint64_t off, size_t bytes, bool copied);
 // After a collective wrote [off, off + bytes) in HBM without
 // begin_device_write (a collect target, whose length is known only after
 // the exchange): the overlapped blocks become DEVICE_NEWER (call flush on the

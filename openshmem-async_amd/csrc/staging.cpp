@@ -204,12 +204,21 @@ void reduce_blocking(int type, int op, void *target, const void *source,
             // them (the DIRECT / SIGNAL peers read this PE's HBM only after a
             // barrier that waits for the stream, or in stream order)
             heap::SameStreamFlush same_stream;
-            const void *s = heap::device_operand(source, bytes);
+            // Small operands whose result one workgroup can also store into
+            // the view's alias (the ISx nreduce = 1 use) take the light path:
+            // only the source's own host-written bytes go up, and no block
+            // changes state or protection (mirror.h begin_light_write), so
+            // the host's next store into those blocks takes no fault either
+            const size_t lim = mirror_settle_limit();
+            void *adst = bytes <= lim ? heap::alias_device(target, bytes) : nullptr;
+            const bool light = adst && heap::twin(target) != target && heap::twin(source) != source &&
+                               copy_one_workgroup(type, adst, heap::twin(target), (size_t)nreduce);
+            const void *s = light ? heap::device_operand_bytes(source, bytes) : heap::device_operand(source, bytes);
             trace_reference_overlap(target, source, bytes);   // the caller's addresses
             // blocks of a host-view target: DEVICE_NEWER from before the call
-            // (host accesses wait for it); the blocking call completes on the
-            // library stream, its recorded writer
-            heap::DeviceWrite t(target, bytes, g_state.stream);
+            // (host accesses wait for it), or on the light path unchanged; the
+            // blocking call completes on the library stream, its recorded writer
+            heap::DeviceWrite t(target, bytes, g_state.stream, light);
             // a small result also goes straight into the view's page-locked
             // alias: the call's last kernel stores it there before the host
             // signal (one workgroup, so its own drained stores and
@@ -224,8 +233,13 @@ void reduce_blocking(int type, int op, void *target, const void *source,
             g_state.settled = false;
             // the call's work is complete: a small result is back in the view
             // (copied above, or now), so the caller's system calls can read
-            // it (larger targets are fetched on first access)
-            t.settle(mirror_settle_limit(), copied);
+            // it (larger targets are fetched on first access).
+            // A call that failed wrote no target: on the light path the view
+            // already holds the target's bytes, and HBM may not (a
+            // host-written target block is not flushed there), so nothing is
+            // copied back
+            const bool failed = shmemx_reduce_last_error() != SHMEMX_OK;
+            t.settle(mirror_settle_limit(), copied || (failed && t.light()));
             return;
         }
     }

@@ -291,6 +291,72 @@ int main(int argc, char **argv) {
         CHECK(M::settle(e, 8, fresh, true) == 0 && g_d2h == d2h1 && M::state_of(e) == M::CLEAN);
         CHECK(h[e + 3] == truth[e + 3] && M::stats(false).read_faults == rf1);
     }
+    // (1d) the light path of a blocking call on small operands: flush_bytes
+    // sends only the operand's bytes of a HOST_NEWER block and leaves it
+    // HOST_NEWER (writable: no fault on the next store); begin_light_write
+    // keeps CLEAN / HOST_NEWER blocks as they are, refuses a block with a
+    // write in flight or DEVICE_NEWER; end_light_write copies the result back
+    // unless the call's stream did, and counts the blocks settled.
+    {
+        const size_t b = 62 * M::kBlock;
+        h[b + 10] = 0x11;                      // HOST_NEWER (a write fault)
+        h[b + 5000] = 0x22;
+        truth[b + 10] = 0x11;
+        truth[b + 5000] = 0x22;
+        CHECK(M::state_of(b) == M::HOST_NEWER);
+        M::flush(b + M::kBlock, M::kBlock);    // block 63 CLEAN (a write fault may open a run)
+        const size_t h2d0 = g_h2d;
+        const auto fl0 = M::stats(false).blocks_flushed;
+        CHECK(M::flush_bytes(b + 8, 8) == 1 && g_h2d - h2d0 == 8 && g_dev[b + 10] == 0x11);
+        CHECK(g_dev[b + 5000] != 0x22);        // the rest of the block stayed on the host
+        CHECK(M::state_of(b) == M::HOST_NEWER && M::stats(false).blocks_flushed == fl0 + 1);
+        const auto wf0 = M::stats(false).write_faults;
+        h[b + 11] = 0x33;                      // still writable: no fault
+        truth[b + 11] = 0x33;
+        CHECK(M::stats(false).write_faults == wf0);
+        CHECK(M::flush_bytes(b + M::kBlock, 8) == 0);   // block 63 is CLEAN: nothing moves
+        // a light write on the HOST_NEWER block, the result also stored into
+        // the alias by the call's stream: nothing changes state
+        CHECK(M::begin_light_write(b + 64, 8));
+        CHECK(M::state_of(b) == M::HOST_NEWER);
+        CHECK(!M::begin_light_write(b + 128, 8));       // a write is in flight on block 62
+        bool fresh = true;
+        CHECK(M::begin_device_write(b + 2 * M::kBlock, 8, &fresh) == 1);   // block 64: in flight
+        CHECK(!M::begin_light_write(b + 2 * M::kBlock + 64, 8));
+        for (size_t i = 0; i < 8; ++i) {
+            g_dev[b + 2 * M::kBlock + i] = (unsigned char)(0x70 + i);
+            truth[b + 2 * M::kBlock + i] = g_dev[b + 2 * M::kBlock + i];
+        }
+        M::end_device_write(b + 2 * M::kBlock, 8);
+        for (size_t i = 0; i < 8; ++i) {
+            g_dev[b + 64 + i] = (unsigned char)(0xA0 + i);
+            M::alias_base()[b + 64 + i] = (char)(0xA0 + i);
+            truth[b + 64 + i] = g_dev[b + 64 + i];
+        }
+        const size_t d2h0 = g_d2h;
+        const auto se0 = M::stats(false).blocks_settled;
+        CHECK(M::end_light_write(b + 64, 8, true) == 0 && g_d2h == d2h0);
+        CHECK(M::stats(false).blocks_settled == se0 + 1);
+        CHECK(h[b + 67] == truth[b + 67] && M::state_of(b) == M::HOST_NEWER);
+        // flushed whole later: HBM then holds the host's bytes and the result
+        CHECK(M::flush(b, 1) == 1 && g_dev[b + 5000] == 0x22 && g_dev[b + 11] == 0x33 && g_dev[b + 64] == 0xA0);
+        // on a CLEAN block without the stream's copy: end_light_write copies
+        // the result's bytes back, and the block stays CLEAN and readable
+        const size_t c = b + M::kBlock;
+        CHECK(M::state_of(c) == M::CLEAN && M::begin_light_write(c + 16, 16));
+        for (size_t i = 0; i < 16; ++i) {
+            g_dev[c + 16 + i] = (unsigned char)(0x50 + i);
+            truth[c + 16 + i] = g_dev[c + 16 + i];
+        }
+        const size_t d2h1 = g_d2h;
+        const auto rf0 = M::stats(false).read_faults;
+        CHECK(M::end_light_write(c + 16, 16, false) == 16 && g_d2h - d2h1 == 16);
+        CHECK(M::state_of(c) == M::CLEAN && h[c + 20] == truth[c + 20] && M::stats(false).read_faults == rf0);
+        // a DEVICE_NEWER block refuses the light path, and is left as it was
+        M::device_wrote(c, M::kBlock);
+        CHECK(!M::begin_light_write(c + 16, 8) && M::state_of(c) == M::DEVICE_NEWER);
+        CHECK(h[c + 20] == truth[c + 20] && M::state_of(c) == M::CLEAN);   // fetched by the fault
+    }
     // (2) A store another thread makes while a flush copies its block (after
     // the protection change, before the copy) is not lost: it faults, waits,
     // and leaves the block HOST_NEWER for the next flush.
@@ -346,7 +412,7 @@ int main(int argc, char **argv) {
     // random interleavings against the model
     std::mt19937_64 rng(12345);
     for (int it = 0; it < iters; ++it) {
-        const int what = (int)(rng() % 4);
+        const int what = (int)(rng() % 5);
         const size_t off = rng() % bytes;
         const size_t len = 1 + rng() % (3 * M::kBlock);
         const size_t n = off + len > bytes ? bytes - off : len;
@@ -361,6 +427,27 @@ int main(int argc, char **argv) {
         } else if (what == 2) {     // a collective reads the range on the device
             M::flush(off, n);
             for (size_t i = off; i < off + n; i += 1 + rng() % 983) CHECK(g_dev[i] == truth[i]);
+        } else if (what == 4) {     // a blocking call on small operands (the light path)
+            const size_t m = 1 + rng() % 4096;
+            const size_t so = rng() % (bytes - m), to = rng() % (bytes - m);
+            M::flush_bytes(so, m);
+            for (size_t i = so; i < so + m; i += 1 + rng() % 97) CHECK(g_dev[i] == truth[i]);
+            if (M::begin_light_write(to, m)) {
+                const bool copied = rng() % 2;
+                for (size_t i = to; i < to + m; ++i) {
+                    g_dev[i] = (unsigned char)(i * 7 + it);
+                    if (copied) M::alias_base()[i] = (char)g_dev[i];   // the call's stream
+                    truth[i] = g_dev[i];
+                }
+                M::end_light_write(to, m, copied);
+            } else {                // a block is DEVICE_NEWER: the ordinary marking
+                M::begin_device_write(to, m);
+                for (size_t i = to; i < to + m; ++i) {
+                    g_dev[i] = (unsigned char)(i * 7 + it);
+                    truth[i] = g_dev[i];
+                }
+                M::end_device_write(to, m);
+            }
         } else {                    // a collective writes the range on the device
             M::flush(off, n);
             // the device holds the whole blocks' truth after the flush
