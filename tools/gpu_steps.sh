@@ -15,6 +15,7 @@
 #   soak           the randomized multi-PE soak (tests/gpu_ipc_child.py "soak"),
 #                  $SOAK_SEEDS x $SOAK_ITERS draws
 #   isx_mirror     tools/isx_mirror_latency.py with and without the small-result settle
+#   mirror_cost    tools/mirror_cost_probe: page-protection changes and block flushes
 # $TAG names the round's files (default r04).
 #   ceiling        tools/stream_lab: copy / read / fill ceilings beside the fold
 #   write          tools/stream_lab: write-only shapes (what bounds the fold's stores)
@@ -90,6 +91,7 @@ for step in "$@"; do
         SHMEMX_FORCE_COLLECTIVE=1 SHMEMX_MIRROR_SETTLE_KB=0 run 120 $O/isx_mirror_coll_before.json python3 tools/isx_mirror_latency.py 2000
         SHMEMX_FORCE_COLLECTIVE=1 run 120 $O/isx_mirror_coll_after.json python3 tools/isx_mirror_latency.py 2000
         cat $O/isx_mirror_*.json ;;
+    mirror_cost) run 120 $O/mirror_cost.txt ./tools/mirror_cost_probe 2000; cat $O/mirror_cost.txt ;;
     ceiling)
         for nd in 33554432 67108864; do
             run 300 $O/stream_lab_ceiling_$nd.txt ./tools/stream_lab $nd 3 10 ceiling
