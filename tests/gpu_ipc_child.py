@@ -827,6 +827,28 @@ elif scenario == "mirrored":
             fails.append(f"mirrored: write(2) of a fresh {m * 8}-byte {t} result without acquire: {wrote}")
         if st["blocks_settled"] < 1 or st["blocks_fetched"] != 0:
             fails.append(f"mirrored: {m * 8}-byte result not settled by the call: {st}")
+    # the light path (ISx's round: host store, blocking call, host load, with
+    # nreduce = 1): past the first round no page fault, no block marked
+    # device-newer, only the source's own bytes flushed, the result settled
+    # into the view by the call, on every PE
+    s8, t8 = shm.malloc(8), shm.malloc(8)
+    sv, tv = host_view(s8, np.int64, 1), host_view(t8, np.int64, 1)
+    for r in range(21):
+        if r == 1:
+            shm.mirror_stats(reset=True)
+        sv[0] = 1000 * (pe + 1) + r
+        shm.to_all("longlong", "sum", t8, s8, 1, 0, 0, npes)
+        want = sum(1000 * (q + 1) + r for q in range(npes))
+        if int(tv[0]) != want:
+            fails.append(f"mirrored light path round {r}: {int(tv[0])}, want {want}")
+            break
+    st = shm.mirror_stats(reset=True)
+    ncases += 1
+    if (st["write_faults"] or st["read_faults"] or st["blocks_device_newer"] or st["blocks_fetched"]
+            or st["blocks_settled"] < 20 or st["blocks_flushed"] < 20):
+        fails.append(f"mirrored light path: 20 ISx rounds changed block states: {st}")
+    shm.free(t8)
+    shm.free(s8)
     # and read(2) straight into a source: acquired for writing first, then
     # the reduction sees the bytes the system call stored
     m = 50000
