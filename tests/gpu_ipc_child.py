@@ -847,6 +847,18 @@ elif scenario == "mirrored":
     if (st["write_faults"] or st["read_faults"] or st["blocks_device_newer"] or st["blocks_fetched"]
             or st["blocks_settled"] < 20 or st["blocks_flushed"] < 20):
         fails.append(f"mirrored light path: 20 ISx rounds changed block states: {st}")
+    # a light call that fails (this PE outside the set, or a set past npes)
+    # writes nothing: the host's own bytes of the target stay, though its
+    # block was never flushed to HBM
+    sv[0] = 5
+    tv[0] = 1234567 + pe
+    if npes > 1:
+        shm.to_all("longlong", "sum", t8, s8, 1, (pe + 1) % npes, 0, 1)
+    else:
+        shm.to_all("longlong", "sum", t8, s8, 1, 0, 0, 2)
+    ncases += 1
+    if shm.last_error() == 0 or int(tv[0]) != 1234567 + pe:
+        fails.append(f"mirrored light path: a failed call (error {shm.last_error()}) left {int(tv[0])}")
     shm.free(t8)
     shm.free(s8)
     # and read(2) straight into a source: acquired for writing first, then
