@@ -4,8 +4,10 @@ shmem_longlong_sum_to_all(nreduce = 1) (examples/ISx/SHMEM/isx.c:615-624),
 then reads the total with a plain host load.  One PE here (the copy path of
 reduce-op.c:213-216); $SHMEMX_FORCE_COLLECTIVE=1 runs the collective schedule
 instead.  Run with $SHMEMX_MIRROR_SETTLE_KB=0 (the result left DEVICE_NEWER:
-the host load faults and fetches its 64 KiB block) and unset (the call copies
-the 8-byte result back before returning) to see what the settle costs.
+the host load faults and fetches its 64 KiB block) and unset (the light path:
+only the source's 8 written bytes go up, no block changes state or
+protection, and the call's last kernel stores the result into the view as
+well) to see what each costs.
 
     python tools/isx_mirror_latency.py [rounds]
 Prints one JSON line: medians in microseconds of the call alone, the host
