@@ -13,8 +13,11 @@ A "step" is one pass of the hot path over one batch of synthetic input
   the whole 32 Mi-element array, called through the C ABI
   (shmemx_fold_on_stream).  value = nreduce*8 B / step time.
 * N > 1 (configs[2]): the full collective shmemx_double_sum_to_all on all N
-  PEs (one per GPU, RCCL over xGMI), stream-ordered.  value = N * nreduce*8 B
-  / step time (whole job, weak scaling: every PE reduces its own 32 Mi array).
+  PEs (one per GPU, RCCL over xGMI), stream-ordered.  value = algbw =
+  nreduce*8 B / step time, SURVEY.md §8(d) config 3's definition (every PE
+  reduces its own 32 Mi array into one 32 Mi result; weak scaling: the array
+  per PE stays 32 Mi as N grows); aggregate_GiBps = N x that (input bytes of
+  the whole job per second) and roofline.busbw_GBps = algbw x 2(N-1)/N.
 
 Timing: W untimed warm-up steps, then K steps bracketed by a barrier and a
 device synchronize on both sides; the max over ranks is reported.  The
@@ -72,29 +75,43 @@ def parse():
                     help="seconds the extras may take before the line is printed without the rest")
     ap.add_argument("--extras-only", default="",
                     help="comma-separated names of the extras to run (default: all)")
+    ap.add_argument("--corrupt-guard-test", action="store_true",
+                    help="tests only: corrupt one element of rank 0's target before the N > 1 "
+                         "correctness guard, which must then report correct false")
     ap.add_argument("--extras-max-nreduce", type=int, default=256 * 1024 * 1024,
                     help="cap on the extras' array sizes (elements; the tests' short N > 1 runs "
                          "lower it; the driver's runs keep the full BASELINE.json sizes)")
     return ap.parse_args()
 
 
-def pmc_traffic(kernel_key: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any
-    (profiles/*pmc*.json, newest round first, written by tools/summarize_prof.py)."""
-    pdir = os.path.join(REPO, "profiles")
+def pmc_traffic(kernel_key: str, pdir: str | None = None, code_sha: str | None = None):
+    """(HBM bytes per launch, note) from the newest committed rocprofv3 PMC
+    summary (profiles/r*_pmc.json, written by tools/summarize_prof.py), but
+    only if it was measured on the device code this run loaded (its
+    library.device_code_sha256 = the sha256 of the loaded library's
+    .hip_fatbin): a kernel change without a fresh counter pass reports
+    traffic None and says why."""
+    pdir = pdir or os.path.join(REPO, "profiles")
+    code_sha = code_sha or shm.device_code_sha256()
     if not os.path.isdir(pdir):
-        return None
+        return None, "no profiles/ directory"
     for name in sorted(os.listdir(pdir), reverse=True):
-        if "pmc" in name and name.endswith(".json"):
-            try:
-                with open(os.path.join(pdir, name)) as f:
-                    d = json.load(f)
-                v = d.get(kernel_key, {}).get("hbm_bytes_per_launch")
-                if v:
-                    return float(v)
-            except (OSError, ValueError):
-                continue
-    return None
+        if not (name.startswith("r") and name.endswith("_pmc.json")):
+            continue
+        try:
+            with open(os.path.join(pdir, name)) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        v = d.get(kernel_key, {}).get("hbm_bytes_per_launch")
+        if not v:
+            continue
+        measured = (d.get("library") or {}).get("device_code_sha256")
+        if not measured or measured != code_sha:
+            return None, (f"profiles/{name} was measured on other device code (sha256 {str(measured)[:16]}, "
+                          f"loaded {str(code_sha)[:16]}): rerun the pmc step (tools/gpu_steps.sh pmc)")
+        return float(v), f"profiles/{name}: FETCH_SIZE / WRITE_SIZE passes on this device code"
+    return None, "no PMC summary with this kernel under profiles/"
 
 
 def cpu_model() -> str:
@@ -135,8 +152,8 @@ def cpu_baseline(n: int, reps: int, world: int = 1):
     * world > 1: the whole shmem_double_sum_to_all of the line's config on
       `world` PEs = `world` forked processes over shared memory (the GASNet
       smp model, oshrun.in:97-98), pinned to `world` consecutive cores, the
-      reference's peer loop (reduce-op.c:213-250); world*n*8/t like the GPU
-      value (whole job), t = PE 0's time per call.
+      reference's peer loop (reduce-op.c:213-250); value = algbw n*8/t like
+      the GPU value (aggregate_GiBps = world x that), t = PE 0's time per call.
     Median of `reps` warm calls, with min / max and the wall time."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle  # cpu_baseline leg only
@@ -156,7 +173,8 @@ def cpu_baseline(n: int, reps: int, world: int = 1):
     wall = time.perf_counter() - t0
     med = statistics.median(times)
     cpus = (str(base) if world == 1 else f"{base}-{base + world - 1}") if base >= 0 else "unpinned"
-    return {"value": round(world * n * 8 / med / GiB, 4), "unit": "GiB/s", "cores": world,
+    return {"value": round(n * 8 / med / GiB, 4), "unit": "GiB/s", "cores": world,
+            "aggregate_GiBps": round(world * n * 8 / med / GiB, 4),
             "kind": "port",
             "sample": f"oracle restatement of reduce-op.c (gcc -O2, faster than the reference's default "
                       f"-std=c99 without -O): {what}, pinned to CPU {cpus} (the last of the job's "
@@ -738,7 +756,7 @@ def exact_target_ok(ht, base, n, members):
 # PE; DIRECT takes any operand and runs the same fused launches on heap ones).
 AUTO_BUCKETS = {"8B": 1, "4KiB": 1 << 9, "512KiB": 1 << 16, "4MiB": 1 << 19, "128MiB": 1 << 24}
 AUTO_TABLE_ALGOS = {"full": ("allreduce", "rccl", "a2a", "direct", "gather"),
-                    "partial": ("a2a", "direct", "gather")}
+                    "partial": ("allreduce", "rccl", "a2a", "direct", "gather")}
 
 
 def crossover_extra(world, rank, sp, stream, barrier, max_over_ranks, cap=1 << 24, out=None):
@@ -820,8 +838,10 @@ def subset_extra(world, rank, sp, stream, barrier, max_over_ranks, cap=1 << 24, 
     (PE_start 0, stride 1) and every other PE (PE_start 0, logPE_stride 1),
     heap operands, per algorithm, microseconds per call (max over ranks;
     non-members skip the call, as OpenSHMEM's do) and whether every member's
-    target was exact.  `auto` sends these through grouped-p2p A2A on the RCCL
-    transport by default; this is the data to revisit it (auto_recommendation).
+    target was exact.  `auto` sends the RCCL-native pairs on these sets
+    through RCCL on the set's members-only communicator (set_comm.cpp; the
+    first call builds it, so the warm-up calls absorb that); the table is the
+    data to revisit it (auto_recommendation).
     `out` (if given) is filled cell by cell, as in crossover_extra."""
     if world < 4:
         return "needs N >= 4"
@@ -840,7 +860,7 @@ def subset_extra(world, rank, sp, stream, barrier, max_over_ranks, cap=1 << 24, 
             table, table_ok = {}, {}
             out[f"{name}_us_per_call"] = table
             out[f"{name}_correct"] = table_ok
-            for algo in ("a2a", "direct", "signal", "gather"):
+            for algo in ("rccl", "allreduce", "a2a", "direct", "signal", "gather"):
                 row, row_ok = {}, {}
                 table[algo] = row
                 table_ok[algo] = row_ok
@@ -1131,7 +1151,10 @@ def main():
     wall = max_over_ranks(wall)
     ev = max_over_ranks(ev)
     ms_per_step = wall / a.steps * 1e3
-    value = world * nbytes * a.steps / wall / GiB
+    # algbw: one PE's array per call time, at every N
+    value = nbytes * a.steps / wall / GiB
+    aggregate = world * value
+    guard = None
 
     # correctness guard on what was timed
     if world == 1:
@@ -1144,35 +1167,62 @@ def main():
         shm.memcpy(got, chk, nbytes)
         ok = torch.equal(got, src + inp_t)
     else:
-        def sum_guard():
-            """The timed target against the sum of every PE's source on 4096
-            sampled elements (the stated ULP bound), and identical on every
-            PE (checksum of the whole target, compared across the set)."""
+        def sum_guard(record=None):
+            """The timed target against the reference's result on EVERY
+            element: each PE regenerates all N sources on its own GPU from
+            their seeds (0x5EED0000 + rank, the generator is deterministic on
+            one device type), folds them left to right in PE_start order in
+            fp64 (reduce-op.c:219-248; the oracle's order) and holds the target
+            to the stated bound |d| <= 2 gamma(N-1) sum_p |x_p|; NaN anywhere
+            fails.  And identical on every PE (checksum of the whole target,
+            compared across the set).  record: filled with what was checked."""
             if use_heap:
                 shm.memcpy(tgt, tgt_a, nbytes)
-            sample = torch.arange(0, n, max(1, n // 4096), device="cuda")
-            mine = src[sample].cpu()
-            allv = [torch.empty_like(mine) for _ in range(world)]
-            dist.all_gather(allv, mine)
-            ref = allv[0].clone()
-            abs_sum = allv[0].abs().clone()
-            for p in range(1, world):
-                ref += allv[p]
-                abs_sum += allv[p].abs()
-            got = tgt[sample].cpu()
-            tol = 2 * (world - 1) * 2.0 ** -53 * abs_sum
-            good = bool(((got - ref).abs() <= tol).all())
-            good = shm.verify("double", tgt, n, 0, 0, world) and good
+            torch.cuda.synchronize()
+            if a.corrupt_guard_test and rank == 0:
+                # the guard's negative control (tests only): one element off
+                # by far more than the bound
+                tgt[n // 2] += 1e-6
+            gen = torch.Generator(device="cuda")
+            ref = abs_sum = None
+            for p in range(world):
+                gen.manual_seed(0x5EED0000 + p)
+                x = torch.rand(n, dtype=torch.float64, device="cuda", generator=gen) + 1.0
+                if ref is None:
+                    ref, abs_sum = x.clone(), x.abs()
+                else:
+                    ref.add_(x)
+                    abs_sum.add_(x.abs())
+                del x
+            u = 2.0 ** -53
+            k = world - 1
+            bound = abs_sum.mul_(2 * k * u / (1 - k * u) * (1 + 2 * world * u))
+            err = (tgt - ref).abs_()
+            bad = int((~(err <= bound)).sum().item())            # NaN counts as bad
+            inexact = int((tgt.view(torch.int64) != ref.view(torch.int64)).sum().item())
+            worst = float((err / bound.clamp_min(1e-300)).max().item())
+            same = shm.verify("double", tgt, n, 0, 0, world)
+            del ref, bound, err
+            good = bad == 0 and same
+            if record is not None:
+                record.update({"elements_checked": n, "elements_out_of_bound": int(max_over_ranks(bad)),
+                               "elements_not_bit_equal_to_pe_order": int(max_over_ranks(inexact)),
+                               "max_err_over_bound": round(max_over_ranks(worst), 4),
+                               "same_on_every_pe": max_over_ranks(0.0 if same else 1.0) == 0.0,
+                               "reference": "fp64 left fold of every PE's regenerated source in PE_start "
+                                            "order (reduce-op.c:219-248), bound 2 gamma(N-1) sum|x|"})
             return max_over_ranks(0.0 if good else 1.0) == 0.0
-        ok = sum_guard()
+        guard = {}
+        ok = sum_guard(guard)
 
     if world == 1:
         t_launch = ev / a.steps
         achieved = alg_bytes / t_launch / 1e9
-        traffic = pmc_traffic("fold_double_sum")
+        traffic, traffic_note = pmc_traffic("fold_double_sum")
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
+                    "traffic": traffic, "traffic_note": traffic_note,
+                    "device_code_sha256": shm.device_code_sha256(), "alg_bytes_per_launch": alg_bytes,
                     "avg_launch_us": round(t_launch * 1e6, 2),
                     "kernel": "fold_kernel<double,SUM,2 inputs>"}
         # cross-check of avg_launch_us (HIP events over the timed region): K
@@ -1215,7 +1265,9 @@ def main():
                     "avg_launch_us": round(t_call * 1e6, 2),
                     "busbw_GBps": round(achieved, 1),
                     "peak_basis": XGMI_PEAK_BASIS,
-                    "algbw_GiBps": round(nbytes / t_call / GiB, 2)}
+                    "algbw_GiBps": round(nbytes / t_call / GiB, 2),
+                    "algbw_note": "algbw here from HIP events on the stream; value from the wall clock "
+                                  "around the timed steps (max over ranks)"}
 
     cpu = None
     if rank == 0 and not a.no_cpu_baseline:
@@ -1251,6 +1303,14 @@ def main():
                    "arrays": "symmetric heap (shmem_malloc, HBM)" if use_heap else "hipMalloc (torch)"},
         "roofline": roofline, "cpu_baseline": cpu, "correct": ok, "extras": extras,
     }
+    if world > 1:
+        line["aggregate_GiBps"] = round(aggregate, 2)
+        line["value_definition"] = (
+            "value = algbw = nreduce x 8 B / time per call (SURVEY.md 8(d) config 3), the rate of one PE's "
+            "array; aggregate_GiBps = N x value (every PE's input bytes per second); roofline.busbw_GBps "
+            "= algbw x 2(N-1)/N in GB/s; cpu_baseline.value is algbw the same way.  extras' *_GiBps "
+            "fields at N > 1 are aggregate (N x nreduce x size / t) unless named algbw")
+        line["guard"] = guard
     emitted = threading.Lock()
     exit_code = 0 if ok else 1
 

@@ -304,6 +304,14 @@ int shmemx_gather_on_stream(const void *const *srcs, void *const *dsts,
  * vectors per lane per input of the 2-input fold (2, 4 or 8; default 4). */
 int shmemx_fold_set_tuning(int max_blocks, int nontemporal, int unroll);
 
+/* Register (on != 0) or deregister the symmetric heap's HBM segment with
+ * the library's RCCL communicator (ncclCommRegister), so RCCL may use
+ * collectives' heap operands in place instead of staging them through its
+ * own buffers.  Off by default: the N > 1 bench times the RCCL algorithms
+ * both ways (extras.rccl_registered) before it is adopted.  Every PE should
+ * call it alike.  ENOTSUP without an RCCL communicator or an HBM segment. */
+int shmemx_rccl_register_heap(int on);
+
 /* The kernel clock: with on != 0, every launch of the fold family (the
  * 2-input and P-input folds, the copy of a one-member call, the peers fold,
  * the gather) carries start / stop events of its own dispatch
@@ -315,16 +323,16 @@ int shmemx_fold_set_tuning(int max_blocks, int nontemporal, int unroll);
  * launches past the 4096 that went untimed to *dropped (may be NULL); it
  * returns how many were written and starts over.  Off by default; timing
  * does not change what runs. */
-/* Register (on != 0) or deregister the symmetric heap's HBM segment with
- * the library's RCCL communicator (ncclCommRegister), so RCCL may use
- * collectives' heap operands in place instead of staging them through its
- * own buffers.  Off by default: the N > 1 bench times the RCCL algorithms
- * both ways (extras.rccl_registered) before it is adopted.  Every PE should
- * call it alike.  ENOTSUP without an RCCL communicator or an HBM segment. */
-int shmemx_rccl_register_heap(int on);
-
 int shmemx_kernel_timing(int on);
 int shmemx_kernel_times(double *us, int *kind, int max, unsigned long long *dropped);
+
+/* Members-only RCCL communicators this PE holds for partial active sets
+ * (PE_start, logPE_stride, PE_size other than the whole job): the RCCL
+ * algorithms run on a set's own communicator, made by its members alone at
+ * the set's first RCCL call and cached until shmem_finalize.  Returns how
+ * many exist; $SHMEMX_SET_COMMS=0 (every PE alike) keeps partial sets on the
+ * world communicator's grouped send/recv schedules instead. */
+int shmemx_set_comms(void);
 
 /* Largest DIRECT / SIGNAL two-shot call, in KiB, that runs as one fused
  * launch (default $SHMEMX_FUSED_TWOSHOT_KB, else 4096; 0 = never).  Every

@@ -68,11 +68,19 @@ bool clock_pair(int kind, hipEvent_t *a, hipEvent_t *b) {
         return false;
     }
     if (g_kclock.ev.size() < 2 * (g_kclock.used + 1)) {
-        for (int i = 0; i < 2; ++i) {
-            hipEvent_t e;
-            if (hipEventCreate(&e) != hipSuccess) return false;
-            g_kclock.ev.push_back(e);
+        // both events or neither: ev stays two per pair, kind one per pair
+        hipEvent_t e0, e1;
+        if (hipEventCreate(&e0) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
         }
+        if (hipEventCreate(&e1) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipEventDestroy(e0);
+            return false;
+        }
+        g_kclock.ev.push_back(e0);
+        g_kclock.ev.push_back(e1);
         g_kclock.kind.push_back(0);
     }
     *a = g_kclock.ev[2 * g_kclock.used];

@@ -409,6 +409,10 @@ static std::vector<AutoCut> parse_auto_table(const char *var) {
 // to the built-in rule, so captured calls still plan.  Every PE of a set
 // must capture its calls alike (as for every stream-ordered collective).
 static thread_local bool t_planning_capture = false;
+// Set while reduce_device plans a call on a partial set that is being
+// captured: a set whose RCCL communicator does not exist yet cannot take an
+// RCCL algorithm (creating one is not a stream operation).
+static thread_local bool t_capturing = false;
 
 // The table's algorithm for an array of `bytes` per PE, or AUTO.
 static int auto_table_algo(bool world, long long bytes) {
@@ -439,9 +443,12 @@ int make_plan(int type, int op, int nreduce, int start, int logstride,
     const int sz = (int)type_size(type);
     const long long g = sz >= 16 ? 1 : 16 / sz;  // elements per 16-byte granule
     const bool world = start == 0 && (logstride == 0 || size == 1) && size == npes;
+    // RCCL's own collectives serve the whole job on the world communicator
+    // and a partial set on the set's members-only communicator (set_comm.cpp)
+    const bool set_rccl = world || (set_comms_enabled() && (!t_capturing || set_comm_cached(start, logstride, size)));
+    const bool rccl_ok = set_rccl && rccl_native(type, op) && !g_state.ipc_only;
     if (algo == SHMEMX_ALGO_AUTO && P > 1) {
         const int t = auto_table_algo(world, n * sz);
-        const bool rccl_ok = world && rccl_native(type, op) && !g_state.ipc_only;
         const bool pull_ok = g_state.node_shared && P <= kMaxFoldInputs && !t_planning_capture;
         if (((t == SHMEMX_ALGO_RCCL || t == SHMEMX_ALGO_ALLREDUCE) && rccl_ok) ||
             (t == SHMEMX_ALGO_A2A && !g_state.ipc_only) || (t == SHMEMX_ALGO_DIRECT && pull_ok) ||
@@ -450,14 +457,13 @@ int make_plan(int type, int op, int nreduce, int start, int logstride,
     }
     if (algo == SHMEMX_ALGO_AUTO) {
         if (g_state.ipc_only) algo = SHMEMX_ALGO_DIRECT;
-        else if (!(world && rccl_native(type, op))) algo = SHMEMX_ALGO_A2A;
+        else if (!rccl_ok) algo = SHMEMX_ALGO_A2A;
         // Small arrays are latency-bound: one RCCL all-reduce (one launch,
         // and RCCL's own small-message all-reduce algorithms) instead of
         // reduce-scatter + all-gather (+ a tail all-reduce).
         else algo = n * sz <= allreduce_max_bytes() ? SHMEMX_ALGO_ALLREDUCE : SHMEMX_ALGO_RCCL;
     }
-    if ((algo == SHMEMX_ALGO_RCCL || algo == SHMEMX_ALGO_ALLREDUCE) &&
-        !(world && rccl_native(type, op)))
+    if ((algo == SHMEMX_ALGO_RCCL || algo == SHMEMX_ALGO_ALLREDUCE) && !(set_rccl && rccl_native(type, op)))
         return SHMEMX_ENOTSUP;
     if (g_state.ipc_only && algo != SHMEMX_ALGO_DIRECT && algo != SHMEMX_ALGO_GATHER &&
         algo != SHMEMX_ALGO_SIGNAL)
@@ -593,10 +599,14 @@ int reduce_device(int type, int op, void *target, const void *source,
                          int nreduce, int start, int logstride, int size,
                          int algo, hipStream_t s) {
     shmemx_plan_t p;
-    t_planning_capture = algo == SHMEMX_ALGO_AUTO && stream_capturing(s);
+    const bool partial = !(start == 0 && (logstride == 0 || size == 1) && size == g_state.npes);
+    const bool capturing = (algo == SHMEMX_ALGO_AUTO || partial) && stream_capturing(s);
+    t_planning_capture = algo == SHMEMX_ALGO_AUTO && capturing;
+    t_capturing = capturing;
     int rc = make_plan(type, op, nreduce, start, logstride, size, g_state.pe,
                        g_state.npes, algo, &p);
     t_planning_capture = false;
+    t_capturing = false;
     if (rc) return set_error(rc);
     if (nreduce == 0) return SHMEMX_OK;
     const bool collective = size > 1 || g_state.force_collective;
@@ -664,24 +674,26 @@ static int reduce_exchange(int type, int op, char *tgt, const char *src, int nre
     }
     auto peer = [&](int i) { return start + i * step; };
 
-    if (p.algo == SHMEMX_ALGO_ALLREDUCE) {  // one RCCL all-reduce, in place allowed
-        ncclDataType_t dt;
-        rccl_dtype(type, &dt);
-        SHMX_NCCL(ncclAllReduce(src, tgt, (size_t)nreduce, dt, rccl_op(op), g_state.comm, s));
-        return SHMEMX_OK;
-    }
-    if (p.algo == SHMEMX_ALGO_RCCL) {
+    if (p.algo == SHMEMX_ALGO_ALLREDUCE || p.algo == SHMEMX_ALGO_RCCL) {
+        // the whole job: the world communicator; a partial set: its own
+        // members-only communicator, rank = index in the set
+        const bool world = start == 0 && (step == 1 || P == 1) && P == g_state.npes;
+        ncclComm_t comm = world ? g_state.comm : set_comm(start, logstride, P, m, s);
         ncclDataType_t dt;
         rccl_dtype(type, &dt);
         const ncclRedOp_t rop = rccl_op(op);
+        if (p.algo == SHMEMX_ALGO_ALLREDUCE) {  // one RCCL all-reduce, in place allowed
+            SHMX_NCCL(ncclAllReduce(src, tgt, (size_t)nreduce, dt, rop, comm, s));
+            return SHMEMX_OK;
+        }
         if (p.chunk > 0) {
             char *mine = tgt + (size_t)m * (size_t)p.chunk * sz;
-            SHMX_NCCL(ncclReduceScatter(src, mine, (size_t)p.chunk, dt, rop, g_state.comm, s));
-            SHMX_NCCL(ncclAllGather(mine, tgt, (size_t)p.chunk, dt, g_state.comm, s));
+            SHMX_NCCL(ncclReduceScatter(src, mine, (size_t)p.chunk, dt, rop, comm, s));
+            SHMX_NCCL(ncclAllGather(mine, tgt, (size_t)p.chunk, dt, comm, s));
         }
         if (p.tail > 0) {
             const size_t off = (size_t)p.main * sz;
-            SHMX_NCCL(ncclAllReduce(src + off, tgt + off, (size_t)p.tail, dt, rop, g_state.comm, s));
+            SHMX_NCCL(ncclAllReduce(src + off, tgt + off, (size_t)p.tail, dt, rop, comm, s));
         }
         return SHMEMX_OK;
     }
@@ -857,6 +869,8 @@ void pshmem_finalize(void) {
     if (node::up()) node::barrier(0, 1, g_state.npes);
     if (g_state.comm && g_state.rccl_reg) (void)ncclCommDeregister(g_state.comm, g_state.rccl_reg);
     g_state.rccl_reg = nullptr;
+    g_state.rccl_reg_refused = false;
+    set_comms_release();
     heap::release_all();
     direct_release();
     node::detach(g_state.pe == 0);
@@ -1114,13 +1128,34 @@ int shmemx_rccl_register_heap(int on) {
     if (int rc = ensure_init()) return rc;
     if (!g_state.comm) return set_error(SHMEMX_ENOTSUP);
     if (on && !g_state.rccl_reg) {
+        // once per segment: a refusal is remembered (the next shmem_malloc
+        // does not try again), and the PEs agree, so all register or none
+        if (g_state.rccl_reg_refused) return set_error(SHMEMX_ENOTSUP);
         void *base = nullptr;
         size_t bytes = 0;
-        if (!heap::segment(&base, &bytes)) return set_error(SHMEMX_ENOTSUP);
+        const bool have = heap::segment(&base, &bytes);
         SHMX_HIP(hipStreamSynchronize(g_state.stream));
-        if (ncclCommRegister(g_state.comm, base, bytes, &g_state.rccl_reg) != ncclSuccess) {
+        if (have && ncclCommRegister(g_state.comm, base, bytes, &g_state.rccl_reg) != ncclSuccess) {
             g_state.rccl_reg = nullptr;
             trace(LOG_INFO, "ncclCommRegister of the heap segment (%zu bytes) failed", bytes);
+        }
+        bool all = g_state.rccl_reg != nullptr;
+        if (g_state.npes > 1) {
+            int *flag = static_cast<int *>(grow(g_state.token, g_state.token_bytes, 64));
+            if (!flag) fatal("shmemx_rccl_register_heap", "no device memory for the agreement");
+            const int mine = all ? 1 : 0;
+            int every = 0;
+            SHMX_HIP(hipMemcpyAsync(flag, &mine, sizeof mine, hipMemcpyHostToDevice, g_state.stream));
+            SHMX_NCCL(ncclAllReduce(flag, flag, 1, ncclInt32, ncclMin, g_state.comm, g_state.stream));
+            SHMX_HIP(hipMemcpyAsync(&every, flag, sizeof every, hipMemcpyDeviceToHost, g_state.stream));
+            SHMX_HIP(hipStreamSynchronize(g_state.stream));
+            all = every != 0;
+        }
+        if (!all) {
+            if (g_state.rccl_reg) (void)ncclCommDeregister(g_state.comm, g_state.rccl_reg);
+            g_state.rccl_reg = nullptr;
+            g_state.rccl_reg_refused = true;
+            trace(LOG_INFO, "heap segment not registered with RCCL (refused on some PE)");
             return set_error(SHMEMX_ENOTSUP);
         }
         trace(LOG_INFO, "heap segment %p (%zu bytes) registered with the RCCL communicator", base, bytes);
@@ -1130,6 +1165,11 @@ int shmemx_rccl_register_heap(int on) {
         g_state.rccl_reg = nullptr;
     }
     return SHMEMX_OK;
+}
+
+int shmemx_set_comms(void) {
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
+    return set_comms_cached();
 }
 
 int shmemx_kernel_timing(int on) { return kernel_timing(on); }

@@ -239,6 +239,12 @@ void reduce_blocking(int type, int op, void *target, const void *source,
             // host-written target block is not flushed there), so nothing is
             // copied back
             const bool failed = shmemx_reduce_last_error() != SHMEMX_OK;
+            // A call that failed before its own work (a bad set, a call-count
+            // mismatch) never waited for the library stream, where the flush
+            // of the host's bytes (SameStreamFlush) may still be in flight:
+            // settle()'s copy-back, and the next call on another stream, must
+            // not read HBM before it has landed
+            if (failed) SHMX_HIP(hipStreamSynchronize(g_state.stream));
             t.settle(mirror_settle_limit(), copied || (failed && t.light()));
             return;
         }

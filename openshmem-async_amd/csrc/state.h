@@ -35,6 +35,8 @@ struct State {
     // the heap segment registered with the RCCL communicator
     // (shmemx_rccl_register_heap), or nullptr
     void *rccl_reg = nullptr;
+    // a registration was refused (on any PE; agreed): not tried again
+    bool rccl_reg_refused = false;
     // test hook ($SHMEMX_FORCE_COLLECTIVE=1): a 1-PE job still builds an RCCL
     // communicator and runs the collective schedules, so a one-GPU box can
     // execute every RCCL call of the path
@@ -99,6 +101,15 @@ void trace(int level, const char *fmt, ...);
     } while (0)
 
 int ensure_init();                  // single-PE auto-init; ENOINIT if npes > 1
+// Members-only RCCL communicators of partial active sets (set_comm.cpp):
+// set_comm returns the set's cached communicator, creating it first (a
+// collective over the set's members alone: `member` is this PE's index in it)
+// if this is the set's first RCCL call.  $SHMEMX_SET_COMMS=0 turns them off.
+bool set_comms_enabled();
+bool set_comm_cached(int start, int logstride, int size);
+int set_comms_cached();
+ncclComm_t set_comm(int start, int logstride, int size, int member, hipStream_t s);
+void set_comms_release();
 // memcpy split over the staging pool's CPU threads (staging.cpp); a caller
 // that finds the pool busy copies alone (the mirrored heap's fault handler
 // uses it too)

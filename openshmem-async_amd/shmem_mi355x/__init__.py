@@ -54,6 +54,35 @@ class Plan(ctypes.Structure):
 _lib = None
 
 
+def device_code_sha256(path: str = LIB_PATH) -> str | None:
+    """sha256 of the library's gfx950 device code (its ELF .hip_fatbin
+    section): what a rocprofv3 counter pass over the kernels measured.  Host
+    code changes leave it alone; any kernel change moves it.  None if the
+    file or the section is missing."""
+    import hashlib
+    import struct
+    try:
+        with open(path, "rb") as f:
+            elf = f.read()
+    except OSError:
+        return None
+    if elf[:4] != b"\x7fELF" or elf[4] != 2:          # ELF64 only
+        return None
+    shoff, = struct.unpack_from("<Q", elf, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", elf, 0x3A)
+
+    def sect(i):
+        name, _, _, _, off, size = struct.unpack_from("<IIQQQQ", elf, shoff + i * shentsize)
+        return name, off, size
+    _, stroff, _ = sect(shstrndx)
+    for i in range(shnum):
+        name, off, size = sect(i)
+        end = elf.index(b"\0", stroff + name)
+        if elf[stroff + name:end] == b".hip_fatbin":
+            return hashlib.sha256(elf[off:off + size]).hexdigest()
+    return None
+
+
 def lib() -> ctypes.CDLL:
     """Load the shared library (once).  Raises if it is missing."""
     global _lib
@@ -99,6 +128,7 @@ def lib() -> ctypes.CDLL:
     L.shmemx_fold_set_tuning.restype = i
     L.shmemx_rccl_register_heap.argtypes = [i]
     L.shmemx_rccl_register_heap.restype = i
+    L.shmemx_set_comms.restype = i
     L.shmemx_kernel_timing.argtypes = [i]
     L.shmemx_kernel_timing.restype = i
     L.shmemx_kernel_times.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int), i,
@@ -329,6 +359,11 @@ def set_fold_tuning(max_blocks: int = 0, nontemporal: int = -1, unroll: int = 4)
 def rccl_register_heap(on: bool) -> None:
     """shmemx_rccl_register_heap: the heap segment (de)registered with RCCL."""
     _check(lib().shmemx_rccl_register_heap(1 if on else 0), "shmemx_rccl_register_heap")
+
+
+def set_comms() -> int:
+    """shmemx_set_comms: members-only RCCL communicators held for partial sets."""
+    return lib().shmemx_set_comms()
 
 
 KERNEL_KINDS = ("fold", "copy", "peers_fold", "gather")

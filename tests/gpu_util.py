@@ -36,6 +36,47 @@ def same_bits(a: np.ndarray, b: np.ndarray) -> bool:
     return a.dtype == b.dtype and a.shape == b.shape and value_bytes(a) == value_bytes(b)
 
 
+def order_bound(got: np.ndarray, want: np.ndarray, member_srcs: np.ndarray, op: str,
+                scale: float = 1.0):
+    """A floating sum / product whose fold order is not the reference's (RCCL's
+    ring or tree) against `want`, the reference's PE_start-order fold
+    (reduce-op.c:219-248), within the bound BASELINE.json's north_star states:
+
+        |got - want| <= 2 gamma(P-1) sum_p |x_p|     (sum)
+        |got - want| <= 2 gamma(P-1) |prod_p x_p|    (prod, + 2(P-1) x the
+                                                      smallest subnormal for
+                                                      gradual underflow)
+
+    gamma(k) = k u / (1 - k u), u = 2^-24 (float) / 2^-53 (double): each order
+    is within gamma(P-1) of the exact value.  NaN must match NaN and an
+    infinity the same infinity.  `scale` multiplies the bound (0: the negative
+    control, only bit-identical elements pass).  Integers, and any other op,
+    are compared bit for bit.  Returns (ok, elements that differ in bits)."""
+    got, want = np.ascontiguousarray(got), np.ascontiguousarray(want)
+    if got.dtype.kind != "f" or op not in ("sum", "prod") or got.dtype == np.longdouble:
+        return same_bits(got, want), 0
+    iv = np.int32 if got.dtype.itemsize == 4 else np.int64
+    inexact = int(np.count_nonzero(got.view(iv) != want.view(iv)))
+    fi = np.finfo(got.dtype)
+    k = len(member_srcs) - 1
+    u = float(fi.eps) / 2
+    gamma = k * u / (1 - k * u)
+    wide = np.float64 if got.dtype == np.float32 else np.longdouble
+    x = np.asarray(member_srcs).astype(wide)
+    if op == "sum":
+        bound = 2 * gamma * np.abs(x).sum(axis=0)
+    else:
+        bound = 2 * gamma * np.abs(np.prod(x, axis=0)) + 2 * k * float(fi.smallest_subnormal)
+    bound = bound * scale
+    g, w = got.astype(wide), want.astype(wide)
+    gn, wn = np.isnan(g), np.isnan(w)
+    fin = np.isfinite(g) & np.isfinite(w)
+    inf = ~fin & ~gn & ~wn
+    ok = (np.array_equal(gn, wn) and bool(np.all(g[inf] == w[inf]))
+          and bool(np.all(np.abs(g[fin] - w[fin]) <= bound[fin])))
+    return ok, inexact
+
+
 def checksum64(a: np.ndarray) -> int:
     """Host twin of shmemx_checksum (openshmem-async_amd/csrc/checksum.hip):
     XOR over the little-endian 8-byte words w_j of the element bytes (long

@@ -15,8 +15,15 @@
 // processes through per-(sender, receiver) mailboxes in one /dev/shm segment
 // per communicator, and copies results back.  Collectives are built from the
 // same point-to-point engine; reductions combine the ranks' data in rank
-// order.  Group calls run at ncclGroupEnd.  Nothing here is fast; it is
-// exact and it deadlocks only where RCCL would.
+// order NOT the reference's: a reduce-scatter folds chunk c in ring order,
+// starting at rank (c + 1) mod n and ending at c, as RCCL's ring reduce-
+// scatter does; an all-reduce splits the array into n chunks and folds chunk
+// j in descending rotation j, j - 1, ..., j + 1 (mod n), yet another order.
+// So a floating sum or product through the RCCL transport differs from the
+// reference's PE_start-order fold in its last bits, as real RCCL's does, and
+// the tests must hold it to the stated bound, not to bit equality.  Group
+// calls run at ncclGroupEnd.  Nothing here is fast; it is exact arithmetic in
+// a fixed order, and it deadlocks only where RCCL would.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -26,6 +33,7 @@
 #include <sys/mman.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdint>
@@ -376,8 +384,18 @@ ncclResult_t ncclAllReduce(const void *send, void *recv, size_t count, ncclDataT
     std::vector<std::vector<char>> out(c->n, to_host(send, b));
     auto in = exchange(c, out, b);
     in[c->rank] = out[c->rank];
-    std::vector<char> acc = in[0];
-    for (int p = 1; p < c->n; ++p) combine(acc.data(), in[p].data(), count, t, op);
+    // chunk j of n (contiguous elements) in descending rotation from j
+    const size_t es = dt_size(t), per = (count + c->n - 1) / c->n;
+    std::vector<char> acc(b);
+    for (int j = 0; j < c->n; ++j) {
+        const size_t lo = std::min(count, j * per), hi = std::min(count, (j + 1) * per);
+        if (hi == lo) continue;
+        std::memcpy(acc.data() + lo * es, in[j].data() + lo * es, (hi - lo) * es);
+        for (int k = 1; k < c->n; ++k) {
+            const int p = ((j - k) % c->n + c->n) % c->n;
+            combine(acc.data() + lo * es, in[p].data() + lo * es, hi - lo, t, op);
+        }
+    }
     to_dev(recv, acc.data(), b);
     return ncclSuccess;
 }
@@ -395,8 +413,9 @@ ncclResult_t ncclReduceScatter(const void *send, void *recv, size_t count, ncclD
     for (int p = 0; p < c->n; ++p) out[p].assign(all.begin() + p * b, all.begin() + (p + 1) * b);
     auto in = exchange(c, out, b);
     in[c->rank] = out[c->rank];
-    std::vector<char> acc = in[0];
-    for (int p = 1; p < c->n; ++p) combine(acc.data(), in[p].data(), count, t, op);
+    // ring order: my chunk starts at rank + 1 and ends with my own
+    std::vector<char> acc = in[(c->rank + 1) % c->n];
+    for (int k = 2; k <= c->n; ++k) combine(acc.data(), in[(c->rank + k) % c->n].data(), count, t, op);
     to_dev(recv, acc.data(), b);
     return ncclSuccess;
 }

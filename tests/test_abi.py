@@ -184,9 +184,14 @@ def test_plan_algorithm_selection(shm):
     for t, o in [("long", "xor"), ("int", "and"), ("double", "min"), ("float", "max"),
                  ("short", "sum"), ("complexd", "prod")]:
         assert P(t, o, 1000, 0, 0, 4, 2, 4).algo == "a2a", (t, o)
-    # strided or partial sets -> A2A, even for RCCL-native pairs
-    assert P("double", "sum", 1000, 0, 1, 4, 2, 8).algo == "a2a"
-    assert P("double", "sum", 1000, 1, 0, 3, 2, 8).algo == "a2a"
+    # strided or partial sets: RCCL on the set's members-only communicator for
+    # the RCCL-native pairs (set_comm.cpp), A2A for the rest
+    assert P("double", "sum", 1000, 0, 1, 4, 2, 8).algo == "allreduce"
+    assert P("double", "sum", 1000, 1, 0, 3, 2, 8).algo == "allreduce"
+    assert P("double", "sum", 1 << 20, 1, 0, 3, 2, 8).algo == "rccl"
+    assert P("double", "sum", 1000, 1, 0, 3, 2, 8, "rccl").algo == "rccl"
+    assert P("long", "xor", 1000, 1, 0, 3, 2, 8).algo == "a2a"
+    assert P("float", "min", 1000, 0, 1, 4, 2, 8).algo == "a2a"
     # explicit choices
     assert P("double", "sum", 1000, 0, 0, 4, 2, 4, "gather").algo == "gather"
     assert P("double", "sum", 1000, 0, 0, 4, 2, 4, "a2a").algo == "a2a"

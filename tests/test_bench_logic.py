@@ -120,7 +120,8 @@ def test_pin_base_takes_the_last_consecutive_cpus(bench, monkeypatch):
 @pytest.mark.parametrize("world", [1, 3])
 def test_cpu_baseline_fields(bench, world):
     """cpu_baseline at N = 1 (the local fold on one core) and N > 1 (the line's
-    config on N PE processes): GiB/s of the whole job, cores = N, the CPUs,
+    config on N PE processes): algbw GiB/s (one PE's array per call time, as
+    the GPU value), the whole job's rate beside it, cores = N, the CPUs,
     min <= median <= max of the timed calls and the wall time."""
     n = 1 << 16
     c = bench.cpu_baseline(n, 3, world)
@@ -128,5 +129,33 @@ def test_cpu_baseline_fields(bench, world):
     assert c["value"] > 0 and c["wall_s"] >= 0
     sp = c["spread"]
     assert sp["calls"] == 3 and sp["min_ms"] <= sp["median_ms"] <= sp["max_ms"]
-    assert abs(c["value"] - world * n * 8 / (sp["median_ms"] * 1e-3) / (1 << 30)) < 0.01 * c["value"] + 1e-3
+    assert abs(c["value"] - n * 8 / (sp["median_ms"] * 1e-3) / (1 << 30)) < 0.01 * c["value"] + 1e-3
+    assert abs(c["aggregate_GiBps"] - world * c["value"]) < 0.01 * c["aggregate_GiBps"] + 1e-3
     assert ("on %d PEs" % world in c["sample"]) == (world > 1)
+
+
+def test_pmc_traffic_tied_to_device_code(bench, tmp_path):
+    """roofline.traffic comes from a committed PMC summary only while the
+    loaded library carries the device code it measured (VERDICT r04 #7)."""
+    import json
+    d = {"fold_double_sum": {"hbm_bytes_per_launch": 805346304.0},
+         "library": {"device_code_sha256": "ab" * 32}}
+    (tmp_path / "r09_pmc.json").write_text(json.dumps(d))
+    v, note = bench.pmc_traffic("fold_double_sum", str(tmp_path), "ab" * 32)
+    assert v == 805346304.0 and "r09_pmc.json" in note
+    v, note = bench.pmc_traffic("fold_double_sum", str(tmp_path), "cd" * 32)
+    assert v is None and "other device code" in note
+    # a summary without the build's hash (rounds before 5) is never trusted
+    del d["library"]
+    (tmp_path / "r09_pmc.json").write_text(json.dumps(d))
+    assert bench.pmc_traffic("fold_double_sum", str(tmp_path), "ab" * 32)[0] is None
+    assert bench.pmc_traffic("fold_double_sum", str(tmp_path / "none"), "ab" * 32)[0] is None
+
+
+def test_device_code_hash_reads_the_fatbin(bench):
+    """The hash is of the library's .hip_fatbin section: stable for the built
+    library, None for a file that is not one."""
+    import shmem_mi355x as shm
+    h = shm.device_code_sha256()
+    assert h and len(h) == 64 and h == shm.device_code_sha256()
+    assert shm.device_code_sha256(__file__) is None

@@ -76,6 +76,14 @@ def test_bench_multi_rank_line(tmp_path, transport, npes):
     line = json.loads(lines[0])
     assert line["correct"] is True
     assert line["n_gpus"] == npes and line["steps"] == 3 and line["value"] > 0
+    # value = algbw; the whole job's rate beside it
+    assert abs(line["aggregate_GiBps"] - npes * line["value"]) <= 0.011 * line["aggregate_GiBps"], line
+    assert "algbw" in line["value_definition"]
+    # the guard checked every element of the timed target against the
+    # regenerated sources' PE_start fold, within the bound
+    g = line["guard"]
+    assert g["elements_checked"] == 1 << 20 and g["elements_out_of_bound"] == 0, g
+    assert g["same_on_every_pe"] is True and g["max_err_over_bound"] <= 1.0, g
     roof = line["roofline"]
     assert roof["bound"] == "xgmi" and "153 GB/s per link in EACH direction" in roof["peak_basis"], roof
     assert roof["peak"] == (npes - 1) * 153.0
@@ -172,3 +180,25 @@ def test_bench_multi_watchdog_cut_keeps_line(tmp_path):
     rec = extras["auto_recommendation"]
     assert isinstance(rec, dict) and "cut short" in rec.get("note", ""), rec
     assert isinstance(rec.get("env"), dict)
+
+
+@pytest.mark.gpu
+def test_bench_multi_guard_catches_a_corrupt_element(tmp_path):
+    """The N > 1 guard's negative control: one element of rank 0's timed
+    target moved by far more than the bound (--corrupt-guard-test) turns the
+    line's correct false and the exit status 1 (2 ranks, IPC transport)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env.update(SHMEMX_SHARE_GPU="1", SHMEMX_BARRIER_TIMEOUT="120", PYTHONUNBUFFERED="1", SHMEMX_TRANSPORT="ipc")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}",
+           os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--nreduce", str(1 << 20), "--extras", "0", "--no-cpu-baseline", "--corrupt-guard-test"]
+    err_path = str(tmp_path / "bench.err")
+    with open(err_path, "w") as err:
+        p = subprocess.run(cmd, env=env, cwd=REPO, stdout=subprocess.PIPE, stderr=err, text=True,
+                           timeout=300, start_new_session=True)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith('{"metric"')]
+    assert len(lines) == 1, f"want one JSON line\n{p.stdout[-2000:]}\n{open(err_path).read()[-2000:]}"
+    line = json.loads(lines[0])
+    assert line["correct"] is False and p.returncode != 0
+    assert line["guard"]["elements_out_of_bound"] >= 1, line["guard"]

@@ -189,7 +189,10 @@ def test_auto_table_from_environment(tmp_path, table):
         expect = [["double", "sum", 16, 0, 0, 4, "allreduce"],
                   ["double", "sum", 1 << 20, 0, 0, 4, "rccl"],
                   ["long", "xor", 4096, 0, 0, 4, "a2a"],
-                  ["double", "sum", 4099, 0, 1, 2, "a2a"]]
+                  # a partial set: RCCL on its members-only communicator
+                  ["double", "sum", 4099, 0, 1, 2, "allreduce"],
+                  ["double", "sum", 1 << 20, 1, 0, 3, "rccl"],
+                  ["long", "xor", 4099, 1, 0, 3, "a2a"]]
     env.update({"SHMEMX_TRANSPORT": "rccl", "FAKE_RCCL": fake, "AUTO_EXPECT": json.dumps(expect)})
     reports = run_pes(tmp_path, 4, "autotable", env, timeout=300)
     for r in reports:
@@ -225,8 +228,10 @@ def test_rccl_transport_with_rccl_double(tmp_path, npes):
     scatter + all-gather + all-reduce tail), ALLREDUCE, A2A and GATHER, heap /
     device / host / in-place / overlapping operands, sizes across the
     all-reduce threshold, and broadcast, [f]collect, barrier and verify over
-    RCCL — all against the oracle, bit for bit (the double reduces in rank
-    order)."""
+    RCCL — all against the oracle: bit for bit, except float sum / prod
+    through RCCL's collectives, which the double folds in ring order (not
+    PE_start's) and which must lie within the stated ULP bound.  Partial sets
+    take RCCL on their members-only communicators."""
     fake = os.path.join(HERE, "native", "libfake_rccl.so")
     assert os.path.exists(fake), "tests/native/libfake_rccl.so not built (make -C tests/native)"
     # at 3 PEs with the heap segment registered with RCCL at its first
@@ -237,6 +242,38 @@ def test_rccl_transport_with_rccl_double(tmp_path, npes):
     for r in reports:
         assert r["ncases"] > 0
         assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
+    if npes >= 3:
+        # the double's order is not PE_start's: some float results differ in bits
+        assert sum(r["rccl_inexact_elements"] for r in reports) > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("npes,scale", [(4, "1"), (8, "1"), (4, "0")])
+def test_rccl_order_within_bound(tmp_path, npes, scale):
+    """Float sum and prod through RCCL's reduce-scatter + all-gather and
+    all-reduce, on the whole job and on every partial set's members-only
+    communicator, with the RCCL test double folding in ring / rotated order
+    (as RCCL does): within |d| <= 2 gamma(P-1) sum|x| (sum) / 2 gamma(P-1)
+    |prod x| (prod) of the reference's PE_start fold (reduce-op.c:219-248),
+    with results that really differ in bits.  scale "0": the negative control
+    (bound 0) must fail on float sums, which proves the bound is what passes
+    them."""
+    fake = os.path.join(HERE, "native", "libfake_rccl.so")
+    env = {"SHMEMX_TRANSPORT": "rccl", "FAKE_RCCL": fake, "RCCL_TOL_SCALE": scale}
+    reports = run_pes(tmp_path, npes, "rccl_order", env, timeout=600)
+    partial = 6 if npes == 8 else 3          # active_sets() with more than one member, minus the world
+    for r in reports:
+        assert r["ncases"] > 0
+        # every partial set this PE belongs to has its own communicator
+        assert r["set_comms"] >= 1 and r["set_comms"] <= partial + 2, r["set_comms"]
+    inexact = sum(r["rccl_inexact_elements"] for r in reports)
+    assert inexact > 0
+    if scale == "0":
+        bad = [f for r in reports for f in r["fails"]]
+        assert any(" sum " in f and ("double" in f or "float" in f) for f in bad), bad[:5]
+    else:
+        for r in reports:
+            assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
 
 
 @pytest.mark.gpu

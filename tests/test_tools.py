@@ -97,5 +97,9 @@ def test_trace_by_grid_splits_sizes(tmp_path):
 def test_bench_reads_traffic_from_the_committed_profile():
     sys.path.insert(0, REPO)
     import bench
-    assert bench.pmc_traffic("fold_double_sum") == 805346304.0
-    assert bench.pmc_traffic("no_such_kernel") is None
+    # the newest committed counter summary was measured on the device code
+    # this tree builds: its traffic is reported, ~1.0x the 768 MiB per launch
+    v, note = bench.pmc_traffic("fold_double_sum")
+    assert v is not None, note
+    assert abs(v / (3 * 8 * 32 * 1024 * 1024) - 1) < 0.01, v
+    assert bench.pmc_traffic("no_such_kernel")[0] is None

@@ -71,6 +71,15 @@ def main():
         summary["fold_double_sum"] = {"hbm_bytes_per_launch": best["hbm_bytes_per_launch"],
                                       "alg_bytes_per_launch": 3 * 8 * 32 * 1024 * 1024,
                                       "kernel": best["name"]}
+    # the build these counters measured: bench.py reports the traffic only
+    # while the library it loads carries the same device code
+    sys.path.insert(0, os.path.join(REPO, "openshmem-async_amd"))
+    import hashlib
+    import shmem_mi355x
+    summary["library"] = {"path": os.path.relpath(shmem_mi355x.LIB_PATH, REPO),
+                          "device_code_sha256": shmem_mi355x.device_code_sha256()}
+    with open(shmem_mi355x.LIB_PATH, "rb") as fh:
+        summary["library"]["file_sha256"] = hashlib.sha256(fh.read()).hexdigest()
     with open(os.path.join(out, f"{tag}_pmc.json"), "w") as fh:
         json.dump(summary, fh, indent=1)
     print(json.dumps(summary, indent=1))
