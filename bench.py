@@ -199,14 +199,15 @@ def cpu_baseline_table(reps: int = 3):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle  # cpu_baseline leg only
     Mi = 1024 * 1024
-    rows = [("int", "sum", 2, 1024, "configs[0]")]
+    rows = [("int", "sum", 2, 1024, "configs[0]"), ("int", "sum", 2, 1, "configs[0] at n = 1"),
+            ("int", "sum", 2, 4096, "configs[0] at n = 4096"), ("longlong", "sum", 1, 1, "ISx's call, 1 PE")]
     rows += [("double", "sum", P, 32 * Mi, "configs[1]" if P == 1 else "configs[2]") for P in (1, 2, 4, 8)]
     rows += [("long", op, 4, 64 * Mi, "configs[3]") for op in ("and", "or", "xor")]
     n = 4 * 1024
     while n <= 16 * Mi:
         rows.append(("float", "sum", 8, n, "configs[4]"))
         n *= 4
-    size = {"int": 4, "double": 8, "long": 8, "float": 4}
+    size = {"int": 4, "double": 8, "long": 8, "float": 4, "longlong": 8}
     out = []
     t0 = time.perf_counter()
     base = pin_base(1)
@@ -450,6 +451,71 @@ def latency_extras(world, barrier, max_over_ranks):
             t = max_over_ranks((time.perf_counter() - t0) / reps)
             out[f"longlong_sum_n{n}_{where}_us"] = round(t * 1e6, 1)
     return out
+
+
+def config0_extra(world, rank, barrier, max_over_ranks, reps=300):
+    """BASELINE.json configs[0] through the product: shmem_int_sum_to_all on
+    2 PEs (PE_start 0, the first two GPUs; the other ranks skip the calls, as
+    OpenSHMEM's non-members do), nreduce 1, 1024 (the config) and 4096,
+    blocking calls from symmetric-heap operands (HBM, what `auto` runs
+    device-resident) and from host arrays (the reference's heap is host
+    memory), microseconds per call: median and min over `reps` calls timed one
+    by one (the slower member's), beside the reference's CPU time for the same
+    call (cpu_baseline.table at N = 1, 4.0-4.6 us at n = 1024).  Every target
+    is checked exactly (integer sums)."""
+    import numpy as np
+    if world < 2:
+        return "needs N >= 2"
+    member = rank < 2
+    psync = np.full(128, -1, dtype=np.int64)
+    out = {}
+    hs, ht = malloc_pair(4096 * 4)
+    try:
+        if not (hs and ht):
+            return "shmem_malloc failed"
+        for n in (1, 1024, 4096):
+            base = np.arange(n, dtype=np.int32) % 977
+            want = base * 2 + 1                        # PE 0: base, PE 1: base + 1
+            mine = base + rank
+            for where in ("heap", "host"):
+                if where == "heap":
+                    shm.memcpy(hs, mine, n * 4)
+                    src, tgt = hs, ht
+                else:
+                    src, tgt = mine.copy(), np.zeros(n, dtype=np.int32)
+                ts, ok = [], True
+                barrier()
+                for k in range(reps + 5):
+                    if member:
+                        t0 = time.perf_counter()
+                        shm.to_all("int", "sum", tgt, src, n, 0, 0, 2, None, psync)
+                        dt = time.perf_counter() - t0
+                        if k >= 5:
+                            ts.append(dt)
+                        ok = ok and shm.last_error() == 0
+                if member:
+                    got = np.empty(n, dtype=np.int32)
+                    if where == "heap":
+                        shm.memcpy(got, ht, n * 4)
+                    else:
+                        got = tgt
+                    ok = ok and bool(np.array_equal(got, want))
+                med = max_over_ranks(statistics.median(ts) if ts else 0.0)
+                lo = max_over_ranks(min(ts) if ts else 0.0)
+                out[f"n{n}_{where}"] = {"median_us": round(med * 1e6, 1), "min_us": round(lo * 1e6, 1),
+                                        "calls": reps,
+                                        "correct": max_over_ranks(0.0 if (ok or not member) else 1.0) == 0.0}
+        algo = shm.plan("int", "sum", 1024, 0, 0, 2, min(rank, 1), world, "auto").algo
+        out["plan_note"] = f"auto's plan for the 2-PE set at n = 1024: {algo}"
+        out["method_note"] = ("shmem_int_sum_to_all on PEs 0-1 (BASELINE configs[0]), blocking, each call timed "
+                              "alone; the reference's CPU time for the same call is cpu_baseline.table's "
+                              "configs[0] rows (N = 1 line)")
+        return out
+    finally:
+        if ht:
+            shm.free(ht)
+        if hs:
+            shm.free(hs)
 
 
 def heap_latency_extras(world, barrier, max_over_ranks):
@@ -1457,6 +1523,7 @@ def main():
         guarded("configs", lambda: config_extras(world, stream, barrier, max_over_ranks,
                                                      a.extras_max_nreduce))
         guarded("latency", lambda: latency_extras(world, barrier, max_over_ranks))
+        guarded("config0", lambda: config0_extra(world, rank, barrier, max_over_ranks))
         guarded("host_resident_e2e", lambda: host_e2e_multi(world, rank, min(n, a.extras_max_nreduce),
                                                             barrier, max_over_ranks))
         # last: the kernels that load from the peers' HBM through IPC mappings

@@ -7,6 +7,7 @@
 // (DESIGN.md §6).  Pageable memory goes through a page-locked ring filled and
 // emptied by a pool of CPU threads.
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <atomic>
@@ -56,6 +57,50 @@ static char *ring_out(size_t slot) {
     return static_cast<char *>(g_state.ring) + (kRingSlots + slot) * g_state.ring_slot;
 }
 
+// A copy whose stores bypass the caches (32-byte non-temporal stores, then a
+// store fence): a destination that is only read again by a DMA engine or,
+// much later, by the program gains nothing from being cached, and the
+// streaming stores skip the read-for-ownership of every destination line that
+// a cached store pays (one memory read fewer per byte).  AVX2 when the CPU
+// has it, memcpy otherwise.
+__attribute__((target("avx2"))) static void nt_copy_avx2(char *dst, const char *src, size_t n) {
+    size_t i = 0;
+    const size_t head = std::min(n, (size_t)((32 - ((uintptr_t)dst & 31)) & 31));
+    if (head) std::memcpy(dst, src, head);
+    i = head;
+    for (; i + 128 <= n; i += 128) {
+        const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(src + i));
+        const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(src + i + 32));
+        const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(src + i + 64));
+        const __m256i d = _mm256_loadu_si256(reinterpret_cast<const __m256i *>(src + i + 96));
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(dst + i), a);
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(dst + i + 32), b);
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(dst + i + 64), c);
+        _mm256_stream_si256(reinterpret_cast<__m256i *>(dst + i + 96), d);
+    }
+    if (i < n) std::memcpy(dst + i, src + i, n - i);
+    _mm_sfence();
+}
+
+static void copy_bytes(char *dst, const char *src, size_t n, bool nt) {
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    if (nt && avx2) nt_copy_avx2(dst, src, n);
+    else std::memcpy(dst, src, n);
+}
+
+// $SHMEMX_COPY_NT: which staging copies of pageable arrays use streaming
+// stores — bit 0 the source into the page-locked ring (read next by the H2D
+// DMA), bit 1 the ring out into the caller's target; default 0 (round 1
+// measured no gain on the box; the r05 sweep, tools/gpu_steps.sh e2e_nt,
+// re-measures it with the copy lab beside it).
+static int copy_nt_mask() {
+    static const int m = [] {
+        const char *e = std::getenv("SHMEMX_COPY_NT");
+        return e && *e ? (std::atoi(e) & 3) : 0;
+    }();
+    return m;
+}
+
 namespace {
 class CopyPool {
   public:
@@ -77,9 +122,9 @@ class CopyPool {
     // memcpy split over the pool; returns when every piece is done.  One
     // caller at a time: a second concurrent caller (the mirrored heap's fault
     // handler on another thread) copies on its own.
-    void copy(void *dst, const void *src, size_t bytes) {
+    void copy(void *dst, const void *src, size_t bytes, bool nt) {
         if (bytes < (size_t(4) << 20) || nthreads_ == 1 || busy_.exchange(true, std::memory_order_acquire)) {
-            std::memcpy(dst, src, bytes);
+            copy_bytes(static_cast<char *>(dst), static_cast<const char *>(src), bytes, nt);
             return;
         }
         {
@@ -87,6 +132,7 @@ class CopyPool {
             dst_ = static_cast<char *>(dst);
             src_ = static_cast<const char *>(src);
             bytes_ = bytes;
+            nt_ = nt;
             pending_ = nthreads_ - 1;
             ++gen_;
         }
@@ -101,7 +147,7 @@ class CopyPool {
     void piece(unsigned i) {
         const size_t per = (bytes_ / nthreads_ + 63) & ~size_t(63);
         const size_t lo = std::min(bytes_, per * i), hi = std::min(bytes_, per * (i + 1));
-        if (hi > lo) std::memcpy(dst_ + lo, src_ + lo, hi - lo);
+        if (hi > lo) copy_bytes(dst_ + lo, src_ + lo, hi - lo, nt_);
     }
     void run(unsigned i) {
         unsigned long long seen = 0;
@@ -130,12 +176,13 @@ class CopyPool {
     char *dst_ = nullptr;
     const char *src_ = nullptr;
     size_t bytes_ = 0;
+    bool nt_ = false;
 };
 }  // namespace
 
-void parallel_copy(void *dst, const void *src, size_t bytes) {
+void parallel_copy(void *dst, const void *src, size_t bytes, bool nt) {
     static CopyPool pool;
-    pool.copy(dst, src, bytes);
+    pool.copy(dst, src, bytes, nt);
 }
 
 // The small-message bounce buffers: fine-grained (coherent) page-locked
@@ -484,7 +531,7 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
         const size_t slot = j % kRingSlots;
         const size_t cnt = std::min(chunk, (size_t)nreduce - j * chunk);
         SHMX_HIP(hipEventSynchronize(ev_out_slot[slot]));
-        parallel_copy(htgt + j * chunk_bytes, ring_out(slot), cnt * sz);
+        parallel_copy(htgt + j * chunk_bytes, ring_out(slot), cnt * sz, copy_nt_mask() & 2);
     };
     int rc = SHMEMX_OK;
     for (size_t k = 0; k < nchunks && !rc; ++k) {
@@ -497,7 +544,7 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
             const char *from = hsrc + off;
             if (in_bounce) {
                 if (k >= kRingSlots) SHMX_HIP(hipEventSynchronize(ev_in_slot[slot]));
-                parallel_copy(ring_in(slot), hsrc + off, b);
+                parallel_copy(ring_in(slot), hsrc + off, b, copy_nt_mask() & 1);
                 from = ring_in(slot);
             }
             SHMX_HIP(hipMemcpyAsync(ssrc + off, from, b, hipMemcpyHostToDevice, g_state.h2d));

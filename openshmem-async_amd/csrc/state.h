@@ -113,7 +113,8 @@ void set_comms_release();
 // memcpy split over the staging pool's CPU threads (staging.cpp); a caller
 // that finds the pool busy copies alone (the mirrored heap's fault handler
 // uses it too)
-void parallel_copy(void *dst, const void *src, size_t bytes);
+// nt: streaming (non-temporal) stores, for a destination nothing reads soon
+void parallel_copy(void *dst, const void *src, size_t bytes, bool nt = false);
 // The plan of one call (shmemx_reduce_plan) and the device-resident engine
 // (runtime.cpp); the host staging of the blocking entry points (staging.cpp)
 // runs the engine chunk by chunk.

@@ -10,8 +10,10 @@ n = 32 * 1024 * 1024
 src = np.random.default_rng(1).random(n) + 1; tgt = np.zeros(n)
 shm.to_all("double", "sum", tgt, src, n, 0, 0, 1)
 ts = []
-for _ in range(5):
+for _ in range(int(os.environ.get("E2E_REPS", "7"))):
     t0 = time.perf_counter(); shm.to_all("double", "sum", tgt, src, n, 0, 0, 1); ts.append(time.perf_counter() - t0)
 t = statistics.median(ts)
 print(f"threads={os.environ.get('SHMEMX_COPY_THREADS','dflt')} chunkMB={os.environ.get('SHMEMX_STAGE_CHUNK_MB','dflt')} "
-      f"{t*1e3:.2f} ms {n*8/t/2**30:.1f} GiB/s ok={bool((tgt==src).all())}", flush=True)
+      f"nt={os.environ.get('SHMEMX_COPY_NT','dflt')} "
+      f"{t*1e3:.2f} ms {n*8/t/2**30:.1f} GiB/s (min {n*8/max(ts)/2**30:.1f} max {n*8/min(ts)/2**30:.1f}) "
+      f"ok={bool((tgt==src).all())}", flush=True)

@@ -16,7 +16,9 @@
 #                  $SOAK_SEEDS x $SOAK_ITERS draws
 #   isx_mirror     tools/isx_mirror_latency.py with and without the small-result settle
 #   mirror_cost    tools/mirror_cost_probe: page-protection changes and block flushes
-# $TAG names the round's files (default r04).
+# $TAG names the round's files (default r05).
+#   copy_lab       tools/copy_lab: host copies through the staging slot, 4/8/16 threads
+#   e2e_nt         tools/e2e_sweep.py per $E2E_THREADS x $E2E_NT (copy threads, streaming-store mask)
 #   ceiling        tools/stream_lab: copy / read / fill ceilings beside the fold
 #   write          tools/stream_lab: write-only shapes (what bounds the fold's stores)
 #   fold2, copy2, gs  tools/stream_lab: fold / copy shapes the write-only lab suggests
@@ -46,7 +48,7 @@ json_line() {   # json_line <log> <json>: the bench line alone, as a JSON file
 }
 
 BENCH_HEAD="python3 bench.py --steps 20 --warmup 5 --extras 0 --no-cpu-baseline"
-TAG=${TAG:-r04}
+TAG=${TAG:-r05}
 
 for step in "$@"; do
     case $step in
@@ -91,6 +93,13 @@ for step in "$@"; do
         SHMEMX_FORCE_COLLECTIVE=1 SHMEMX_MIRROR_SETTLE_KB=0 run 120 $O/isx_mirror_coll_before.json python3 tools/isx_mirror_latency.py 2000
         SHMEMX_FORCE_COLLECTIVE=1 run 120 $O/isx_mirror_coll_after.json python3 tools/isx_mirror_latency.py 2000
         cat $O/isx_mirror_*.json ;;
+    e2e_nt)   # the pageable host-resident path: copy threads x streaming-store mask
+        for th in ${E2E_THREADS:-8 16}; do for nt in ${E2E_NT:-0 1 2 3}; do
+            SHMEMX_COPY_THREADS=$th SHMEMX_COPY_NT=$nt run 120 $O/e2e_nt_${th}_${nt}.txt python3 tools/e2e_sweep.py
+            cat $O/e2e_nt_${th}_${nt}.txt
+        done; done ;;
+    copy_lab)   # host memcpy vs streaming stores through a 16 MiB slot (no GPU)
+        for t in 4 8 16; do run 120 $O/copy_lab_$t.txt ./tools/copy_lab $t 256 5; cat $O/copy_lab_$t.txt; done ;;
     mirror_cost) run 120 $O/mirror_cost.txt ./tools/mirror_cost_probe 2000; cat $O/mirror_cost.txt ;;
     ceiling)
         for nd in 33554432 67108864; do
