@@ -426,6 +426,31 @@ def config_extras(world, stream, barrier, max_over_ranks, cap=256 * 1024 * 1024)
     return out
 
 
+_CALL_TIMER = None
+
+
+def call_times_us(type_name, op, target, source, n, start, logstride, size, psync, warm, reps):
+    """Per-call microseconds of the blocking shmem_<type>_<op>_to_all, each
+    call timed from C (tools/libcalltimer.so: no Python between calls), or
+    None if the helper is not built."""
+    import ctypes
+    global _CALL_TIMER
+    if _CALL_TIMER is None:
+        path = os.path.join(REPO, "tools", "libcalltimer.so")
+        if not os.path.exists(path):
+            return None
+        L = ctypes.CDLL(path)
+        vp, i = ctypes.c_void_p, ctypes.c_int
+        L.call_timer_to_all.argtypes = [vp, vp, vp, i, i, i, i, vp, vp, i, i, ctypes.POINTER(ctypes.c_double)]
+        L.call_timer_to_all.restype = i
+        _CALL_TIMER = L
+    fn = ctypes.cast(getattr(shm.lib(), f"shmem_{type_name}_{op}_to_all"), ctypes.c_void_p)
+    out = (ctypes.c_double * max(1, reps))()
+    rc = _CALL_TIMER.call_timer_to_all(fn, shm.addr(target), shm.addr(source), n, start, logstride, size,
+                                       None, shm.addr(psync), warm, reps, out)
+    return list(out)[:reps] if rc == 0 else None
+
+
 def latency_extras(world, barrier, max_over_ranks):
     """Small-message latency of the blocking drop-in call (the ISx use:
     shmem_longlong_sum_to_all with nreduce = 1, isx.c:617), host- and
@@ -450,6 +475,15 @@ def latency_extras(world, barrier, max_over_ranks):
                 shm.to_all("longlong", "sum", tgt, src, n, 0, 0, world, None, psync)
             t = max_over_ranks((time.perf_counter() - t0) / reps)
             out[f"longlong_sum_n{n}_{where}_us"] = round(t * 1e6, 1)
+            # the same call from C, each call timed alone (median, min)
+            barrier()
+            ct = call_times_us("longlong", "sum", tgt, src, n, 0, 0, world, psync, 5, reps)
+            if ct:
+                out[f"longlong_sum_n{n}_{where}_from_c_us"] = {
+                    "median": round(max_over_ranks(statistics.median(ct)), 2),
+                    "min": round(max_over_ranks(min(ct)), 2)}
+    out["from_c_note"] = ("*_from_c_us: the same blocking call timed call by call from C "
+                          "(tools/call_timer.c), without the Python caller's overhead")
     return out
 
 
@@ -460,7 +494,8 @@ def config0_extra(world, rank, barrier, max_over_ranks, reps=300):
     blocking calls from symmetric-heap operands (HBM, what `auto` runs
     device-resident) and from host arrays (the reference's heap is host
     memory), microseconds per call: median and min over `reps` calls timed one
-    by one (the slower member's), beside the reference's CPU time for the same
+    by one from C (tools/call_timer.c; the slower member's), beside the
+    reference's CPU time for the same
     call (cpu_baseline.table at N = 1, 4.0-4.6 us at n = 1024).  Every target
     is checked exactly (integer sums)."""
     import numpy as np
@@ -485,14 +520,17 @@ def config0_extra(world, rank, barrier, max_over_ranks, reps=300):
                     src, tgt = mine.copy(), np.zeros(n, dtype=np.int32)
                 ts, ok = [], True
                 barrier()
-                for k in range(reps + 5):
-                    if member:
-                        t0 = time.perf_counter()
-                        shm.to_all("int", "sum", tgt, src, n, 0, 0, 2, None, psync)
-                        dt = time.perf_counter() - t0
-                        if k >= 5:
-                            ts.append(dt)
-                        ok = ok and shm.last_error() == 0
+                if member:
+                    ct = call_times_us("int", "sum", tgt, src, n, 0, 0, 2, psync, 5, reps)
+                    if ct is not None:
+                        ts = [t * 1e-6 for t in ct]
+                    else:
+                        for k in range(reps + 5):
+                            t0 = time.perf_counter()
+                            shm.to_all("int", "sum", tgt, src, n, 0, 0, 2, None, psync)
+                            if k >= 5:
+                                ts.append(time.perf_counter() - t0)
+                    ok = shm.last_error() == 0
                 if member:
                     got = np.empty(n, dtype=np.int32)
                     if where == "heap":

@@ -103,3 +103,23 @@ def test_bench_reads_traffic_from_the_committed_profile():
     assert v is not None, note
     assert abs(v / (3 * 8 * 32 * 1024 * 1024) - 1) < 0.01, v
     assert bench.pmc_traffic("no_such_kernel")[0] is None
+
+
+def test_call_timer_calls_the_entry_point_it_is_given():
+    """tools/libcalltimer.so (bench.py's per-call timer from C) calls the
+    given entry point warm + reps times with the given arguments and times
+    each timed call."""
+    import ctypes
+    import subprocess
+    subprocess.run(["make", "-s", "-C", os.path.join(REPO, "tools"), "libcalltimer.so"], check=True)
+    L = ctypes.CDLL(os.path.join(REPO, "tools", "libcalltimer.so"))
+    vp, i = ctypes.c_void_p, ctypes.c_int
+    L.call_timer_to_all.argtypes = [vp, vp, vp, i, i, i, i, vp, vp, i, i, ctypes.POINTER(ctypes.c_double)]
+    seen = []
+    proto = ctypes.CFUNCTYPE(None, vp, vp, i, i, i, i, vp, vp)
+    cb = proto(lambda t, s, n, a, b, c, w, p: seen.append((t, s, n, a, b, c)))
+    out = (ctypes.c_double * 7)()
+    rc = L.call_timer_to_all(ctypes.cast(cb, vp), 16, 32, 5, 0, 1, 2, None, None, 3, 7, out)
+    assert rc == 0 and len(seen) == 10
+    assert all(x == (16, 32, 5, 0, 1, 2) for x in seen)
+    assert all(v >= 0 for v in out)
