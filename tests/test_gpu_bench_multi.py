@@ -77,7 +77,8 @@ def test_bench_multi_rank_line(tmp_path, transport, npes):
     assert line["correct"] is True
     assert line["n_gpus"] == npes and line["steps"] == 3 and line["value"] > 0
     # value = algbw; the whole job's rate beside it
-    assert abs(line["aggregate_GiBps"] - npes * line["value"]) <= 0.011 * line["aggregate_GiBps"], line
+    # (both rounded to 0.01 in the line)
+    assert abs(line["aggregate_GiBps"] - npes * line["value"]) <= 0.005 * (npes + 1) + 1e-9, line
     assert "algbw" in line["value_definition"]
     # the guard checked every element of the timed target against the
     # regenerated sources' PE_start fold, within the bound
