@@ -185,6 +185,85 @@ void parallel_copy(void *dst, const void *src, size_t bytes, bool nt) {
     pool.copy(dst, src, bytes, nt);
 }
 
+namespace {
+// A gang of CPU threads that runs one copy at a time in the background: the
+// caller starts it and waits for it later, doing other work (enqueueing DMA,
+// starting the other gang's copy) meanwhile.  The pageable staging pipeline
+// has two: one fills the page-locked ring from the caller's source, the other
+// empties it into the caller's target, at the same time (round 5: one pool
+// doing both in turn left each copy waiting for the other).
+class CopyGang {
+  public:
+    explicit CopyGang(unsigned n) : n_(std::max(1u, n)) {
+        for (unsigned i = 0; i < n_; ++i) workers_.emplace_back([this, i] { run(i); });
+    }
+    ~CopyGang() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : workers_) t.join();
+    }
+    void start(void *dst, const void *src, size_t bytes, bool nt) {
+        wait();
+        std::lock_guard<std::mutex> lk(mu_);
+        dst_ = static_cast<char *>(dst);
+        src_ = static_cast<const char *>(src);
+        bytes_ = bytes;
+        nt_ = nt;
+        pending_ = n_;
+        ++gen_;
+        cv_.notify_all();
+    }
+    void wait() {
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [this] { return pending_ == 0; });
+    }
+
+  private:
+    void run(unsigned i) {
+        unsigned long long seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+            }
+            const size_t per = (bytes_ / n_ + 63) & ~size_t(63);
+            const size_t lo = std::min(bytes_, per * i), hi = std::min(bytes_, per * (i + 1));
+            if (hi > lo) copy_bytes(dst_ + lo, src_ + lo, hi - lo, nt_);
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--pending_ == 0) done_.notify_all();
+        }
+    }
+    unsigned n_;
+    std::vector<std::thread> workers_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    bool stop_ = false;
+    unsigned long long gen_ = 0;
+    unsigned pending_ = 0;
+    char *dst_ = nullptr;
+    const char *src_ = nullptr;
+    size_t bytes_ = 0;
+    bool nt_ = false;
+};
+
+// The staging pipeline's two gangs, made on first use: $SHMEMX_COPY_THREADS
+// (default 8) split between them.
+CopyGang &gang(int which) {
+    static unsigned total = [] {
+        unsigned n = 8;
+        if (const char *e = std::getenv("SHMEMX_COPY_THREADS")) n = (unsigned)std::max(2, std::min(64, std::atoi(e)));
+        return n;
+    }();
+    static CopyGang in(total / 2), out(total - total / 2);
+    return which == 0 ? in : out;
+}
+}  // namespace
+
 // The small-message bounce buffers: fine-grained (coherent) page-locked
 // memory, so a kernel that reads or writes them in place sees the host's
 // bytes and the host sees its stores after the stream wait, with no cached
@@ -525,26 +604,42 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
     char *htgt = static_cast<char *>(target);
     char *ssrc = static_cast<char *>(g_state.stage_src);
     char *stgt = static_cast<char *>(g_state.stage_tgt);
-    size_t drained = 0;  // chunks copied out of the ring so far (out_bounce)
-    auto drain_one = [&]() {
-        const size_t j = drained++;
-        const size_t slot = j % kRingSlots;
-        const size_t cnt = std::min(chunk, (size_t)nreduce - j * chunk);
-        SHMX_HIP(hipEventSynchronize(ev_out_slot[slot]));
-        parallel_copy(htgt + j * chunk_bytes, ring_out(slot), cnt * sz, copy_nt_mask() & 2);
+    // Pageable ends run through the ring with two CPU gangs working at once
+    // (bounce in: source -> ring_in[k % kRingSlots], read by the H2D of chunk
+    // k; bounce out: ring_out[k % kRingSlots], written by the D2H of chunk k,
+    // -> target), so the CPU copies in and out overlap each other and the
+    // DMA and the fold of the chunks between them.  Slot reuse: the in-copy
+    // of chunk k waits for the H2D of chunk k - kRingSlots (event), the D2H of
+    // chunk k for the out-copy of chunk k - kRingSlots (host side).
+    const bool nt_in = copy_nt_mask() & 1, nt_out = copy_nt_mask() & 2;
+    auto count_of_chunk = [&](size_t k) { return std::min(chunk, (size_t)nreduce - k * chunk); };
+    auto start_in = [&](size_t k) {
+        const size_t slot = k % kRingSlots;
+        if (k >= kRingSlots) SHMX_HIP(hipEventSynchronize(ev_in_slot[slot]));
+        gang(0).start(ring_in(slot), hsrc + k * chunk_bytes, count_of_chunk(k) * sz, nt_in);
+    };
+    size_t out_started = 0;   // out-copies started; all but the last are complete
+    auto start_out = [&]() {
+        const size_t j = out_started++;
+        SHMX_HIP(hipEventSynchronize(ev_out_slot[j % kRingSlots]));
+        gang(1).start(htgt + j * chunk_bytes, ring_out(j % kRingSlots), count_of_chunk(j) * sz, nt_out);
+    };
+    // the out-copy of chunk j has completed (starting the ones before it)
+    auto out_done = [&](size_t j) {
+        while (out_started <= j) start_out();
+        gang(1).wait();
     };
     int rc = SHMEMX_OK;
+    if (in_bounce && nchunks) start_in(0);
     for (size_t k = 0; k < nchunks && !rc; ++k) {
         const size_t off = k * chunk_bytes;
-        const size_t cnt = std::min(chunk, (size_t)nreduce - k * chunk);
-        const size_t b = cnt * sz;
+        const size_t b = count_of_chunk(k) * sz;
         const size_t slot = k % kRingSlots;
         const void *dsrc = hsrc + off;
         if (!sdev) {
             const char *from = hsrc + off;
             if (in_bounce) {
-                if (k >= kRingSlots) SHMX_HIP(hipEventSynchronize(ev_in_slot[slot]));
-                parallel_copy(ring_in(slot), hsrc + off, b, copy_nt_mask() & 1);
+                gang(0).wait();              // chunk k is in its ring slot
                 from = ring_in(slot);
             }
             SHMX_HIP(hipMemcpyAsync(ssrc + off, from, b, hipMemcpyHostToDevice, g_state.h2d));
@@ -552,26 +647,31 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
             if (in_bounce) SHMX_HIP(hipEventRecord(ev_in_slot[slot], g_state.h2d));
             SHMX_HIP(hipStreamWaitEvent(s, ev_chunk[2 * k], 0));
             dsrc = ssrc + off;
+            if (in_bounce && k + 1 < nchunks) start_in(k + 1);   // runs while this chunk moves
         }
         void *dtgt = tdev ? static_cast<void *>(htgt + off) : static_cast<void *>(stgt + off);
-        rc = reduce_device(type, op, dtgt, dsrc, (int)cnt, start, logstride, size, g_state.algo, s);
+        rc = reduce_device(type, op, dtgt, dsrc, (int)(b / sz), start, logstride, size, g_state.algo, s);
         if (!rc && !tdev) {
             SHMX_HIP(hipEventRecord(ev_chunk[2 * k + 1], s));
             SHMX_HIP(hipStreamWaitEvent(g_state.d2h, ev_chunk[2 * k + 1], 0));
             if (out_bounce) {
-                // the slot's previous chunk must be copied out before reuse
-                while (drained + kRingSlots <= k) drain_one();
+                if (k >= kRingSlots) out_done(k - kRingSlots);   // the slot's previous chunk is out
                 SHMX_HIP(hipMemcpyAsync(ring_out(slot), dtgt, b, hipMemcpyDeviceToHost, g_state.d2h));
                 SHMX_HIP(hipEventRecord(ev_out_slot[slot], g_state.d2h));
-                // keep the CPU busy on the oldest finished chunk, one behind
-                if (k >= 1 && drained < k) drain_one();
+                // keep the out gang on the oldest chunk whose D2H is enqueued
+                // one behind, so this thread is free to enqueue the next one
+                if (k >= 1 && out_started < k) {
+                    gang(1).wait();
+                    start_out();
+                }
             } else {
                 SHMX_HIP(hipMemcpyAsync(htgt + off, dtgt, b, hipMemcpyDeviceToHost, g_state.d2h));
             }
         }
     }
-    if (out_bounce && !rc)
-        while (drained < nchunks) drain_one();
+    if (in_bounce) gang(0).wait();          // no copy still writes the ring
+    if (out_bounce && !rc && nchunks) out_done(nchunks - 1);
+    if (out_bounce) gang(1).wait();
     SHMX_HIP(hipStreamSynchronize(g_state.h2d));
     SHMX_HIP(hipStreamSynchronize(s));
     SHMX_HIP(hipStreamSynchronize(g_state.d2h));
