@@ -147,6 +147,12 @@ def run_case(t, op, n, st, algo, mode, seed, expect_algo=None):
         shm.to_all(t, op, tgt, src, n, *st)
         shm.set_algo("auto")
         got = tgt
+    elif mode == "hostinplace":     # one pageable array, target == source
+        buf = mine.copy()
+        shm.set_algo(algo)
+        shm.to_all(t, op, buf, buf, n, *st)
+        shm.set_algo("auto")
+        got = buf
     elif mode == "hostheap":
         # $SHMEMX_HEAP_MEMORY=host: symmetric objects the host writes directly
         src = host_view(HEAP_SRC, mine.dtype, n)
@@ -305,6 +311,11 @@ if scenario == "full":
     for n in (0, 1, 2, 63, 65, 100003, 1 << 20):
         seed += 1
         run_case("double", "sum", n, (0, 0, npes), "auto", "heap", seed)
+    # pageable host arrays over several 16 MiB staging chunks (the copy gangs
+    # filling and draining the page-locked ring), separate and in place
+    for t, op, mode in (("double", "sum", "host"), ("long", "xor", "hostinplace"), ("int", "max", "host")):
+        seed += 1
+        run_case(t, op, (40 << 20) // oracle.NP_DTYPE[t]().itemsize + 3, (0, 0, npes), "auto", mode, seed)
     # heap operands off 16-B alignment through the fused one- and two-shot
     for t, op in (("double", "sum"), ("short", "max"), ("int", "prod")):
         for n in (1013, 100003):
@@ -470,6 +481,10 @@ elif scenario == "rccl":
         run_case("double", "sum", n, (0, 0, npes), "auto", "device", seed)   # all-reduce, then RS+AG+tail
     seed += 1
     run_case("long", "sum", (6 << 20) + 5, (0, 0, npes), "rccl", "device", seed)
+    # pageable host arrays across staging chunks, separate and in place
+    for t, op, mode in (("double", "sum", "host"), ("long", "xor", "hostinplace")):
+        seed += 1
+        run_case(t, op, (5 << 20) + 3, (0, 0, npes), "auto", mode, seed)
     # A2A with every shard full on the whole job: its all-gather is RCCL's
     # own (in place), not grouped p2p
     for t, op in (("long", "xor"), ("float", "min"), ("short", "and"), ("double", "sum")):
