@@ -17,6 +17,7 @@
 #   isx_mirror     tools/isx_mirror_latency.py with and without the small-result settle
 #   mirror_cost    tools/mirror_cost_probe: page-protection changes and block flushes
 # $TAG names the round's files (default r05).
+#   small_calls    tools/small_call_probe.py plain and under rocprofv3 (1 PE; IPC / RCCL collective schedule forced)
 #   copy_lab       tools/copy_lab: host copies through the staging slot, 4/8/16 threads
 #   e2e_nt         tools/e2e_sweep.py per $E2E_CHUNK x $E2E_THREADS x $E2E_NT (chunk MiB, copy threads, NT mask)
 #   ceiling        tools/stream_lab: copy / read / fill ceilings beside the fold
@@ -99,6 +100,19 @@ for step in "$@"; do
                 python3 tools/e2e_sweep.py
             cat $O/e2e_nt_${ch}_${th}_${nt}.txt
         done; done; done ;;
+    small_calls)   # configs[0]'s call at n 1/1024/4096, heap and host operands, wall (C timer) and kernel time
+        for mode in plain ipc_coll rccl_coll; do
+            envs=""; [ $mode = ipc_coll ] && envs="SHMEMX_TRANSPORT=ipc SHMEMX_FORCE_COLLECTIVE=1"
+            [ $mode = rccl_coll ] && envs="SHMEMX_FORCE_COLLECTIVE=1"
+            env $envs timeout -k 10 120 python3 tools/small_call_probe.py 3000 > $O/small_calls_$mode.json 2>$O/small_calls_$mode.err \
+                || { tail -20 $O/small_calls_$mode.err; exit 1; }
+            cat $O/small_calls_$mode.json
+            ([ -n "$envs" ] && export $envs; run 200 $O/small_calls_${mode}_trace.log rocprofv3 --kernel-trace --stats -d $O/small_calls_${mode}_trace \
+                -o t --output-format csv -- python3 tools/small_call_probe.py 3000)
+            cp $O/small_calls_${mode}_trace/*kernel_stats.csv $O/small_calls_${mode}_kernel_stats.csv 2>/dev/null \
+                || cp $O/small_calls_${mode}_trace/*/*kernel_stats.csv $O/small_calls_${mode}_kernel_stats.csv
+            cut -d, -f1-5 $O/small_calls_${mode}_kernel_stats.csv | cut -c1-220
+        done ;;
     copy_lab)   # host memcpy vs streaming stores through a 16 MiB slot (no GPU)
         for t in 4 8 16; do run 120 $O/copy_lab_$t.txt ./tools/copy_lab $t 256 5; cat $O/copy_lab_$t.txt; done ;;
     mirror_cost) run 120 $O/mirror_cost.txt ./tools/mirror_cost_probe 2000; cat $O/mirror_cost.txt ;;
