@@ -253,7 +253,7 @@ def host_e2e(n: int):
             tgt = torch.zeros(n, dtype=torch.float64).pin_memory()
         shm.to_all("double", "sum", tgt, src, n, 0, 0, 1, None, psync)   # warm-up
         ts = []
-        for _ in range(3):
+        for _ in range(7):
             t0 = time.perf_counter()
             shm.to_all("double", "sum", tgt, src, n, 0, 0, 1, None, psync)
             ts.append(time.perf_counter() - t0)
@@ -263,6 +263,7 @@ def host_e2e(n: int):
             shm.host_unregister(src)
             shm.host_unregister(tgt)
         res[kind] = {"GiBps": round(n * 8 / t / GiB, 2), "ms_per_call": round(t * 1e3, 2),
+                     "GiBps_min_max": [round(n * 8 / max(ts) / GiB, 2), round(n * 8 / min(ts) / GiB, 2)],
                      "correct": ok}
     return res
 
