@@ -8,8 +8,13 @@
 // emptied by a pool of CPU threads.
 #include <hip/hip_runtime.h>
 #include <immintrin.h>
+#include <pthread.h>
+#include <sched.h>
 
 #include <algorithm>
+#include <fstream>
+#include <sstream>
+#include <string>
 #include <atomic>
 #include <condition_variable>
 #include <cstdlib>
@@ -185,6 +190,58 @@ void parallel_copy(void *dst, const void *src, size_t bytes, bool nt) {
     pool.copy(dst, src, bytes, nt);
 }
 
+// The CPUs the staging copy gangs run on ($SHMEMX_COPY_CPUS): "gpu" (the
+// default) = this process's allowed CPUs on the GPU's NUMA node, so the
+// copies into and out of the page-locked ring stay on the socket whose
+// memory controllers and PCIe root the DMA uses; "all" = unpinned; or an
+// explicit list "a-b,c".  An empty result (no NUMA information, no allowed
+// CPU there) leaves the threads unpinned.
+static std::vector<int> parse_cpulist(const std::string &list) {
+    std::vector<int> cpus;
+    std::stringstream ss(list);
+    std::string item;
+    while (std::getline(ss, item, ',')) {
+        if (item.empty()) continue;
+        const size_t dash = item.find('-');
+        const int lo = std::atoi(item.c_str());
+        const int hi = dash == std::string::npos ? lo : std::atoi(item.c_str() + dash + 1);
+        for (int c = lo; c <= hi && c >= 0; ++c) cpus.push_back(c);
+    }
+    return cpus;
+}
+
+static std::vector<int> copy_cpus() {
+    const char *e = std::getenv("SHMEMX_COPY_CPUS");
+    const std::string mode = e && *e ? e : "gpu";
+    if (mode == "all") return {};
+    std::vector<int> want;
+    if (mode == "gpu") {
+        char bus[64] = {0};
+        if (hipDeviceGetPCIBusId(bus, sizeof bus, g_state.device) != hipSuccess) {
+            (void)hipGetLastError();
+            return {};
+        }
+        std::string id(bus);
+        for (auto &c : id) c = (char)std::tolower((unsigned char)c);
+        std::ifstream nf("/sys/bus/pci/devices/" + id + "/numa_node");
+        int node = -1;
+        if (!(nf >> node) || node < 0) return {};
+        std::ifstream cf("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");
+        std::string list;
+        if (!std::getline(cf, list)) return {};
+        want = parse_cpulist(list);
+    } else {
+        want = parse_cpulist(mode);
+    }
+    cpu_set_t allowed;
+    CPU_ZERO(&allowed);
+    if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return {};
+    std::vector<int> out;
+    for (int c : want)
+        if (c < CPU_SETSIZE && CPU_ISSET(c, &allowed)) out.push_back(c);
+    return out;
+}
+
 namespace {
 // A gang of CPU threads that runs one copy at a time in the background: the
 // caller starts it and waits for it later, doing other work (enqueueing DMA,
@@ -194,8 +251,16 @@ namespace {
 // doing both in turn left each copy waiting for the other).
 class CopyGang {
   public:
-    explicit CopyGang(unsigned n) : n_(std::max(1u, n)) {
-        for (unsigned i = 0; i < n_; ++i) workers_.emplace_back([this, i] { run(i); });
+    CopyGang(unsigned n, const std::vector<int> &cpus) : n_(std::max(1u, n)) {
+        for (unsigned i = 0; i < n_; ++i) {
+            workers_.emplace_back([this, i] { run(i); });
+            if (!cpus.empty()) {
+                cpu_set_t set;
+                CPU_ZERO(&set);
+                for (int c : cpus) CPU_SET(c, &set);
+                (void)pthread_setaffinity_np(workers_.back().native_handle(), sizeof set, &set);
+            }
+        }
     }
     ~CopyGang() {
         {
@@ -259,7 +324,16 @@ CopyGang &gang(int which) {
         if (const char *e = std::getenv("SHMEMX_COPY_THREADS")) n = (unsigned)std::max(2, std::min(64, std::atoi(e)));
         return n;
     }();
-    static CopyGang in(total / 2), out(total - total / 2);
+    static const std::vector<int> cpus = [] {
+        std::vector<int> c = copy_cpus();
+        if (log_enabled(LOG_INFO)) {
+            std::string l;
+            for (int x : c) l += std::to_string(x) + " ";
+            trace(LOG_INFO, "staging copy gangs on CPUs: %s", c.empty() ? "(unpinned)" : l.c_str());
+        }
+        return c;
+    }();
+    static CopyGang in(total / 2, cpus), out(total - total / 2, cpus);
     return which == 0 ? in : out;
 }
 }  // namespace

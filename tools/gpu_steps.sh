@@ -18,6 +18,7 @@
 #   mirror_cost    tools/mirror_cost_probe: page-protection changes and block flushes
 # $TAG names the round's files (default r05).
 #   small_calls    tools/small_call_probe.py plain and under rocprofv3 (1 PE; IPC / RCCL collective schedule forced)
+#   e2e_numa       the pageable e2e with the copy gangs pinned to the GPU's NUMA node (gpu) or not (all)
 #   copy_lab       tools/copy_lab: host copies through the staging slot, 4/8/16 threads
 #   e2e_nt         tools/e2e_sweep.py per $E2E_CHUNK x $E2E_THREADS x $E2E_NT (chunk MiB, copy threads, NT mask)
 #   ceiling        tools/stream_lab: copy / read / fill ceilings beside the fold
@@ -113,6 +114,13 @@ for step in "$@"; do
                 || cp $O/small_calls_${mode}_trace/*/*kernel_stats.csv $O/small_calls_${mode}_kernel_stats.csv
             cut -d, -f1-5 $O/small_calls_${mode}_kernel_stats.csv | cut -c1-220
         done ;;
+    e2e_numa)   # the pageable path with the copy gangs pinned to the GPU's NUMA node or not, alternating
+        for f in /sys/devices/system/node/node*/cpulist; do echo "$f: $(cat $f)"; done
+        python3 -c "import ctypes;h=ctypes.CDLL('libamdhip64.so');b=ctypes.create_string_buffer(64);h.hipDeviceGetPCIBusId(b,64,0);import sys;bus=b.value.decode().lower();print('GPU', bus, 'numa_node', open('/sys/bus/pci/devices/'+bus+'/numa_node').read().strip())" || true
+        for rep in 1 2 3; do for cpus in all gpu; do
+            SHMEMX_COPY_CPUS=$cpus run 120 $O/e2e_numa_${cpus}_$rep.txt python3 tools/e2e_sweep.py
+            echo "cpus=$cpus $(grep threads $O/e2e_numa_${cpus}_$rep.txt)"
+        done; done ;;
     copy_lab)   # host memcpy vs streaming stores through a 16 MiB slot (no GPU)
         for t in 4 8 16; do run 120 $O/copy_lab_$t.txt ./tools/copy_lab $t 256 5; cat $O/copy_lab_$t.txt; done ;;
     mirror_cost) run 120 $O/mirror_cost.txt ./tools/mirror_cost_probe 2000; cat $O/mirror_cost.txt ;;
