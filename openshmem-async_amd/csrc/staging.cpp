@@ -10,6 +10,8 @@
 #include <immintrin.h>
 #include <pthread.h>
 #include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <fstream>
@@ -190,12 +192,11 @@ void parallel_copy(void *dst, const void *src, size_t bytes, bool nt) {
     pool.copy(dst, src, bytes, nt);
 }
 
-// The CPUs the staging copy gangs run on ($SHMEMX_COPY_CPUS): "gpu" (the
-// default) = this process's allowed CPUs on the GPU's NUMA node, so the
-// copies into and out of the page-locked ring stay on the socket whose
-// memory controllers and PCIe root the DMA uses; "all" = unpinned; or an
-// explicit list "a-b,c".  An empty result (no NUMA information, no allowed
-// CPU there) leaves the threads unpinned.
+// The CPUs the staging copy gangs run on ($SHMEMX_COPY_CPUS): "all" (the
+// default) = unpinned; "gpu" = this process's allowed CPUs on the GPU's NUMA
+// node; "data" = per call, each gang on the node of the caller's array it
+// reads or writes; or an explicit list "a-b,c".  An empty result (no NUMA
+// information, no allowed CPU there) leaves the threads unpinned.
 static std::vector<int> parse_cpulist(const std::string &list) {
     std::vector<int> cpus;
     std::stringstream ss(list);
@@ -210,10 +211,39 @@ static std::vector<int> parse_cpulist(const std::string &list) {
     return cpus;
 }
 
+static const std::string &copy_cpus_mode() {
+    static const std::string m = [] {
+        const char *e = std::getenv("SHMEMX_COPY_CPUS");
+        return std::string(e && *e ? e : "all");
+    }();
+    return m;
+}
+
+// allowed CPUs of NUMA node `node` (empty if unknown)
+static std::vector<int> node_cpus(int node) {
+    std::ifstream cf("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");
+    std::string list;
+    if (node < 0 || !std::getline(cf, list)) return {};
+    cpu_set_t allowed;
+    CPU_ZERO(&allowed);
+    if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return {};
+    std::vector<int> out;
+    for (int c : parse_cpulist(list))
+        if (c < CPU_SETSIZE && CPU_ISSET(c, &allowed)) out.push_back(c);
+    return out;
+}
+
+// NUMA node of the page holding `p` (move_pages with no target: a query), or -1
+static int page_node(const void *p) {
+    void *page = reinterpret_cast<void *>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(4095));
+    int status = -1;
+    if (syscall(SYS_move_pages, 0, 1UL, &page, nullptr, &status, 0) != 0) return -1;
+    return status >= 0 ? status : -1;
+}
+
 static std::vector<int> copy_cpus() {
-    const char *e = std::getenv("SHMEMX_COPY_CPUS");
-    const std::string mode = e && *e ? e : "gpu";
-    if (mode == "all") return {};
+    const std::string &mode = copy_cpus_mode();
+    if (mode == "all" || mode == "data") return {};
     std::vector<int> want;
     if (mode == "gpu") {
         char bus[64] = {0};
@@ -270,6 +300,16 @@ class CopyGang {
         cv_.notify_all();
         for (auto &t : workers_) t.join();
     }
+    // run the next copies on these CPUs (empty: leave as is)
+    void pin(const std::vector<int> &cpus) {
+        if (cpus.empty() || cpus == pinned_) return;
+        wait();
+        cpu_set_t set;
+        CPU_ZERO(&set);
+        for (int c : cpus) CPU_SET(c, &set);
+        for (auto &t : workers_) (void)pthread_setaffinity_np(t.native_handle(), sizeof set, &set);
+        pinned_ = cpus;
+    }
     void start(void *dst, const void *src, size_t bytes, bool nt) {
         wait();
         std::lock_guard<std::mutex> lk(mu_);
@@ -304,6 +344,7 @@ class CopyGang {
         }
     }
     unsigned n_;
+    std::vector<int> pinned_;
     std::vector<std::thread> workers_;
     std::mutex mu_;
     std::condition_variable cv_, done_;
@@ -686,6 +727,11 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
     // of chunk k waits for the H2D of chunk k - kRingSlots (event), the D2H of
     // chunk k for the out-copy of chunk k - kRingSlots (host side).
     const bool nt_in = copy_nt_mask() & 1, nt_out = copy_nt_mask() & 2;
+    if (copy_cpus_mode() == "data") {
+        // each gang on the NUMA node of the caller's array it touches
+        if (in_bounce) gang(0).pin(node_cpus(page_node(source)));
+        if (out_bounce) gang(1).pin(node_cpus(page_node(target)));
+    }
     auto count_of_chunk = [&](size_t k) { return std::min(chunk, (size_t)nreduce - k * chunk); };
     auto start_in = [&](size_t k) {
         const size_t slot = k % kRingSlots;

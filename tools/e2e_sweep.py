@@ -13,7 +13,17 @@ ts = []
 for _ in range(int(os.environ.get("E2E_REPS", "7"))):
     t0 = time.perf_counter(); shm.to_all("double", "sum", tgt, src, n, 0, 0, 1); ts.append(time.perf_counter() - t0)
 t = statistics.median(ts)
+import ctypes  # noqa: E402
+
+
+def node_of(a):
+    """NUMA node of the array's first page (move_pages query, x86-64 syscall 279)."""
+    libc = ctypes.CDLL(None, use_errno=True)
+    page = ctypes.c_void_p(a.ctypes.data & ~4095)
+    status = ctypes.c_int(-1)
+    libc.syscall(279, 0, ctypes.c_ulong(1), ctypes.byref(page), None, ctypes.byref(status), 0)
+    return status.value
 print(f"threads={os.environ.get('SHMEMX_COPY_THREADS','dflt')} chunkMB={os.environ.get('SHMEMX_STAGE_CHUNK_MB','dflt')} "
-      f"nt={os.environ.get('SHMEMX_COPY_NT','dflt')} "
+      f"nt={os.environ.get('SHMEMX_COPY_NT','dflt')} nodes src {node_of(src)} tgt {node_of(tgt)} cpu {os.sched_getaffinity(0).__len__()} "
       f"{t*1e3:.2f} ms {n*8/t/2**30:.1f} GiB/s (min {n*8/max(ts)/2**30:.1f} max {n*8/min(ts)/2**30:.1f}) "
       f"ok={bool((tgt==src).all())}", flush=True)

@@ -117,7 +117,7 @@ for step in "$@"; do
     e2e_numa)   # the pageable path with the copy gangs pinned to the GPU's NUMA node or not, alternating
         for f in /sys/devices/system/node/node*/cpulist; do echo "$f: $(cat $f)"; done
         python3 -c "import ctypes;h=ctypes.CDLL('libamdhip64.so');b=ctypes.create_string_buffer(64);h.hipDeviceGetPCIBusId(b,64,0);import sys;bus=b.value.decode().lower();print('GPU', bus, 'numa_node', open('/sys/bus/pci/devices/'+bus+'/numa_node').read().strip())" || true
-        for rep in 1 2 3; do for cpus in all gpu; do
+        for rep in 1 2 3; do for cpus in ${E2E_CPUS:-all gpu data}; do
             SHMEMX_COPY_CPUS=$cpus run 120 $O/e2e_numa_${cpus}_$rep.txt python3 tools/e2e_sweep.py
             echo "cpus=$cpus $(grep threads $O/e2e_numa_${cpus}_$rep.txt)"
         done; done ;;
