@@ -885,9 +885,7 @@ void pshmem_finalize(void) {
     }
     g_state.ws_bytes = g_state.tmp_bytes = g_state.stage_bytes = 0;
     g_state.token_bytes = g_state.cws_src_bytes = g_state.cws_tgt_bytes = 0;
-    if (g_state.ring) (void)hipHostFree(g_state.ring);
-    g_state.ring = nullptr;
-    g_state.ring_slot = 0;
+    ring_free();
     if (g_state.bounce) (void)hipHostFree(g_state.bounce);
     g_state.bounce = nullptr;
     g_state.bounce_bytes = 0;

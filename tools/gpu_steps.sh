@@ -117,10 +117,11 @@ for step in "$@"; do
     e2e_numa)   # the pageable path with the copy gangs pinned to the GPU's NUMA node or not, alternating
         for f in /sys/devices/system/node/node*/cpulist; do echo "$f: $(cat $f)"; done
         python3 -c "import ctypes;h=ctypes.CDLL('libamdhip64.so');b=ctypes.create_string_buffer(64);h.hipDeviceGetPCIBusId(b,64,0);import sys;bus=b.value.decode().lower();print('GPU', bus, 'numa_node', open('/sys/bus/pci/devices/'+bus+'/numa_node').read().strip())" || true
-        for rep in 1 2 3; do for cpus in ${E2E_CPUS:-all gpu data}; do
-            SHMEMX_COPY_CPUS=$cpus run 120 $O/e2e_numa_${cpus}_$rep.txt python3 tools/e2e_sweep.py
-            echo "cpus=$cpus $(grep threads $O/e2e_numa_${cpus}_$rep.txt)"
-        done; done ;;
+        cat /sys/kernel/mm/transparent_hugepage/enabled || true
+        for rep in 1 2 3; do for cpus in ${E2E_CPUS:-all gpu data}; do for thp in ${E2E_THP:-0}; do
+            SHMEMX_RING_THP=$thp SHMEMX_COPY_CPUS=$cpus run 120 $O/e2e_numa_${cpus}_${thp}_$rep.txt python3 tools/e2e_sweep.py
+            echo "cpus=$cpus ring_thp=$thp $(grep threads $O/e2e_numa_${cpus}_${thp}_$rep.txt)"
+        done; done; done ;;
     copy_lab)   # host memcpy vs streaming stores through a 16 MiB slot (no GPU)
         for t in 4 8 16; do run 120 $O/copy_lab_$t.txt ./tools/copy_lab $t 256 5; cat $O/copy_lab_$t.txt; done ;;
     mirror_cost) run 120 $O/mirror_cost.txt ./tools/mirror_cost_probe 2000; cat $O/mirror_cost.txt ;;
