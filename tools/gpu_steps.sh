@@ -19,6 +19,7 @@
 # $TAG names the round's files (default r05).
 #   small_calls    tools/small_call_probe.py plain and under rocprofv3 (1 PE; IPC / RCCL collective schedule forced)
 #   e2e_numa       the pageable e2e with the copy gangs pinned to the GPU's NUMA node (gpu) or not (all)
+#   fused_blocks   tools/small_call_probe.py on DIRECT's fused one shot per $SHMEMX_FUSED_BLOCKS
 #   copy_lab       tools/copy_lab: host copies through the staging slot, 4/8/16 threads
 #   e2e_nt         tools/e2e_sweep.py per $E2E_CHUNK x $E2E_THREADS x $E2E_NT (chunk MiB, copy threads, NT mask)
 #   ceiling        tools/stream_lab: copy / read / fill ceilings beside the fold
@@ -113,6 +114,12 @@ for step in "$@"; do
             cp $O/small_calls_${mode}_trace/*kernel_stats.csv $O/small_calls_${mode}_kernel_stats.csv 2>/dev/null \
                 || cp $O/small_calls_${mode}_trace/*/*kernel_stats.csv $O/small_calls_${mode}_kernel_stats.csv
             cut -d, -f1-5 $O/small_calls_${mode}_kernel_stats.csv | cut -c1-220
+        done ;;
+    fused_blocks)   # DIRECT's fused one shot at 1 PE (IPC, collective forced) per grid size
+        for b in ${FB_BLOCKS:-64 32 16 8 64}; do
+            SHMEMX_FUSED_BLOCKS=$b SHMEMX_TRANSPORT=ipc SHMEMX_FORCE_COLLECTIVE=1 run 120 $O/fused_blocks_$b.json \
+                python3 tools/small_call_probe.py 3000
+            echo "blocks $b: $(grep '^{' $O/fused_blocks_$b.json | cut -c1-400)"
         done ;;
     e2e_numa)   # the pageable path with the copy gangs pinned to the GPU's NUMA node or not, alternating
         for f in /sys/devices/system/node/node*/cpulist; do echo "$f: $(cat $f)"; done
