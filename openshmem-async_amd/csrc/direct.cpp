@@ -405,7 +405,7 @@ int direct_fused(int type, int op, char *tgt, size_t n, int start, int step, int
     }
     const double t0 = now_us();
     SHMX_HIP(launch_signal_fold(type, op, fa, s));   // reduce-op.c:217-250
-    if (stage_tgt) SHMX_HIP(hipMemcpyAsync(tgt, scratch_tgt, n * sz, hipMemcpyDeviceToDevice, s));
+    if (stage_tgt) SHMX_HIP(hipMemcpyAsync(tgt, scratch_tgt, n * sz, hipMemcpyDefault, s));
     if (!self_signal) SHMX_HIP(launch_host_signal(sig, s));
     wait_host_signal(sig, s);
     g_phase_us[kFold] += now_us() - t0;
@@ -531,7 +531,7 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     if (!own_order) d.aux = (uint64_t)(oneshot_bytes() >> 10) << 32 | (uint64_t)(fused_twoshot_bytes() >> 10);
     node::put_desc(d);
     if (single && stage_src)
-        SHMX_HIP(hipMemcpyAsync(g_scratch.base, src, bytes, hipMemcpyDeviceToDevice, s));
+        SHMX_HIP(hipMemcpyAsync(g_scratch.base, src, bytes, hipMemcpyDefault, s));
     g_calls += 1;
     std::vector<node::Desc> desc(P);
     auto read_descs = [&] {
@@ -610,7 +610,7 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
             // the staged chunk in; the previous chunk's exit barrier has
             // already seen every member done reading my scratch
             if (stage_src)
-                SHMX_HIP(hipMemcpyAsync(scratch_src, src + c0 * sz, cnt * sz, hipMemcpyDeviceToDevice, s));
+                SHMX_HIP(hipMemcpyAsync(scratch_src, src + c0 * sz, cnt * sz, hipMemcpyDefault, s));
             node_sync(start, step, P, s, &g_phase_us[kEntryWait], &g_phase_us[kEntryBarrier]);
         }
         // a staged operand holds only the current chunk, at its region offset
@@ -630,7 +630,7 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
             // reduce-op.c:250: no member reads my source any more
             node_done(start, step, P, s, &g_phase_us[kFold], &g_phase_us[kExitBarrier], tf);
             if (stage_tgt)
-                SHMX_HIP(hipMemcpyAsync(tgt + c0 * sz, scratch_tgt, cnt * sz, hipMemcpyDeviceToDevice, s));
+                SHMX_HIP(hipMemcpyAsync(tgt + c0 * sz, scratch_tgt, cnt * sz, hipMemcpyDefault, s));
             continue;
         }
         // two shots: slice i of the chunk belongs to member i

@@ -691,17 +691,32 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
         // and the host waits once.
         char *bin = static_cast<char *>(g_state.bounce);
         char *bout = bin + kSmallHostBytes;
+        // DIRECT and own-order GATHER over IPC take the bounce buffers
+        // themselves (page-locked, device-accessible): the source goes
+        // straight into the IPC scratch the peers read, the fold writes the
+        // result into bout over PCIe, and the call returns with its work
+        // done, so the copy kernels on either side and the extra wait go.
+        // RCCL's algorithms need device memory: they keep the staging copies.
+        const bool pulls = collective && (plan.algo == SHMEMX_ALGO_DIRECT ||
+                                          (plan.algo == SHMEMX_ALGO_GATHER && g_state.ipc_only));
         const void *dsrc = source;
         if (!sdev) {
             std::memcpy(bin, source, bytes);
-            const void *in[1] = {bin};
-            fold_chain(type, op, g_state.stage_src, in, 1, (size_t)nreduce, s);
-            dsrc = g_state.stage_src;
+            if (pulls) {
+                dsrc = bin;
+            } else {
+                const void *in[1] = {bin};
+                fold_chain(type, op, g_state.stage_src, in, 1, (size_t)nreduce, s);
+                dsrc = g_state.stage_src;
+            }
         }
-        void *dtgt = tdev ? target : g_state.stage_tgt;
+        void *dtgt = tdev ? target : pulls ? static_cast<void *>(bout) : g_state.stage_tgt;
         const int rc = reduce_device(type, op, dtgt, dsrc, nreduce, start, logstride, size,
                                      g_state.algo, s);
-        if (!rc) {
+        if (!rc && pulls) {
+            // the pulls returned with the result in place (host barriers, or
+            // the fused launch's host signal)
+        } else if (!rc) {
             // the last copy (or a marker) signals the host: no stream wait
             const HostSignal sig = next_host_signal();
             if (!tdev) {
