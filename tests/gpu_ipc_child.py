@@ -501,6 +501,7 @@ elif scenario == "rccl":
                 run_collect(bits, [517] * npes, st, mode, seed)
                 seed += 1
                 run_collect(bits, [(37 * (q + 1)) % 101 for q in range(npes)], st, mode, seed)
+    extra["set_comms"] = shm.set_comms()
     for st in active_sets():
         if member(*st):
             shm.barrier(*st)

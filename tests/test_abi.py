@@ -304,3 +304,20 @@ def test_fused_twoshot_limit_setter(shm):
     with pytest.raises(shm.ShmemError):
         shm.set_fused_twoshot_kb(-1)
     assert shm.set_fused_twoshot_kb(prev) == 16384
+
+
+def test_plan_without_set_comms():
+    """$SHMEMX_SET_COMMS=0 (read once per process, so in a child): partial
+    sets plan A2A for the RCCL-native pairs and refuse an explicit rccl, as
+    before set communicators existed; the whole job is unchanged."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path.insert(0, %r); import shmem_mi355x as shm\n"
+            "assert shm.plan('double', 'sum', 1000, 1, 0, 3, 2, 8).algo == 'a2a'\n"
+            "assert shm.plan('double', 'sum', 1000, 0, 0, 8, 2, 8).algo == 'allreduce'\n"
+            "try:\n    shm.plan('double', 'sum', 1000, 1, 0, 3, 2, 8, 'rccl')\n    raise SystemExit('rccl planned')\n"
+            "except shm.ShmemError as e:\n    assert e.code == 3\n"
+            "print('ok')\n") % os.path.join(os.path.dirname(HEADER), "..", "openshmem-async_amd")
+    out = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, SHMEMX_SET_COMMS="0"),
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and out.stdout.strip() == "ok", out.stdout + out.stderr

@@ -248,6 +248,21 @@ def test_rccl_transport_with_rccl_double(tmp_path, npes):
 
 
 @pytest.mark.gpu
+def test_rccl_transport_without_set_comms(tmp_path):
+    """$SHMEMX_SET_COMMS=0: partial sets keep the grouped send/recv schedules
+    on the world communicator (no set communicator is made, auto takes A2A
+    there, an explicit rccl on a partial set is refused), every case still
+    against the oracle (4 PE processes, RCCL test double)."""
+    fake = os.path.join(HERE, "native", "libfake_rccl.so")
+    reports = run_pes(tmp_path, 4, "rccl", {"SHMEMX_TRANSPORT": "rccl", "FAKE_RCCL": fake,
+                                           "SHMEMX_SET_COMMS": "0"}, timeout=600)
+    for r in reports:
+        assert r["ncases"] > 0
+        assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
+        assert r["set_comms"] == 0, r["set_comms"]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("npes,scale", [(4, "1"), (8, "1"), (4, "0")])
 def test_rccl_order_within_bound(tmp_path, npes, scale):
     """Float sum and prod through RCCL's reduce-scatter + all-gather and
