@@ -445,7 +445,8 @@ int make_plan(int type, int op, int nreduce, int start, int logstride,
     const bool world = start == 0 && (logstride == 0 || size == 1) && size == npes;
     // RCCL's own collectives serve the whole job on the world communicator
     // and a partial set on the set's members-only communicator (set_comm.cpp)
-    const bool set_rccl = world || (set_comms_enabled() && (!t_capturing || set_comm_cached(start, logstride, size)));
+    const bool set_rccl = world || (set_comms_enabled() && !set_comm_refused(start, logstride, size) &&
+                                    (!t_capturing || set_comm_cached(start, logstride, size)));
     const bool rccl_ok = set_rccl && rccl_native(type, op) && !g_state.ipc_only;
     if (algo == SHMEMX_ALGO_AUTO && P > 1) {
         const int t = auto_table_algo(world, n * sz);
@@ -605,6 +606,12 @@ int reduce_device(int type, int op, void *target, const void *source,
     t_capturing = capturing;
     int rc = make_plan(type, op, nreduce, start, logstride, size, g_state.pe,
                        g_state.npes, algo, &p);
+    // a partial set's first RCCL call: its members agree on and make its
+    // communicator; if they refuse (a member's cache is full), all of them
+    // plan again without it (A2A under auto, ENOTSUP for an explicit rccl)
+    if (!rc && partial && size > 1 && (p.algo == SHMEMX_ALGO_RCCL || p.algo == SHMEMX_ALGO_ALLREDUCE) &&
+        !set_comm_cached(start, logstride, size) && !set_comm_prepare(start, logstride, size, p.member, s))
+        rc = make_plan(type, op, nreduce, start, logstride, size, g_state.pe, g_state.npes, algo, &p);
     t_planning_capture = false;
     t_capturing = false;
     if (rc) return set_error(rc);

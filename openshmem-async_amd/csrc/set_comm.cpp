@@ -21,7 +21,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <set>
 #include <tuple>
+#include <vector>
 
 #include "state.h"
 
@@ -34,6 +36,24 @@ using SetKey = std::tuple<int, int, int>;
 std::map<SetKey, ncclComm_t> &cache() {
     static std::map<SetKey, ncclComm_t> c;
     return c;
+}
+
+// sets whose members agreed not to make a communicator (some member's cache
+// was full): they keep the world communicator's schedules
+std::set<SetKey> &refused() {
+    static std::set<SetKey> r;
+    return r;
+}
+
+// $SHMEMX_SET_COMMS_MAX: communicators one PE keeps (default 16; RCCL's
+// buffers cost device memory per communicator)
+size_t cache_cap() {
+    static const size_t cap = [] {
+        const char *e = std::getenv("SHMEMX_SET_COMMS_MAX");
+        const long v = e && *e ? std::atol(e) : 16;
+        return (size_t)(v < 0 ? 0 : v);
+    }();
+    return cap;
 }
 
 // one key per set of PEs: a one-member or a stride-free set has one spelling
@@ -58,6 +78,34 @@ bool set_comm_cached(int start, int logstride, int size) {
 }
 
 int set_comms_cached() { return (int)cache().size(); }
+
+bool set_comm_refused(int start, int logstride, int size) {
+    return refused().count(key_of(start, logstride, size)) != 0;
+}
+
+bool set_comm_prepare(int start, int logstride, int size, int member, hipStream_t s) {
+    const SetKey k = key_of(start, logstride, size);
+    if (cache().count(k)) return true;
+    if (refused().count(k)) return false;
+    // the members agree first (one 8-byte exchange among them): every member
+    // must have room, or none makes the communicator and all plan without it
+    std::vector<unsigned long long> all;
+    const unsigned long long mine = cache().size() < cache_cap() ? 1 : 0;
+    if (exchange_u64(start, logstride, size, mine, all)) {
+        refused().insert(k);   // (a bad set fails alike on every member)
+        return false;
+    }
+    for (unsigned long long v : all) {
+        if (!v) {
+            refused().insert(k);
+            trace(LOG_INFO, "set (%d,%d,%d): a member holds %zu set communicators already "
+                  "($SHMEMX_SET_COMMS_MAX); the set keeps the world communicator", start, logstride, size,
+                  cache_cap());
+            return false;
+        }
+    }
+    return set_comm(start, logstride, size, member, s) != nullptr;
+}
 
 ncclComm_t set_comm(int start, int logstride, int size, int member, hipStream_t s) {
     const SetKey k = key_of(start, logstride, size);
@@ -96,6 +144,7 @@ void set_comms_release() {
     for (auto &kv : cache())
         if (kv.second) (void)ncclCommDestroy(kv.second);
     cache().clear();
+    refused().clear();
 }
 
 }  // namespace shmx

@@ -111,6 +111,11 @@ bool set_comms_enabled();
 bool set_comm_cached(int start, int logstride, int size);
 int set_comms_cached();
 ncclComm_t set_comm(int start, int logstride, int size, int member, hipStream_t s);
+// Before a set's first RCCL call: the members agree (every member has room
+// under $SHMEMX_SET_COMMS_MAX) and make the communicator; false = refused,
+// alike on every member, and remembered (set_comm_refused).
+bool set_comm_prepare(int start, int logstride, int size, int member, hipStream_t s);
+bool set_comm_refused(int start, int logstride, int size);
 void set_comms_release();
 // memcpy split over the staging pool's CPU threads (staging.cpp); a caller
 // that finds the pool busy copies alone (the mirrored heap's fault handler

@@ -538,6 +538,19 @@ elif scenario == "rccl_order":
                 seed += 1
                 run_case("int", "sum", 1000 + rep, st, "auto", "device", seed)
     extra["set_comms"] = shm.set_comms()
+elif scenario == "setcap":
+    # $SHMEMX_SET_COMMS_MAX: a PE keeps at most that many set communicators;
+    # a set whose members do not all have room keeps the world communicator
+    # (auto: A2A), decided alike on every member.  Every partial set, twice,
+    # auto on an RCCL-native pair and a bitwise one, against the oracle.
+    for rep in range(2):
+        for st in active_sets():
+            if st[2] < 2 or st == (0, 0, npes):
+                continue
+            for t, op in (("double", "sum"), ("long", "xor")):
+                seed += 1
+                run_case(t, op, 2053, st, "auto", "device", seed)
+    extra["set_comms"] = shm.set_comms()
 elif scenario == "soak":
     # Random calls, the same sequence on every PE (one seeded generator):
     # type/op pair, size (edges favoured), active set, algorithm and operand

@@ -263,6 +263,25 @@ def test_rccl_transport_without_set_comms(tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cap", ["1", "0"])
+def test_set_comms_cap(tmp_path, cap):
+    """$SHMEMX_SET_COMMS_MAX: no PE holds more set communicators than the cap;
+    a set whose members do not all have room keeps the world communicator
+    (auto plans A2A there), agreed among its members so none waits for a
+    communicator the others are not building; every call against the oracle
+    (4 PE processes, RCCL test double)."""
+    fake = os.path.join(HERE, "native", "libfake_rccl.so")
+    reports = run_pes(tmp_path, 4, "setcap", {"SHMEMX_TRANSPORT": "rccl", "FAKE_RCCL": fake,
+                                             "SHMEMX_SET_COMMS_MAX": cap}, timeout=300)
+    for r in reports:
+        assert r["ncases"] > 0
+        assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
+        assert r["set_comms"] <= int(cap), r["set_comms"]
+    if cap == "1":
+        assert any(r["set_comms"] == 1 for r in reports)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("npes,scale", [(4, "1"), (8, "1"), (4, "0")])
 def test_rccl_order_within_bound(tmp_path, npes, scale):
     """Float sum and prod through RCCL's reduce-scatter + all-gather and
