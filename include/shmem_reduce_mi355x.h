@@ -200,13 +200,15 @@ enum {
 /* Exchange algorithms (DESIGN.md "Multi-GPU").
  *   AUTO    RCCL for what RCCL reduces exactly as specified, A2A otherwise
  *   RCCL    ncclReduceScatter + ncclAllGather (+ ncclAllReduce on the
- *           <P*16-byte tail); full active set, RCCL-native type/op only
+ *           <P*16-byte tail); RCCL-native type/op only; the whole job on the
+ *           world communicator, a partial set on its own members-only
+ *           communicator (made at the set's first RCCL call, cached)
  *   A2A     shard exchange (grouped ncclSend/ncclRecv) -> HIP fold of the P
  *           shards in active-set order -> shard all-gather; any set, any op;
  *           every PE gets the reference's PE_start result bit for bit
  *   GATHER  every PE receives every source and folds in its own reference
  *           order: bit-exact with the reference on EVERY PE, (P-1)x traffic
- *   ALLREDUCE  one ncclAllReduce (full set, RCCL-native pairs, as RCCL)
+ *   ALLREDUCE  one ncclAllReduce (RCCL-native pairs, any set, as RCCL)
  *   DIRECT  one HIP kernel per PE reads slice m of every member's source
  *           straight from the peers' HBM (IPC-mapped symmetric heap, over
  *           xGMI) and folds it in active-set order into its own target; a
