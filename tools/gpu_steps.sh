@@ -32,6 +32,7 @@
 #   rehearse2      bench.py N = 2 on the IPC transport, both ranks on this GPU
 #   rehearse8      the same with 8 ranks
 #   rehearse_rccl  bench.py N = $REH_N (2) on the RCCL transport against the RCCL test double
+#                  (extras capped at $REH_EXTRAS_MAX elements: the double moves every byte through host memory)
 set -u
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -167,7 +168,7 @@ for step in "$@"; do
         np=${REH_N:-2}; q=4; [ "$np" -gt 4 ] && q=2
         GPU_MAX_HW_QUEUES=$q FAKE_RCCL=$PWD/tests/native/libfake_rccl.so SHMEMX_SHARE_GPU=1 run 900 $O/rehearse_rccl_n$np.log \
             python3 -m torch.distributed.run --nnodes=1 --nproc-per-node $np --master-addr 127.0.0.1 \
-            --master-port 29512 bench.py --gpus $np --steps 10 --warmup 3
+            --master-port 29512 bench.py --gpus $np --steps 10 --warmup 3 --extras-max-nreduce ${REH_EXTRAS_MAX:-1048576}
         json_line $O/rehearse_rccl_n$np.log $O/rehearse_rccl_n$np.json ;;
     *) echo "unknown step $step"; exit 2 ;;
     esac
