@@ -270,34 +270,47 @@ def host_e2e(n: int):
 
 def host_e2e_multi(world: int, rank: int, n: int, barrier, max_over_ranks):
     """SURVEY §8(d) "host-resident e2e" for configs[2]: every PE's source and
-    target in page-locked HOST memory (the reference's heap is host memory),
-    the blocking shmem_double_sum_to_all over all N PEs = per PE H2D + the
-    collective + D2H (the pinned pipeline).  The rate is the
-    line's own unit, N * n * 8 B / t with t the slowest PE's call (median of
-    3 warm calls).  Sources are integer-valued doubles, PE r's = (r + 1) *
-    base, so every rounding order gives the exact sum and the check is
-    bit-exact: base * N (N + 1) / 2."""
+    target in HOST memory (the reference's heap is host memory), the blocking
+    shmem_double_sum_to_all over all N PEs = per PE H2D + the collective + D2H:
+    page-locked arrays (the pinned pipeline) and, under
+    "pageable", numpy arrays (the page-locked ring and its copy gangs, every
+    PE's copies sharing the host's memory).  t = the slowest PE's call (median
+    of 3 warm calls); GiBps = N * n * 8 B / t (every PE's input bytes, the
+    extras' aggregate unit), algbw_GiBps = n * 8 B / t.  Sources are
+    integer-valued doubles, PE r's = (r + 1) * base, so every rounding order
+    gives the exact sum and the check is bit-exact: base * N (N + 1) / 2."""
     import numpy as np
     psync = np.full(128, -1, dtype=np.int64)
     base = torch.randint(0, 1 << 20, (n,), dtype=torch.int64,
                          generator=torch.Generator().manual_seed(7)).to(torch.float64)
+    want = base * (world * (world + 1) // 2)
+
+    def run(src, tgt, read):
+        shm.to_all("double", "sum", tgt, src, n, 0, 0, world, None, psync)   # warm-up
+        err = shm.last_error()
+        ts = []
+        for _ in range(3):
+            barrier()
+            t0 = time.perf_counter()
+            shm.to_all("double", "sum", tgt, src, n, 0, 0, world, None, psync)
+            ts.append(max_over_ranks(time.perf_counter() - t0))
+            err = err or shm.last_error()
+        t = statistics.median(ts)
+        ok = err == 0 and bool(torch.equal(read(), want))
+        ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
+        return {"GiBps": round(world * n * 8 / t / GiB, 2), "algbw_GiBps": round(n * 8 / t / GiB, 2),
+                "ms_per_call": round(t * 1e3, 2), "correct": ok, "last_error": err}
+
     src = (base * (rank + 1)).pin_memory()
     tgt = torch.full((n,), float("nan"), dtype=torch.float64).pin_memory()
-    shm.to_all("double", "sum", tgt, src, n, 0, 0, world, None, psync)   # warm-up
-    err = shm.last_error()
-    ts = []
-    for _ in range(3):
-        barrier()
-        t0 = time.perf_counter()
-        shm.to_all("double", "sum", tgt, src, n, 0, 0, world, None, psync)
-        ts.append(max_over_ranks(time.perf_counter() - t0))
-        err = err or shm.last_error()
-    t = statistics.median(ts)
-    ok = err == 0 and bool(torch.equal(tgt, base * (world * (world + 1) // 2)))
-    ok = max_over_ranks(0.0 if ok else 1.0) == 0.0
-    return {"GiBps": round(world * n * 8 / t / GiB, 2), "ms_per_call": round(t * 1e3, 2),
-            "nreduce": n, "buffers_note": "page-locked host memory (torch pin_memory) on every PE",
-            "correct": ok, "last_error": err}
+    out = run(src, tgt, lambda: tgt)
+    out.update(nreduce=n, buffers_note="page-locked host memory (torch pin_memory) on every PE")
+    del src, tgt
+    psrc = (base * (rank + 1)).numpy().copy()
+    ptgt = np.full(n, np.nan)
+    out["pageable"] = run(psrc, ptgt, lambda: torch.from_numpy(ptgt))
+    out["pageable_note"] = "numpy (pageable) arrays on every PE: the page-locked ring and its two copy gangs"
+    return out
 
 
 def config_extras(world, stream, barrier, max_over_ranks, cap=256 * 1024 * 1024):

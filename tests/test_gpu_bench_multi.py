@@ -121,6 +121,7 @@ def test_bench_multi_rank_line(tmp_path, transport, npes):
     he = extras["host_resident_e2e"]   # host-resident operands on every PE, exact sums
     assert isinstance(he, dict) and he["correct"] is True and he["last_error"] == 0 and he["GiBps"] > 0, he
     assert he["nreduce"] == 1 << 20, he
+    assert he["pageable"]["correct"] is True and he["pageable"]["GiBps"] > 0, he
     c0 = extras["config0"]             # BASELINE configs[0] through the product, 2 PEs
     for k in ("n1_heap", "n1_host", "n1024_heap", "n1024_host", "n4096_heap", "n4096_host"):
         assert c0[k]["correct"] is True and c0[k]["median_us"] > 0, (k, c0)
