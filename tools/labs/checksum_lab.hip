@@ -5,7 +5,7 @@
 //   pipe     the next iteration's load issued before this one is mixed
 //   pipe2    two iterations ahead
 //   unroll4  four independent loads per lane, then the mixing
-//   Build: hipcc --offload-arch=gfx950 -O3 tools/checksum_lab.hip -o tools/checksum_lab
+//   Build: hipcc --offload-arch=gfx950 -O3 tools/labs/checksum_lab.hip -o tools/labs/checksum_lab
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

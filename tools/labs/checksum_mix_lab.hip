@@ -8,7 +8,7 @@
 //          position constants (one v_mad_u64_u32 per word)
 //   none   plain XOR of the words (the memory-only floor)
 // 32 Mi doubles (256 MiB), grids 1024/2048/4096, median of 15 launches.
-//   hipcc --offload-arch=gfx950 -O3 tools/checksum_mix_lab.hip -o tools/checksum_mix_lab
+//   hipcc --offload-arch=gfx950 -O3 tools/labs/checksum_mix_lab.hip -o tools/labs/checksum_mix_lab
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

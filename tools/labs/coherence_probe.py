@@ -8,7 +8,7 @@ os.environ.setdefault("SHMEMX_HEAP_MEMORY", "device")
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "openshmem-async_amd"))
 import shmem_mi355x as shm  # noqa: E402
 

@@ -1,7 +1,7 @@
 // Experiment harness (not part of the library): variants of the 2-input
 // double fold acc[i] += in[i] over 32 Mi elements on gfx950, timed with HIP
 // events in interleaved rounds.  Build: hipcc --offload-arch=gfx950 -O3
-// tools/fold_lab.hip -o tools/fold_lab ; run on the GPU box.
+// tools/labs/fold_lab.hip -o tools/labs/fold_lab ; run on the GPU box.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

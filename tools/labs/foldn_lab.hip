@@ -14,8 +14,8 @@
 //               GB/s counts the P input streams plus the never-written output)
 // Timed with HIP events, interleaved rounds, warm (back to back) and cold
 // (a 1 GiB scratch rewritten before every launch).
-//   Build: hipcc --offload-arch=gfx950 -O3 tools/foldn_lab.hip -o tools/foldn_lab
-//   Run:   tools/foldn_lab <n per input> <cold 0|1> [skew bytes, -1 = separate]
+//   Build: hipcc --offload-arch=gfx950 -O3 tools/labs/foldn_lab.hip -o tools/labs/foldn_lab
+//   Run:   tools/labs/foldn_lab <n per input> <cold 0|1> [skew bytes, -1 = separate]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

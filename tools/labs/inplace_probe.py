@@ -6,7 +6,7 @@ import sys
 
 import torch
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "openshmem-async_amd"))
 os.environ.setdefault("SHMEMX_HEAP_MEMORY", "device")   # device addresses from shmem_malloc
 import shmem_mi355x as shm  # noqa: E402

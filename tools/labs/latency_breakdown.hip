@@ -10,9 +10,9 @@
 //                 host-coherent memory, the host spinning on it
 //   kernel_self   the copy kernel storing the sequence number itself (one
 //                 block: system-scope release store after its copy)
-//   Build: hipcc --offload-arch=gfx950 -O3 -I include tools/latency_breakdown.hip \
+//   Build: hipcc --offload-arch=gfx950 -O3 -I include tools/labs/latency_breakdown.hip \
 //            -L openshmem-async_amd -lshmem_reduce_mi355x -Wl,-rpath,$PWD/openshmem-async_amd \
-//            -o tools/latency_breakdown
+//            -o tools/labs/latency_breakdown
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

@@ -4,7 +4,7 @@ shmem_double_sum_to_all on the HBM twins (flush of the touched blocks, the
 kernel, marking the target device-newer), the host reading the target back
 (read faults, fetches), and the same call again on untouched operands.
 
-    SHMEMX_HEAP_MEMORY=mirrored python tools/mirror_probe.py [nreduce ...]
+    SHMEMX_HEAP_MEMORY=mirrored python tools/labs/mirror_probe.py [nreduce ...]
 """
 import ctypes
 import os
@@ -13,7 +13,7 @@ import time
 
 import numpy as np
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "openshmem-async_amd"))
 import shmem_mi355x as shm  # noqa: E402
 

@@ -6,7 +6,7 @@
 // arithmetic and its VGPRs go away; the cache-policy operand (sc0 = 1, nt = 2,
 // sc1 = 16) is set per variant.  Timed warm (back to back) and cold (a 1 GiB
 // read-only sweep before every launch), interleaved rounds.
-//   hipcc --offload-arch=gfx950 -O3 tools/peers_buf_lab.hip -o tools/peers_buf_lab
+//   hipcc --offload-arch=gfx950 -O3 tools/labs/peers_buf_lab.hip -o tools/labs/peers_buf_lab
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

@@ -17,8 +17,8 @@
 // chunk size.  Timed with HIP events, interleaved rounds, warm (back to back)
 // and cold (a 1 GiB read-only sweep before every launch: evicts, leaves
 // nothing dirty).
-//   Build: hipcc --offload-arch=gfx950 -O3 tools/peers_gather_lab.hip -o tools/peers_gather_lab
-//   Run:   tools/peers_gather_lab
+//   Build: hipcc --offload-arch=gfx950 -O3 tools/labs/peers_gather_lab.hip -o tools/labs/peers_gather_lab
+//   Run:   tools/labs/peers_gather_lab
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

@@ -8,8 +8,8 @@
 // combination per array.  Timed with HIP events in interleaved rounds, warm
 // (back to back) and cold (a 1 GiB read-only sweep before every step, so no
 // dirty line is left in the Infinity Cache).
-//   hipcc --offload-arch=gfx950 -O3 tools/policy_lab.hip -o tools/policy_lab
-//   tools/policy_lab [n_elems] [cold 0|1] [list 0|1]
+//   hipcc --offload-arch=gfx950 -O3 tools/labs/policy_lab.hip -o tools/labs/policy_lab
+//   tools/labs/policy_lab [n_elems] [cold 0|1] [list 0|1]
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

@@ -4,7 +4,7 @@ Infinity Cache), so each launch streams from HBM.  Compared with the
 back-to-back (warm) rate of the same config."""
 import json, os, statistics, sys
 import torch
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "openshmem-async_amd"))
 import shmem_mi355x as shm
 torch.cuda.set_device(0)

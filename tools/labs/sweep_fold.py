@@ -4,7 +4,7 @@ device references.  Interleaved rounds in one process
 (cdna_hip_programming.md §5.4 rule 24); prints one JSON object."""
 import json, os, statistics, sys
 import torch
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "openshmem-async_amd"))
 import shmem_mi355x as shm
 

@@ -3,7 +3,7 @@ every (nt mode, unroll) config, 7 interleaved rounds of 20 launches each,
 median / min / max of the per-launch time.  One JSON object on stdout."""
 import json, os, statistics, sys
 import torch
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "openshmem-async_amd"))
 import shmem_mi355x as shm
 

@@ -11,7 +11,7 @@
 //   fence64_sync  the library's 64-block system fence kernel, then sync
 //   fence64_poll  the same kernel, host spinning on its 64 words
 // With `spin` as argv[1], hipSetDeviceFlags(hipDeviceScheduleSpin) first.
-//   Build: hipcc --offload-arch=gfx950 -O3 tools/sync_lab.hip -o tools/sync_lab
+//   Build: hipcc --offload-arch=gfx950 -O3 tools/labs/sync_lab.hip -o tools/labs/sync_lab
 #include <hip/hip_runtime.h>
 
 #include <algorithm>

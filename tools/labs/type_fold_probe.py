@@ -5,14 +5,14 @@ of 10 launches after 3 warm ones.  GB/s counts the algorithmic 3 x 256 MiB
 (read acc, read in, write acc); a pair far below the HBM rate of the others
 is compute-bound (the soft-float long double, the complex products).
 
-    python tools/type_fold_probe.py
+    python tools/labs/type_fold_probe.py
 """
 import os
 import sys
 
 import torch
 
-REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(REPO, "openshmem-async_amd"))
 import shmem_mi355x as shm  # noqa: E402
 
