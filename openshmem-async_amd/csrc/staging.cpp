@@ -141,13 +141,15 @@ static void copy_bytes(char *dst, const char *src, size_t n, bool nt) {
 
 // $SHMEMX_COPY_NT: which staging copies of pageable arrays use streaming
 // stores — bit 0 the source into the page-locked ring (read next by the H2D
-// DMA), bit 1 the ring out into the caller's target; default 0 (round 1
-// measured no gain on the box; the r05 sweep, tools/gpu_steps.sh e2e_nt,
-// re-measures it with the copy lab beside it).
+// DMA), bit 1 the ring out into the caller's target; default 2: the out
+// gang's 4 threads copy 94 against 81 GB/s with them in the copy lab, and the
+// pipeline averages 36.0 against 34.9 GiB/s over interleaved runs, with the
+// smaller dip (profiles/r05_e2e_nt.txt); into the ring they lose (30.3
+// against 36.2: the H2D DMA reads the slot right after).
 static int copy_nt_mask() {
     static const int m = [] {
         const char *e = std::getenv("SHMEMX_COPY_NT");
-        return e && *e ? (std::atoi(e) & 3) : 0;
+        return e && *e ? (std::atoi(e) & 3) : 2;
     }();
     return m;
 }
