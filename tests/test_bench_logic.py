@@ -159,3 +159,22 @@ def test_device_code_hash_reads_the_fatbin(bench):
     h = shm.device_code_sha256()
     assert h and len(h) == 64 and h == shm.device_code_sha256()
     assert shm.device_code_sha256(__file__) is None
+
+
+def test_auto_recommendation_partial_sets_may_name_rccl(bench):
+    """Partial sets get RCCL on their own communicators (round 5), so the
+    partial table may name allreduce / rccl when they are the fastest correct
+    choice; SIGNAL is timed but never a table choice."""
+    sizes = [str(n) for n in (1, 1 << 9, 1 << 16, 1 << 19, 1 << 24)]
+    us = {"allreduce": [9, 10, 30, 150, 4000], "rccl": [20, 22, 40, 120, 2500],
+          "a2a": [15, 16, 50, 300, 9000], "direct": [8, 20, 40, 250, 8000], "signal": [5, 5, 5, 5, 5]}
+    t = {a: dict(zip(sizes, v)) for a, v in us.items()}
+    ok = {a: {n: True for n in sizes} for a in us}
+    rec = bench.auto_recommendation({"us_per_call": {}, "correct": {}},
+                                    {"first_half_us_per_call": t, "first_half_correct": ok,
+                                     "every_other_us_per_call": t, "every_other_correct": ok})
+    row = rec["strided"]
+    assert [row[b]["table"] for b in ("8B", "4KiB", "512KiB", "4MiB", "128MiB")] == \
+        ["direct", "allreduce", "allreduce", "rccl", "rccl"]
+    assert row["8B"]["fastest"] == "signal"
+    assert rec["env"]["SHMEMX_AUTO_PARTIAL"] == "0:direct,181:allreduce,1482910:rccl"
