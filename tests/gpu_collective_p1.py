@@ -2,7 +2,8 @@
 SHMEMX_FORCE_COLLECTIVE=1 a one-PE job runs the full RCCL / ALLREDUCE / A2A /
 GATHER schedules (RCCL communicator of one rank), so every RCCL call of the
 path executes on a one-GPU box; host arrays take the collective path's
-bounce and staging copies.  Prints "ok" or raises."""
+bounce and staging copies; the stream-ordered schedules are also captured
+into HIP graphs and replayed.  Prints "ok" or raises."""
 import os
 import sys
 
@@ -58,4 +59,32 @@ for t in ("long", "double", "short"):
             assert buf[:n].tobytes() == want.tobytes(), (t, n, k, "in place")
             shm.to_all(t, "sum", buf[3:], buf, n, 0, 0, 1)           # host, partial overlap
             assert buf[3:n + 3].tobytes() == want.tobytes(), (t, n, k, "overlap")
+
+# HIP graph capture of the stream-ordered collective schedules on the real
+# RCCL (one rank): RS + AG (+ the ragged tail's all-reduce), the single
+# all-reduce, A2A's grouped send/recv + fold + all-gather and GATHER, and
+# AUTO, each warmed once (workspaces sized outside the capture), captured,
+# then replayed on fresh inputs.  DIRECT is refused under capture (host
+# barriers), so it is not here.
+st = torch.cuda.Stream()
+for t, op, algo, n in [("double", "sum", "rccl", (1 << 20) + 3), ("double", "sum", "allreduce", 4103),
+                       ("int", "max", "rccl", 65536), ("long", "xor", "a2a", 70001),
+                       ("float", "min", "gather", 4103), ("double", "sum", "auto", (1 << 20) + 3)]:
+    s = torch.from_numpy(oracle.fill(t, 1, 5, n)).cuda()
+    d = torch.zeros_like(s)
+    st.wait_stream(torch.cuda.current_stream())
+    shm.reduce_on_stream(t, op, d, s, n, 0, 0, 1, algo, st.cuda_stream)       # warm
+    st.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        shm.reduce_on_stream(t, op, d, s, n, 0, 0, 1, algo, st.cuda_stream)
+    for k in range(3):
+        src = oracle.fill(t, 1, 60 + k, n)
+        s.copy_(torch.from_numpy(src))
+        d.zero_()
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        assert d.cpu().numpy().tobytes() == src.tobytes(), (t, op, algo, n, "graph replay", k)
+    del g
 print("ok")

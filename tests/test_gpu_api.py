@@ -180,7 +180,8 @@ def test_fortran_forwarder(cuda, shm, oracle):
 
 def test_rccl_schedules_one_rank(cuda):
     """Every RCCL call of the multi-PE path (reduce-scatter, all-gather,
-    all-reduce, grouped send/recv schedules) on a one-rank communicator."""
+    all-reduce, grouped send/recv schedules) on a one-rank communicator,
+    called directly and captured into HIP graphs that are replayed."""
     import subprocess
     import sys
     env = dict(os.environ, SHMEMX_FORCE_COLLECTIVE="1")
