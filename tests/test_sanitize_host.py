@@ -38,3 +38,22 @@ def test_host_code_under_asan_ubsan(tmp_path, name):
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
     assert out.stdout.startswith(want), out.stdout[-2000:]
     assert "runtime error" not in out.stderr, out.stderr[-4000:]
+
+
+def test_gpu_asan_build_is_instrumented():
+    """tests/test_gpu_asan.py's library build is really instrumented: its host
+    objects call the ASan runtime, which the drivers carry, and the driver
+    that runs over the RCCL test double binds it before the library."""
+    asan = os.path.join(REPO, "tests", "native", "asan")
+    subprocess.run(["make", "-s", "-C", os.path.join(REPO, "tests", "native"), "asan"], check=True)
+    lib = subprocess.run(["nm", "-D", os.path.join(asan, "libshmem_reduce_mi355x.so")],
+                         capture_output=True, text=True, check=True).stdout
+    assert "__asan_report_load8" in lib and "__asan_init" in lib
+    for exe in ("asan_driver", "asan_driver_fake"):
+        syms = subprocess.run(["nm", os.path.join(asan, exe)], capture_output=True, text=True,
+                              check=True).stdout
+        assert "__asan_init" in syms
+    needed = subprocess.run(["readelf", "-d", os.path.join(asan, "asan_driver_fake")], capture_output=True,
+                            text=True).stdout
+    libs = [ln.split("[")[1].rstrip("]") for ln in needed.splitlines() if "(NEEDED)" in ln]
+    assert libs.index("libfake_rccl.so") < libs.index("libshmem_reduce_mi355x.so")
