@@ -222,6 +222,7 @@ void mir_by_region(uint64_t off, size_t bytes, F f) {
 }
 
 void mir_to_device(uint64_t off, size_t bytes, void *) {
+    bind_device();
     mir_by_region(off, bytes, [](uint64_t o, size_t len, bool locked) {
         const char *src = mirror::alias_base() + o;
         if (locked) {
@@ -247,6 +248,7 @@ void mir_to_device(uint64_t off, size_t bytes, void *) {
 void mir_copy_to_host(uint64_t off, size_t bytes);
 
 void mir_to_host(uint64_t off, size_t bytes, void *) {
+    bind_device();
     wait_writers();
     mir_copy_to_host(off, bytes);
 }
@@ -257,6 +259,7 @@ void mir_to_host(uint64_t off, size_t bytes, void *) {
 void mir_to_host_done(uint64_t off, size_t bytes, void *) { mir_copy_to_host(off, bytes); }
 
 void mir_copy_to_host(uint64_t off, size_t bytes) {
+    bind_device();   // also runs on the fault service thread
     const hipStream_t fs = mir_fetch_stream();
     mir_by_region(off, bytes, [fs](uint64_t o, size_t len, bool locked) {
         char *dst = mirror::alias_base() + o;

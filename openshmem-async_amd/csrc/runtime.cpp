@@ -295,8 +295,16 @@ static int file_bootstrap(int pe, int npes, int device) {
     return rc;
 }
 
+void bind_device() {
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess || cur != g_state.device) SHMX_HIP(hipSetDevice(g_state.device));
+}
+
 int ensure_init() {
-    if (g_state.inited) return SHMEMX_OK;
+    if (g_state.inited) {
+        bind_device();
+        return SHMEMX_OK;
+    }
     const int npes = env_int("SHMEM_NPES", "WORLD_SIZE", 1);
     if (npes != 1) return set_error(SHMEMX_ENOINIT);
     int dev = 0;

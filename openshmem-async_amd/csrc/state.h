@@ -103,6 +103,12 @@ void trace(int level, const char *fmt, ...);
     } while (0)
 
 int ensure_init();                  // single-PE auto-init; ENOINIT if npes > 1
+// HIP's current device is per host thread, and the library makes streams,
+// events and workspaces lazily on whatever thread calls it: every entry point
+// (through ensure_init) and the mirrored heap's service thread make the PE's
+// device current first, so a thread other than shmem_init's does not make
+// them on device 0 (one PE per GPU: LOCAL_RANK > 0 is never device 0).
+void bind_device();
 // Members-only RCCL communicators of partial active sets (set_comm.cpp):
 // set_comm returns the set's cached communicator, creating it first (a
 // collective over the set's members alone: `member` is this PE's index in it)

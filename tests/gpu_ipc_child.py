@@ -1179,6 +1179,104 @@ elif scenario == "big":
     extra["big_bytes_per_pe"] = nbytes
     shm.free(BIG_TGT)
     shm.free(BIG_SRC)
+elif scenario == "threads":
+    # Several host threads of one PE call the library at once (the reference
+    # program's threads, each on its own arrays).  Workers make PE_size 1
+    # calls on their own PE (reduce-op.c:213-216: a copy; no peer takes part,
+    # so the PEs' call orders stay aligned) on host arrays (staging, small and
+    # chunked), on torch tensors through the stream form on their own
+    # non-blocking stream, and on their own 64 KiB-aligned mirrored heap
+    # blocks (host stores, blocking call, host reads that fault and fetch on
+    # the service thread); meanwhile the main thread runs world-set
+    # collectives against the oracle.  Each worker first makes no device
+    # current itself: the library binds the PE's device on the calling thread.
+    import threading
+    nthreads, iters = 4, int(os.environ.get("THREAD_ITERS", "25"))
+    heap_n = (4096, 65536 + 7)               # a light-path call and a block-marking one
+    blocks = []
+    for _ in range(nthreads):                # shmem_malloc is collective: main thread, same order
+        pair = []
+        for n in heap_n:
+            nb = (n * 8 + 65535) & ~65535
+            pair.append((shm.align(65536, nb), shm.align(65536, nb)))
+        blocks.append(pair)
+    lock = threading.Lock()
+    counts = [0] * nthreads
+
+    def worker(w):
+        rng = np.random.default_rng(0x7E + 31 * pe + w)
+        stream = None
+        try:
+            for it in range(iters):
+                # host arrays: one bounce-buffer call, and a chunked pageable one
+                for n in (1000, 300001 if it % 5 == 0 else 20000):
+                    src = rng.standard_normal(n)
+                    tgt = np.full(n, np.nan)
+                    shm.to_all("double", "sum", tgt, src, n, pe, 0, 1)
+                    if not same_bits(tgt, src) or shm.last_error():
+                        with lock:
+                            fails.append(f"thread {w} it {it}: host n={n} wrong")
+                # torch tensors on this thread's own stream
+                if stream is None:
+                    stream = torch.cuda.Stream(device=0)
+                n = 50000 + w
+                with torch.cuda.stream(stream):
+                    s = torch.randint(-1000, 1000, (n,), dtype=torch.int64, device="cuda")
+                    d = torch.zeros_like(s)
+                shm.reduce_on_stream("long", "sum", d, s, n, pe, 0, 1, "auto", stream.cuda_stream)
+                stream.synchronize()
+                if not torch.equal(d, s):
+                    with lock:
+                        fails.append(f"thread {w} it {it}: stream form wrong")
+                # mirrored heap view: host stores, the call, host loads
+                if MIRRORED:
+                    for (hs, ht), n in zip(blocks[w], heap_n):
+                        want = rng.integers(-2**40, 2**40, n).astype(np.int64)
+                        host_view(hs, np.int64, n)[:] = want
+                        shm.to_all("longlong", "sum", ht, hs, n, pe, 0, 1)
+                        got = host_view(ht, np.int64, n).copy()
+                        if not np.array_equal(got, want) or shm.last_error():
+                            with lock:
+                                fails.append(f"thread {w} it {it}: heap n={n}: "
+                                             f"{int((got != want).sum())} elements differ")
+                counts[w] += 1
+        except Exception as e:                # noqa: BLE001 — reported, not raised in a thread
+            with lock:
+                fails.append(f"thread {w}: {type(e).__name__}: {e}")
+
+    threads = [threading.Thread(target=worker, args=(w,)) for w in range(nthreads)]
+    for t in threads:
+        t.start()
+    srcs = oracle.sources("int", 0, npes, 1024, base_seed=0x7B00)
+    want = oracle.reduce_sim("int", "sum", srcs, 0, 0, npes)[pe]
+    src, tgt = host_view(HEAP_SRC, np.int32, 1024), host_view(HEAP_TGT, np.int32, 1024)
+    main_calls = 0
+    # a fixed count (every PE makes the same world calls), most of them while
+    # the workers run
+    for _ in range(int(os.environ.get("THREAD_MAIN_CALLS", "200"))):
+        if MIRRORED:
+            src[:] = srcs[pe]
+            tgt[:] = 0
+            shm.to_all("int", "sum", HEAP_TGT, HEAP_SRC, 1024, 0, 0, npes)
+            got = tgt.copy()
+        else:
+            got = np.zeros(1024, np.int32)
+            shm.to_all("int", "sum", got, srcs[pe].copy(), 1024, 0, 0, npes)
+        if not np.array_equal(got, want):
+            fails.append(f"main call {main_calls}: world int sum wrong")
+        main_calls += 1
+    extra["workers_alive_after_main"] = sum(t.is_alive() for t in threads)
+    for t in threads:
+        t.join()
+    ncases = sum(counts) + main_calls
+    extra["worker_iterations"] = counts
+    extra["main_calls"] = main_calls
+    if MIRRORED:
+        extra["mirror_stats"] = shm.mirror_stats()
+    for pair in blocks:
+        for hs, ht in pair:
+            shm.free(ht)
+            shm.free(hs)
 elif scenario == "signal_timeout":
     # one SIGNAL call together (maps and votes), then PE 0 calls again alone:
     # its device barrier must give up after $SHMEMX_SIGNAL_TIMEOUT seconds and

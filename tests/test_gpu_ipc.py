@@ -521,6 +521,24 @@ def test_mirrored_view_fetch_waits_for_non_blocking_stream(tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("transport,npes,mode", [("ipc", 2, "mirrored"), ("rccl", 2, "device")])
+def test_threads_of_one_pe(tmp_path, transport, npes, mode):
+    """Four host threads per PE call the library at once (PE_size 1 calls on
+    host arrays, torch tensors on their own streams, and their own mirrored
+    heap blocks read back through the view) while each PE's main thread runs
+    world-set collectives: every result right, nothing deadlocks."""
+    env = {"SHMEMX_TRANSPORT": transport, "SHMEMX_HEAP_MEMORY": mode}
+    if transport == "rccl":
+        env["FAKE_RCCL"] = os.path.join(HERE, "native", "libfake_rccl.so")
+    reports = run_pes(tmp_path, npes, "threads", env, timeout=300)
+    for r in reports:
+        assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
+        assert r["worker_iterations"] == [25] * 4, r
+        if mode == "mirrored":
+            assert r["mirror_stats"]["blocks_fetched"] > 0, r
+
+
+@pytest.mark.gpu
 def test_ipc_full_scenario_on_mirrored_heap(tmp_path):
     """The 2-PE "full" scenario (every reference pair and active set on heap
     operands, in place, overlap, torch and host arrays, heap_ptr puts,
