@@ -1054,9 +1054,16 @@ int shmemx_reduce_on_stream(int type, int op, void *target, const void *source,
                             logPE_stride, PE_size, algo, stream);
 }
 
+// The local folds need no shmem_init (they run on the caller's stream); after
+// it, a NULL stream means the PE's device, as for every other entry point.
+static void bind_if_inited() {
+    if (g_state.inited) bind_device();
+}
+
 int shmemx_fold_on_stream(int type, int op, void *acc, const void *in,
                           size_t nelems, void *stream) {
     t_last_error = SHMEMX_OK;
+    bind_if_inited();
     if (!op_on_device(type, op)) return set_error(op_valid(type, op) ? SHMEMX_ENOTSUP : SHMEMX_EINVAL);
     if (nelems == 0) return SHMEMX_OK;
     if (!acc || !in) return set_error(SHMEMX_EINVAL);
@@ -1070,6 +1077,7 @@ static int fold_n(int type, int op, void *out, const void *const *ins, int nins,
                   void *stream, bool peers) {
     auto launch = peers ? launch_fold_peers : launch_fold;
     t_last_error = SHMEMX_OK;
+    bind_if_inited();
     if (!op_on_device(type, op)) return set_error(op_valid(type, op) ? SHMEMX_ENOTSUP : SHMEMX_EINVAL);
     if (nins < 1 || !ins) return set_error(SHMEMX_EINVAL);
     if (nelems == 0) return SHMEMX_OK;
@@ -1102,6 +1110,7 @@ int shmemx_fold_n_peers_on_stream(int type, int op, void *out, const void *const
 int shmemx_gather_on_stream(const void *const *srcs, void *const *dsts, const size_t *bytes,
                             int nseg, void *stream) {
     t_last_error = SHMEMX_OK;
+    bind_if_inited();
     if (nseg < 0 || nseg > kMaxFoldInputs || (nseg > 0 && (!srcs || !dsts || !bytes)))
         return set_error(SHMEMX_EINVAL);
     for (int i = 0; i < nseg; ++i)
