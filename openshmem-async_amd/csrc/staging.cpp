@@ -238,11 +238,14 @@ void parallel_copy(void *dst, const void *src, size_t bytes, bool nt) {
     pool.copy(dst, src, bytes, nt);
 }
 
-// The CPUs the staging copy gangs run on ($SHMEMX_COPY_CPUS): "all" (the
-// default) = unpinned; "gpu" = this process's allowed CPUs on the GPU's NUMA
-// node; "data" = per call, each gang on the node of the caller's array it
-// reads or writes; or an explicit list "a-b,c".  An empty result (no NUMA
-// information, no allowed CPU there) leaves the threads unpinned.
+// The CPUs the staging copy gangs run on ($SHMEMX_COPY_CPUS): "spread" (the
+// default) = each copy thread alone on one core of its own cache domain of the
+// GPU's NUMA node (spread_cpus: 36.9-37.7 GiB/s on two boxes where the
+// scheduler's placement gave 27.2-37.7, profiles/r05_e2e_spread.txt); "all" =
+// unpinned; "gpu" = this process's allowed CPUs on the GPU's NUMA node, any
+// of them; "data" = per call, each gang on the node of the caller's array it
+// reads or writes; or an explicit list "a-b,c".  An empty result (no NUMA or
+// cache information, no allowed CPU there) leaves the threads unpinned.
 static std::vector<int> parse_cpulist(const std::string &list) {
     std::vector<int> cpus;
     std::stringstream ss(list);
@@ -260,7 +263,7 @@ static std::vector<int> parse_cpulist(const std::string &list) {
 static const std::string &copy_cpus_mode() {
     static const std::string m = [] {
         const char *e = std::getenv("SHMEMX_COPY_CPUS");
-        return std::string(e && *e ? e : "all");
+        return std::string(e && *e ? e : "spread");
     }();
     return m;
 }
@@ -287,21 +290,67 @@ static int page_node(const void *p) {
     return status >= 0 ? status : -1;
 }
 
+// NUMA node of the PE's GPU (its PCI device's numa_node), or -1
+static int gpu_numa_node() {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof bus, g_state.device) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    std::string id(bus);
+    for (auto &c : id) c = (char)std::tolower((unsigned char)c);
+    std::ifstream nf("/sys/bus/pci/devices/" + id + "/numa_node");
+    int node = -1;
+    if (!(nf >> node) || node < 0) return -1;
+    return node;
+}
+
+// One allowed CPU per last-level-cache domain (a CCD on EPYC) of the GPU's
+// NUMA node, the first hardware thread of a core, in domain order: each copy
+// thread gets a domain's own path to memory instead of the scheduler's
+// placement, which may stack several on one CCD or put them on the other
+// socket (profiles/r05_e2e_spread.txt).  Within a domain PE p takes its
+// (p mod cores)-th core, so the PEs whose GPUs share a node use different
+// cores.  Empty if the topology is unknown.
+static std::vector<int> spread_cpus() {
+    const int node = gpu_numa_node();
+    std::vector<int> on_node = node >= 0 ? node_cpus(node) : std::vector<int>{};
+    if (on_node.empty()) return {};
+    std::vector<std::pair<std::string, std::vector<int>>> doms;   // L3 shared_cpu_list -> its cores
+    for (int c : on_node) {
+        const std::string base = "/sys/devices/system/cpu/cpu" + std::to_string(c);
+        std::ifstream sib(base + "/topology/thread_siblings_list");
+        std::string sl;
+        if (std::getline(sib, sl)) {
+            const std::vector<int> sibs = parse_cpulist(sl);
+            if (!sibs.empty() && sibs.front() != c) continue;   // not a core's first thread
+        }
+        std::string dom;
+        for (int idx = 0; idx < 8 && dom.empty(); ++idx) {
+            std::ifstream lv(base + "/cache/index" + std::to_string(idx) + "/level");
+            int level = 0;
+            if (!(lv >> level)) break;
+            if (level != 3) continue;
+            std::ifstream sh(base + "/cache/index" + std::to_string(idx) + "/shared_cpu_list");
+            std::getline(sh, dom);
+        }
+        if (dom.empty()) return {};
+        auto it = std::find_if(doms.begin(), doms.end(), [&](const auto &d) { return d.first == dom; });
+        if (it == doms.end()) doms.push_back({dom, {c}});
+        else it->second.push_back(c);
+    }
+    std::vector<int> out;
+    for (const auto &d : doms) out.push_back(d.second[(size_t)g_state.pe % d.second.size()]);
+    return out;
+}
+
 static std::vector<int> copy_cpus() {
     const std::string &mode = copy_cpus_mode();
-    if (mode == "all" || mode == "data") return {};
+    if (mode == "all" || mode == "data" || mode == "spread") return {};
     std::vector<int> want;
     if (mode == "gpu") {
-        char bus[64] = {0};
-        if (hipDeviceGetPCIBusId(bus, sizeof bus, g_state.device) != hipSuccess) {
-            (void)hipGetLastError();
-            return {};
-        }
-        std::string id(bus);
-        for (auto &c : id) c = (char)std::tolower((unsigned char)c);
-        std::ifstream nf("/sys/bus/pci/devices/" + id + "/numa_node");
-        int node = -1;
-        if (!(nf >> node) || node < 0) return {};
+        const int node = gpu_numa_node();
+        if (node < 0) return {};
         std::ifstream cf("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");
         std::string list;
         if (!std::getline(cf, list)) return {};
@@ -327,15 +376,18 @@ namespace {
 // doing both in turn left each copy waiting for the other).
 class CopyGang {
   public:
-    CopyGang(unsigned n, const std::vector<int> &cpus) : n_(std::max(1u, n)) {
+    // cpus: every worker may run on any of them; per_thread (if not empty):
+    // worker i on per_thread[i % size] alone
+    CopyGang(unsigned n, const std::vector<int> &cpus, const std::vector<int> &per_thread = {})
+        : n_(std::max(1u, n)) {
         for (unsigned i = 0; i < n_; ++i) {
             workers_.emplace_back([this, i] { run(i); });
-            if (!cpus.empty()) {
-                cpu_set_t set;
-                CPU_ZERO(&set);
-                for (int c : cpus) CPU_SET(c, &set);
+            cpu_set_t set;
+            CPU_ZERO(&set);
+            if (!per_thread.empty()) CPU_SET(per_thread[i % per_thread.size()], &set);
+            else for (int c : cpus) CPU_SET(c, &set);
+            if (!per_thread.empty() || !cpus.empty())
                 (void)pthread_setaffinity_np(workers_.back().native_handle(), sizeof set, &set);
-            }
         }
     }
     ~CopyGang() {
@@ -420,7 +472,24 @@ CopyGang &gang(int which) {
         }
         return c;
     }();
-    static CopyGang in(total / 2, cpus), out(total - total / 2, cpus);
+    // spread: the in gang takes every other domain from the first, the out
+    // gang the ones between, so no two copy threads share a domain while
+    // there are domains enough
+    static const std::vector<int> spread = [] {
+        std::vector<int> c = copy_cpus_mode() == "spread" ? spread_cpus() : std::vector<int>{};
+        if (!c.empty() && log_enabled(LOG_INFO)) {
+            std::string l;
+            for (int x : c) l += std::to_string(x) + " ";
+            trace(LOG_INFO, "staging copy gangs spread over one CPU per cache domain: %s", l.c_str());
+        }
+        return c;
+    }();
+    auto half = [](const std::vector<int> &all, size_t first) {
+        std::vector<int> h;
+        for (size_t i = first; i < all.size(); i += 2) h.push_back(all[i]);
+        return h.empty() ? all : h;
+    };
+    static CopyGang in(total / 2, cpus, half(spread, 0)), out(total - total / 2, cpus, half(spread, 1));
     return which == 0 ? in : out;
 }
 }  // namespace
