@@ -239,9 +239,9 @@ void parallel_copy(void *dst, const void *src, size_t bytes, bool nt) {
 }
 
 // The CPUs the staging copy gangs run on ($SHMEMX_COPY_CPUS): "spread" (the
-// default) = each copy thread alone on one core of its own cache domain of the
-// GPU's NUMA node (spread_cpus: 36.9-37.7 GiB/s on two boxes where the
-// scheduler's placement gave 27.2-37.7, profiles/r05_e2e_spread.txt); "all" =
+// default) = each copy thread in its own cache domain of the GPU's NUMA node
+// (spread_domains: 36.8-37.7 GiB/s on three boxes where the scheduler's
+// placement gave 27.2-37.7, profiles/r05_e2e_spread.txt); "all" =
 // unpinned; "gpu" = this process's allowed CPUs on the GPU's NUMA node, any
 // of them; "data" = per call, each gang on the node of the caller's array it
 // reads or writes; or an explicit list "a-b,c".  An empty result (no NUMA or
@@ -305,33 +305,26 @@ static int gpu_numa_node() {
     return node;
 }
 
-// One allowed CPU per last-level-cache domain (a CCD on EPYC) of the GPU's
-// NUMA node, the first hardware thread of a core, in domain order: each copy
-// thread gets a domain's own path to memory instead of the scheduler's
-// placement, which may stack several on one CCD or put them on the other
-// socket (profiles/r05_e2e_spread.txt).  Within a domain PE p takes its
-// (p mod cores)-th core, so the PEs whose GPUs share a node use different
-// cores.  Empty if the topology is unknown.
-static std::vector<int> spread_cpus() {
+// The last-level-cache domains (CCDs on EPYC) of the GPU's NUMA node, each as
+// this process's allowed CPUs in it, in domain order: each copy thread is
+// confined to one domain, so the threads use different domains' paths to
+// memory instead of the scheduler's placement, which may stack several on one
+// CCD or put them on the other socket (profiles/r05_e2e_spread.txt); within a
+// domain the scheduler still picks an idle core.  Empty if the topology is
+// unknown.
+static std::vector<std::vector<int>> spread_domains() {
     const int node = gpu_numa_node();
-    std::vector<int> on_node = node >= 0 ? node_cpus(node) : std::vector<int>{};
-    if (on_node.empty()) return {};
-    std::vector<std::pair<std::string, std::vector<int>>> doms;   // L3 shared_cpu_list -> its cores
+    const std::vector<int> on_node = node >= 0 ? node_cpus(node) : std::vector<int>{};
+    std::vector<std::pair<std::string, std::vector<int>>> doms;   // L3 shared_cpu_list -> CPUs
     for (int c : on_node) {
-        const std::string base = "/sys/devices/system/cpu/cpu" + std::to_string(c);
-        std::ifstream sib(base + "/topology/thread_siblings_list");
-        std::string sl;
-        if (std::getline(sib, sl)) {
-            const std::vector<int> sibs = parse_cpulist(sl);
-            if (!sibs.empty() && sibs.front() != c) continue;   // not a core's first thread
-        }
+        const std::string base = "/sys/devices/system/cpu/cpu" + std::to_string(c) + "/cache/index";
         std::string dom;
         for (int idx = 0; idx < 8 && dom.empty(); ++idx) {
-            std::ifstream lv(base + "/cache/index" + std::to_string(idx) + "/level");
+            std::ifstream lv(base + std::to_string(idx) + "/level");
             int level = 0;
             if (!(lv >> level)) break;
             if (level != 3) continue;
-            std::ifstream sh(base + "/cache/index" + std::to_string(idx) + "/shared_cpu_list");
+            std::ifstream sh(base + std::to_string(idx) + "/shared_cpu_list");
             std::getline(sh, dom);
         }
         if (dom.empty()) return {};
@@ -339,8 +332,8 @@ static std::vector<int> spread_cpus() {
         if (it == doms.end()) doms.push_back({dom, {c}});
         else it->second.push_back(c);
     }
-    std::vector<int> out;
-    for (const auto &d : doms) out.push_back(d.second[(size_t)g_state.pe % d.second.size()]);
+    std::vector<std::vector<int>> out;
+    for (auto &d : doms) out.push_back(std::move(d.second));
     return out;
 }
 
@@ -377,17 +370,17 @@ namespace {
 class CopyGang {
   public:
     // cpus: every worker may run on any of them; per_thread (if not empty):
-    // worker i on per_thread[i % size] alone
-    CopyGang(unsigned n, const std::vector<int> &cpus, const std::vector<int> &per_thread = {})
+    // worker i on the CPUs of per_thread[i % size]
+    CopyGang(unsigned n, const std::vector<int> &cpus, const std::vector<std::vector<int>> &per_thread = {})
         : n_(std::max(1u, n)) {
         for (unsigned i = 0; i < n_; ++i) {
             workers_.emplace_back([this, i] { run(i); });
+            const std::vector<int> &mine = per_thread.empty() ? cpus : per_thread[i % per_thread.size()];
+            if (mine.empty()) continue;
             cpu_set_t set;
             CPU_ZERO(&set);
-            if (!per_thread.empty()) CPU_SET(per_thread[i % per_thread.size()], &set);
-            else for (int c : cpus) CPU_SET(c, &set);
-            if (!per_thread.empty() || !cpus.empty())
-                (void)pthread_setaffinity_np(workers_.back().native_handle(), sizeof set, &set);
+            for (int c : mine) CPU_SET(c, &set);
+            (void)pthread_setaffinity_np(workers_.back().native_handle(), sizeof set, &set);
         }
     }
     ~CopyGang() {
@@ -475,17 +468,18 @@ CopyGang &gang(int which) {
     // spread: the in gang takes every other domain from the first, the out
     // gang the ones between, so no two copy threads share a domain while
     // there are domains enough
-    static const std::vector<int> spread = [] {
-        std::vector<int> c = copy_cpus_mode() == "spread" ? spread_cpus() : std::vector<int>{};
-        if (!c.empty() && log_enabled(LOG_INFO)) {
+    static const std::vector<std::vector<int>> spread = [] {
+        std::vector<std::vector<int>> d =
+            copy_cpus_mode() == "spread" ? spread_domains() : std::vector<std::vector<int>>{};
+        if (!d.empty() && log_enabled(LOG_INFO)) {
             std::string l;
-            for (int x : c) l += std::to_string(x) + " ";
-            trace(LOG_INFO, "staging copy gangs spread over one CPU per cache domain: %s", l.c_str());
+            for (const auto &x : d) l += std::to_string(x.front()) + "+" + std::to_string(x.size() - 1) + " ";
+            trace(LOG_INFO, "staging copy threads one per cache domain (first CPU+others): %s", l.c_str());
         }
-        return c;
+        return d;
     }();
-    auto half = [](const std::vector<int> &all, size_t first) {
-        std::vector<int> h;
+    auto half = [](const std::vector<std::vector<int>> &all, size_t first) {
+        std::vector<std::vector<int>> h;
         for (size_t i = first; i < all.size(); i += 2) h.push_back(all[i]);
         return h.empty() ? all : h;
     };
