@@ -83,6 +83,7 @@ struct Heap {
     char *base = nullptr;     // the segment (nullptr until the first allocation)
     char *view = nullptr;     // its host view (mirrored mode), else nullptr
     bool failed = false;      // the segment could not be allocated
+    bool checked = false;     // every PE's segment state compared (first allocation)
     Arena arena;
     std::map<void *, Private> priv;   // blocks outside the segment
 } g_heap;
@@ -355,6 +356,20 @@ bool in_view(const void *p) {
 
 void *alloc(size_t alignment, size_t bytes) {
     if (!bytes) return nullptr;
+    // The first allocation (a collective call on every PE, shmem_malloc's
+    // rule, symmem.c:209) checks that the segment exists on every PE or on
+    // none: a PE without it would carve its objects elsewhere and the heap
+    // would no longer be symmetric, which the IPC algorithms and heap_ptr
+    // rely on (the reference's heap-attach failure is fatal too).
+    if (!g_heap.checked && g_state.npes > 1 && node::up()) {
+        g_heap.checked = true;
+        const bool mine = ensure_segment();
+        const bool all_have = node::agree(0, 1, g_state.npes, mine);
+        const bool none_has = node::agree(0, 1, g_state.npes, !mine);   // then all use private blocks
+        if (!all_have && !none_has)
+            fatal("shmem_malloc", "the symmetric heap segment could not be allocated on every PE "
+                                  "(SHMEM_SYMMETRIC_HEAP_SIZE)");
+    }
     if (ensure_segment()) {
         const uint64_t off = g_heap.arena.alloc(bytes, alignment ? alignment : 1);
         if (off != Arena::kNone) return (g_heap.view ? g_heap.view : g_heap.base) + off;
@@ -581,6 +596,7 @@ void release_all() {
     g_heap.priv.clear();
     g_heap.base = nullptr;
     g_heap.failed = false;
+    g_heap.checked = false;
     g_heap.arena.reset(0);
 }
 

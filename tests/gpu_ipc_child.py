@@ -282,7 +282,7 @@ HEAP_SRC = shm.malloc(CAP + 64)
 HEAP_TGT = shm.malloc(CAP)
 assert HEAP_SRC and HEAP_TGT, "shmem_malloc failed"
 HOST_HEAP = os.environ.get("SHMEMX_HEAP_MEMORY") == "host"
-for q in range(npes):
+for q in range(npes if scenario != "heapcheck" else 0):   # (heapcheck may run on private blocks)
     # a host-kind heap is not peer-addressable: NULL, as the reference's
     # shmem_ptr; nor is a mirrored heap's host view (a peer's store would go
     # behind that peer's view), whose HBM twin is
@@ -1179,6 +1179,23 @@ elif scenario == "big":
     extra["big_bytes_per_pe"] = nbytes
     shm.free(BIG_TGT)
     shm.free(BIG_SRC)
+elif scenario == "heapcheck":
+    # one world call on heap objects (segment or, when no PE has a segment,
+    # private blocks alike on every PE), checked against the oracle
+    n = 1000
+    srcs = oracle.sources("long", 0, npes, n, base_seed=0x4EA9)
+    want = oracle.reduce_sim("long", "sum", srcs, 0, 0, npes)[pe]
+    private_host = MIRRORED and not shm.mirror_device_ptr(HEAP_SRC)   # page-locked private blocks
+    if private_host:
+        host_view(HEAP_SRC, np.int64, n)[:] = srcs[pe]
+    else:
+        heap_write(HEAP_SRC, srcs[pe], n * 8)
+    shm.to_all("long", "sum", HEAP_TGT, HEAP_SRC, n, 0, 0, npes)
+    got = host_view(HEAP_TGT, np.int64, n).copy() if private_host else read(HEAP_TGT, "long", n)
+    extra["private_blocks"] = bool(private_host or not shm.heap_ptr(HEAP_SRC, pe))
+    ncases += 1
+    if not np.array_equal(got, want):
+        fails.append("world long sum on heap objects wrong")
 elif scenario == "threads":
     # Several host threads of one PE call the library at once (the reference
     # program's threads, each on its own arrays).  Workers make PE_size 1

@@ -43,7 +43,11 @@ def start_pes(tmp_path, npes, scenario, extra_env=None):
             env["GPU_MAX_HW_QUEUES"] = "2"
         env.pop("RANK", None)
         env.pop("WORLD_SIZE", None)
-        for k, v in (extra_env or {}).items():   # None: unset
+        for k, v in (extra_env or {}).items():   # None: unset; "PE<p>:VAR" for PE p only
+            if ":" in k:
+                who, k = k.split(":", 1)
+                if who != f"PE{pe}":
+                    continue
             if v is None:
                 env.pop(k, None)
             else:
@@ -518,6 +522,24 @@ def test_mirrored_view_fetch_waits_for_non_blocking_stream(tmp_path):
     r = reports[0]
     assert not r["fails"], r["fails"]
     assert r["ncases"] == 2 and r["mirror_stats"]["blocks_fetched"] > 0, r
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["mirrored", "device"])
+def test_heap_segment_on_some_pes_only_is_fatal(tmp_path, mode):
+    """A PE whose symmetric heap segment cannot be allocated (a heap size no
+    GPU holds) while its peer's can: the first shmem_malloc fails on both PEs
+    with a FATAL line, instead of one PE carving its objects outside the
+    segment (an asymmetric heap); with the size on every PE, both use private
+    blocks alike and the calls are right."""
+    env = {"SHMEMX_HEAP_MEMORY": mode, "PE1:SHMEM_SYMMETRIC_HEAP_SIZE": "4000000G"}
+    procs = start_pes(tmp_path, 2, "heapcheck", env)
+    rcs, logs = wait_pes(procs, 120)
+    for pe, (rc, log) in enumerate(zip(rcs, logs)):
+        assert rc != 0 and "could not be allocated on every PE" in log, f"PE {pe} exit {rc}:\n{log[-2000:]}"
+    env = {"SHMEMX_HEAP_MEMORY": mode, "SHMEM_SYMMETRIC_HEAP_SIZE": "4000000G"}
+    for r in run_pes(tmp_path, 2, "heapcheck", env, timeout=120):
+        assert not r["fails"] and r["ncases"] == 1 and r["private_blocks"], r
 
 
 @pytest.mark.gpu
