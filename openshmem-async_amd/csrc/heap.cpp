@@ -369,6 +369,11 @@ void *alloc(size_t alignment, size_t bytes) {
         if (!all_have && !none_has)
             fatal("shmem_malloc", "the symmetric heap segment could not be allocated on every PE "
                                   "(SHMEM_SYMMETRIC_HEAP_SIZE)");
+        // and one size everywhere (published before the votes' barriers), or
+        // the arenas would run out at different allocations
+        if (all_have && !node::agree(0, 1, g_state.npes,
+                                     node::peer_bytes(node::kHeap, 0) == node::peer_bytes(node::kHeap, g_state.pe)))
+            fatal("shmem_malloc", "SHMEM_SYMMETRIC_HEAP_SIZE differs across PEs");
     }
     if (ensure_segment()) {
         const uint64_t off = g_heap.arena.alloc(bytes, alignment ? alignment : 1);

@@ -531,12 +531,18 @@ def test_heap_segment_on_some_pes_only_is_fatal(tmp_path, mode):
     GPU holds) while its peer's can: the first shmem_malloc fails on both PEs
     with a FATAL line, instead of one PE carving its objects outside the
     segment (an asymmetric heap); with the size on every PE, both use private
-    blocks alike and the calls are right."""
+    blocks alike and the calls are right.  Segments of different sizes
+    (SHMEM_SYMMETRIC_HEAP_SIZE set differently) are FATAL as well."""
     env = {"SHMEMX_HEAP_MEMORY": mode, "PE1:SHMEM_SYMMETRIC_HEAP_SIZE": "4000000G"}
     procs = start_pes(tmp_path, 2, "heapcheck", env)
     rcs, logs = wait_pes(procs, 120)
     for pe, (rc, log) in enumerate(zip(rcs, logs)):
         assert rc != 0 and "could not be allocated on every PE" in log, f"PE {pe} exit {rc}:\n{log[-2000:]}"
+    # segments on both PEs, of different sizes: FATAL on both too
+    procs = start_pes(tmp_path, 2, "heapcheck", {"SHMEMX_HEAP_MEMORY": mode, "PE1:SHMEM_SYMMETRIC_HEAP_SIZE": "2G"})
+    rcs, logs = wait_pes(procs, 120)
+    for pe, (rc, log) in enumerate(zip(rcs, logs)):
+        assert rc != 0 and "SHMEM_SYMMETRIC_HEAP_SIZE differs across PEs" in log, f"PE {pe} exit {rc}:\n{log[-2000:]}"
     env = {"SHMEMX_HEAP_MEMORY": mode, "SHMEM_SYMMETRIC_HEAP_SIZE": "4000000G"}
     for r in run_pes(tmp_path, 2, "heapcheck", env, timeout=120):
         assert not r["fails"] and r["ncases"] == 1 and r["private_blocks"], r
