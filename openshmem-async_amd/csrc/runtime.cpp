@@ -190,6 +190,42 @@ static bool make_uid(ncclUniqueId *id) {
     return ok;
 }
 
+// Settings every PE must share: they choose each call's algorithm and
+// schedule, and every member of a set must run the same one (reduce-op.c:
+// 213-250: one call sequence on every PE).  A launcher that exports one on
+// some ranks only would make the plans diverge and the collectives mismatch,
+// so init compares a hash of them across the PEs once.
+// (SHMEM_SYMMETRIC_HEAP_SIZE is compared as the sizes themselves, at the
+// first allocation: heap.cpp.)
+static const char *const kPlanSettings[] = {
+    "SHMEM_REDUCE_ALGO",        "SHMEMX_AUTO_FULL",         "SHMEMX_AUTO_PARTIAL",
+    "SHMEMX_ALLREDUCE_MAX_KB",  "SHMEMX_DIRECT_ONESHOT_KB", "SHMEMX_FUSED_TWOSHOT_KB",
+    "SHMEMX_FUSED_ONESHOT",     "SHMEMX_SET_COMMS",         "SHMEMX_SET_COMMS_MAX",
+    "SHMEMX_STAGE_CHUNK_MB",    "SHMEMX_DIRECT_SCRATCH_MB", "SHMEMX_TRANSPORT"};
+
+static std::string plan_settings() {
+    std::string t;
+    for (const char *k : kPlanSettings) {
+        const char *v = std::getenv(k);
+        if (v) t += std::string(k) + "=" + v + " ";
+    }
+    return t;
+}
+
+static void check_plan_settings() {
+    const std::string mine = plan_settings();
+    unsigned long long h = 1469598103934665603ull;   // FNV-1a
+    for (unsigned char c : mine) h = (h ^ c) * 1099511628211ull;
+    std::vector<unsigned long long> all;
+    if (exchange_u64(0, 0, g_state.npes, h, all)) fatal("shmem_init", "cannot compare the PEs' settings");
+    for (size_t q = 0; q < all.size(); ++q) {
+        if (all[q] == h) continue;
+        const std::string why = "the algorithm settings differ across PEs (PE " + std::to_string(q) +
+                                " has others); this PE's: " + (mine.empty() ? "(none set)" : mine);
+        fatal("shmem_init", why.c_str());
+    }
+}
+
 static int init_locked(int pe, int npes, int device, const void *uid) {
     if (g_state.inited) return SHMEMX_OK;
     if (npes < 1 || pe < 0 || pe >= npes) return set_error(SHMEMX_EINVAL);
@@ -250,6 +286,7 @@ static int init_locked(int pe, int npes, int device, const void *uid) {
     g_state.device = device;
     g_state.algo = parse_algo(std::getenv("SHMEM_REDUCE_ALGO"));
     g_state.inited = true;
+    if (npes > 1) check_plan_settings();
     trace(LOG_INIT, "PE %d of %d on HIP device %d%s%s", pe, npes, device,
           g_state.comm ? ", RCCL communicator up" : "", node::up() ? ", node block up" : "");
     return SHMEMX_OK;

@@ -525,6 +525,23 @@ def test_mirrored_view_fetch_waits_for_non_blocking_stream(tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["ipc", "rccl"])
+def test_algorithm_settings_differing_across_pes_is_fatal(tmp_path, transport):
+    """An algorithm setting exported on one PE only ($SHMEM_REDUCE_ALGO here)
+    would make the PEs plan different schedules for the same call: shmem_init
+    compares the settings and fails on every PE with a FATAL line naming this
+    PE's, instead of mismatched collectives later."""
+    env = {"SHMEMX_TRANSPORT": transport, "PE1:SHMEM_REDUCE_ALGO": "gather"}
+    if transport == "rccl":
+        env["FAKE_RCCL"] = os.path.join(HERE, "native", "libfake_rccl.so")
+    procs = start_pes(tmp_path, 2, "heapcheck", env)
+    rcs, logs = wait_pes(procs, 120)
+    for pe, (rc, log) in enumerate(zip(rcs, logs)):
+        assert rc != 0 and "algorithm settings differ across PEs" in log, f"PE {pe} exit {rc}:\n{log[-2000:]}"
+    assert "SHMEM_REDUCE_ALGO=gather" in logs[1] and "SHMEM_REDUCE_ALGO" not in logs[0], logs
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["mirrored", "device"])
 def test_heap_segment_on_some_pes_only_is_fatal(tmp_path, mode):
     """A PE whose symmetric heap segment cannot be allocated (a heap size no
