@@ -30,6 +30,7 @@
 #include "internal.h"
 #include "shmem_reduce_mi355x.h"
 #include "state.h"
+#include "topology.h"
 
 namespace shmx {
 
@@ -246,20 +247,6 @@ void parallel_copy(void *dst, const void *src, size_t bytes, bool nt) {
 // of them; "data" = per call, each gang on the node of the caller's array it
 // reads or writes; or an explicit list "a-b,c".  An empty result (no NUMA or
 // cache information, no allowed CPU there) leaves the threads unpinned.
-static std::vector<int> parse_cpulist(const std::string &list) {
-    std::vector<int> cpus;
-    std::stringstream ss(list);
-    std::string item;
-    while (std::getline(ss, item, ',')) {
-        if (item.empty()) continue;
-        const size_t dash = item.find('-');
-        const int lo = std::atoi(item.c_str());
-        const int hi = dash == std::string::npos ? lo : std::atoi(item.c_str() + dash + 1);
-        for (int c = lo; c <= hi && c >= 0; ++c) cpus.push_back(c);
-    }
-    return cpus;
-}
-
 static const std::string &copy_cpus_mode() {
     static const std::string m = [] {
         const char *e = std::getenv("SHMEMX_COPY_CPUS");
@@ -268,19 +255,19 @@ static const std::string &copy_cpus_mode() {
     return m;
 }
 
-// allowed CPUs of NUMA node `node` (empty if unknown)
-static std::vector<int> node_cpus(int node) {
-    std::ifstream cf("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");
-    std::string list;
-    if (node < 0 || !std::getline(cf, list)) return {};
-    cpu_set_t allowed;
-    CPU_ZERO(&allowed);
-    if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return {};
+// this process's allowed CPUs
+static std::vector<int> allowed_cpus() {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof set, &set) != 0) return {};
     std::vector<int> out;
-    for (int c : parse_cpulist(list))
-        if (c < CPU_SETSIZE && CPU_ISSET(c, &allowed)) out.push_back(c);
+    for (int c = 0; c < CPU_SETSIZE; ++c)
+        if (CPU_ISSET(c, &set)) out.push_back(c);
     return out;
 }
+
+// allowed CPUs of NUMA node `node` (empty if unknown)
+static std::vector<int> node_cpus(int node) { return topo::node_cpus("/sys", node, allowed_cpus()); }
 
 // NUMA node of the page holding `p` (move_pages with no target: a query), or -1
 static int page_node(const void *p) {
@@ -314,49 +301,17 @@ static int gpu_numa_node() {
 // unknown.
 static std::vector<std::vector<int>> spread_domains() {
     const int node = gpu_numa_node();
-    const std::vector<int> on_node = node >= 0 ? node_cpus(node) : std::vector<int>{};
-    std::vector<std::pair<std::string, std::vector<int>>> doms;   // L3 shared_cpu_list -> CPUs
-    for (int c : on_node) {
-        const std::string base = "/sys/devices/system/cpu/cpu" + std::to_string(c) + "/cache/index";
-        std::string dom;
-        for (int idx = 0; idx < 8 && dom.empty(); ++idx) {
-            std::ifstream lv(base + std::to_string(idx) + "/level");
-            int level = 0;
-            if (!(lv >> level)) break;
-            if (level != 3) continue;
-            std::ifstream sh(base + std::to_string(idx) + "/shared_cpu_list");
-            std::getline(sh, dom);
-        }
-        if (dom.empty()) return {};
-        auto it = std::find_if(doms.begin(), doms.end(), [&](const auto &d) { return d.first == dom; });
-        if (it == doms.end()) doms.push_back({dom, {c}});
-        else it->second.push_back(c);
-    }
-    std::vector<std::vector<int>> out;
-    for (auto &d : doms) out.push_back(std::move(d.second));
-    return out;
+    return node >= 0 ? topo::cache_domains("/sys", node_cpus(node)) : std::vector<std::vector<int>>{};
 }
 
 static std::vector<int> copy_cpus() {
     const std::string &mode = copy_cpus_mode();
     if (mode == "all" || mode == "data" || mode == "spread") return {};
-    std::vector<int> want;
-    if (mode == "gpu") {
-        const int node = gpu_numa_node();
-        if (node < 0) return {};
-        std::ifstream cf("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist");
-        std::string list;
-        if (!std::getline(cf, list)) return {};
-        want = parse_cpulist(list);
-    } else {
-        want = parse_cpulist(mode);
-    }
-    cpu_set_t allowed;
-    CPU_ZERO(&allowed);
-    if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return {};
+    if (mode == "gpu") return node_cpus(gpu_numa_node());
+    const std::vector<int> allowed = allowed_cpus();
     std::vector<int> out;
-    for (int c : want)
-        if (c < CPU_SETSIZE && CPU_ISSET(c, &allowed)) out.push_back(c);
+    for (int c : topo::parse_cpulist(mode))
+        if (std::find(allowed.begin(), allowed.end(), c) != allowed.end()) out.push_back(c);
     return out;
 }
 

@@ -1,8 +1,9 @@
 """The host-compilable parts of the library under AddressSanitizer and
 UndefinedBehaviorSanitizer (gcc, -fno-sanitize-recover: the first report
 fails the run): the symmetric-heap arena (arena.cpp), the intra-node block's
-host barrier and descriptors over forked PEs (node.cpp), and the soft x87
-arithmetic the GPU runs for long double (ld80.h).  The same harnesses run
+host barrier and descriptors over forked PEs (node.cpp), the soft x87
+arithmetic the GPU runs for long double (ld80.h), and the copy threads'
+placement over a fake sysfs tree (topology.cpp).  The same harnesses run
 unsanitized, at larger sizes, in test_heap_host.py, test_node_host.py and
 test_ld80_host.py.  GPU-side sanitizers are not available on the MI355X pool."""
 import os
@@ -23,6 +24,9 @@ CASES = {
     "node": ([os.path.join(NATIVE, "test_node_barrier.cpp"), os.path.join(CSRC, "node.cpp")], HIP_LINK,
              ["4", "1000"], "ok 4"),
     "ld80": ([os.path.join(NATIVE, "test_ld80.cpp")], [], ["300000"], "ok 300000"),
+    # the copy threads' placement (staging.cpp: cache domains of the GPU's node)
+    "topology": ([os.path.join(NATIVE, "test_topology.cpp"), os.path.join(CSRC, "topology.cpp")], [],
+                 ["{tmp}/sys"], "ok "),
 }
 
 
@@ -34,6 +38,7 @@ def test_host_code_under_asan_ubsan(tmp_path, name):
     env = dict(os.environ, SHMEMX_BARRIER_TIMEOUT="60",
                ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
                UBSAN_OPTIONS="print_stacktrace=1")
+    args = [a.replace("{tmp}", str(tmp_path)) for a in args]
     out = subprocess.run([str(exe), *args], capture_output=True, text=True, timeout=300, env=env)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
     assert out.stdout.startswith(want), out.stdout[-2000:]
