@@ -147,6 +147,16 @@ static void copy_bytes(char *dst, const char *src, size_t n, bool nt) {
 // pipeline averages 36.0 against 34.9 GiB/s over interleaved runs, with the
 // smaller dip (profiles/r05_e2e_nt.txt); into the ring they lose (30.3
 // against 36.2: the H2D DMA reads the slot right after).
+// $SHMEMX_STAGE_RAMP=0: uniform staging chunks (no quarter / half chunks at
+// the pipeline's ends)
+static bool stage_ramp() {
+    static const bool on = [] {
+        const char *e = std::getenv("SHMEMX_STAGE_RAMP");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
+
 static int copy_nt_mask() {
     static const int m = [] {
         const char *e = std::getenv("SHMEMX_COPY_NT");
@@ -774,7 +784,37 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
     // overwritten under a later chunk's H2D: no pipelining then
     const bool host_overlap = !tdev && !sdev && overlap(target, source, bytes);
     if (host_overlap) chunk = (size_t)nreduce;
-    const size_t nchunks = ((size_t)nreduce + chunk - 1) / chunk;
+    // The chunk schedule (elements), the same on every PE (calls_agree
+    // compares its length): full chunks, except that with at least four of
+    // them the first two and the last two go in quarter and half sizes, so
+    // the pipeline's fill (the first chunk's copy and H2D, which nothing
+    // overlaps) and drain (the last chunk's D2H and copy out) are short
+    // ($SHMEMX_STAGE_RAMP=0: uniform chunks).
+    std::vector<size_t> c_off, c_n;
+    {
+        const size_t n = (size_t)nreduce;
+        std::vector<size_t> head, tail;
+        if (stage_ramp() && !host_overlap && n >= 4 * chunk) {
+            const size_t q = std::max(g, (chunk / 4) / g * g), h = std::max(g, (chunk / 2) / g * g);
+            head = {q, h};
+            tail = {h, q};
+        }
+        size_t mid = n;
+        for (size_t x : head) mid -= x;
+        for (size_t x : tail) mid -= x;
+        if (!tail.empty()) {   // every chunk starts 16 B into the arrays' alignment: the odd elements go last
+            tail.back() += mid % g;
+            mid -= mid % g;
+        }
+        auto add = [&](size_t cnt) {
+            c_off.push_back(c_off.empty() ? 0 : c_off.back() + c_n.back());
+            c_n.push_back(cnt);
+        };
+        for (size_t x : head) add(x);
+        for (size_t done = 0; done < mid; done += chunk) add(std::min(chunk, mid - done));
+        for (size_t x : tail) add(x);
+    }
+    const size_t nchunks = c_n.size();
     if (collective && !calls_agree(start, logstride, size, nchunks)) return;
     // How each end reaches the device: directly (device memory), by DMA
     // (page-locked host memory), or through the page-locked bounce ring
@@ -811,17 +851,17 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
         if (in_bounce) gang(0).pin(node_cpus(page_node(source)));
         if (out_bounce) gang(1).pin(node_cpus(page_node(target)));
     }
-    auto count_of_chunk = [&](size_t k) { return std::min(chunk, (size_t)nreduce - k * chunk); };
+    auto count_of_chunk = [&](size_t k) { return c_n[k]; };
     auto start_in = [&](size_t k) {
         const size_t slot = k % kRingSlots;
         if (k >= kRingSlots) SHMX_HIP(hipEventSynchronize(ev_in_slot[slot]));
-        gang(0).start(ring_in(slot), hsrc + k * chunk_bytes, count_of_chunk(k) * sz, nt_in);
+        gang(0).start(ring_in(slot), hsrc + c_off[k] * sz, count_of_chunk(k) * sz, nt_in);
     };
     size_t out_started = 0;   // out-copies started; all but the last are complete
     auto start_out = [&]() {
         const size_t j = out_started++;
         SHMX_HIP(hipEventSynchronize(ev_out_slot[j % kRingSlots]));
-        gang(1).start(htgt + j * chunk_bytes, ring_out(j % kRingSlots), count_of_chunk(j) * sz, nt_out);
+        gang(1).start(htgt + c_off[j] * sz, ring_out(j % kRingSlots), count_of_chunk(j) * sz, nt_out);
     };
     // the out-copy of chunk j has completed (starting the ones before it)
     auto out_done = [&](size_t j) {
@@ -831,7 +871,7 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
     int rc = SHMEMX_OK;
     if (in_bounce && nchunks) start_in(0);
     for (size_t k = 0; k < nchunks && !rc; ++k) {
-        const size_t off = k * chunk_bytes;
+        const size_t off = c_off[k] * sz;
         const size_t b = count_of_chunk(k) * sz;
         const size_t slot = k % kRingSlots;
         const void *dsrc = hsrc + off;
