@@ -1,4 +1,5 @@
 set -u
+# (run from tools/: also copy tools/labs/e2e_pinned_sweep.py to tools/ with its REPO one directory up)
 # staging chunk ramp on / off, pageable and pinned host arrays, alternating in fresh processes
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; O=gpurun_out/e2e_ramp_ab.txt; : > $O
 for rep in 1 2 3; do for r in 1 0; do
