@@ -201,7 +201,8 @@ static const char *const kPlanSettings[] = {
     "SHMEM_REDUCE_ALGO",        "SHMEMX_AUTO_FULL",         "SHMEMX_AUTO_PARTIAL",
     "SHMEMX_ALLREDUCE_MAX_KB",  "SHMEMX_DIRECT_ONESHOT_KB", "SHMEMX_FUSED_TWOSHOT_KB",
     "SHMEMX_FUSED_ONESHOT",     "SHMEMX_SET_COMMS",         "SHMEMX_SET_COMMS_MAX",
-    "SHMEMX_STAGE_CHUNK_MB",    "SHMEMX_DIRECT_SCRATCH_MB", "SHMEMX_TRANSPORT"};
+    "SHMEMX_STAGE_CHUNK_MB",    "SHMEMX_STAGE_RAMP",        "SHMEMX_DIRECT_SCRATCH_MB",
+    "SHMEMX_TRANSPORT"};
 
 static std::string plan_settings() {
     std::string t;
