@@ -30,6 +30,7 @@
 #include "internal.h"
 #include "shmem_reduce_mi355x.h"
 #include "state.h"
+#include "stage_plan.h"
 #include "topology.h"
 
 namespace shmx {
@@ -784,36 +785,10 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
     // overwritten under a later chunk's H2D: no pipelining then
     const bool host_overlap = !tdev && !sdev && overlap(target, source, bytes);
     if (host_overlap) chunk = (size_t)nreduce;
-    // The chunk schedule (elements), the same on every PE (calls_agree
-    // compares its length): full chunks, except that with at least four of
-    // them the first two and the last two go in quarter and half sizes, so
-    // the pipeline's fill (the first chunk's copy and H2D, which nothing
-    // overlaps) and drain (the last chunk's D2H and copy out) are short
-    // ($SHMEMX_STAGE_RAMP=0: uniform chunks).
+    // The chunk schedule (elements, stage_plan.h), the same on every PE
+    // (calls_agree compares its length); $SHMEMX_STAGE_RAMP=0: uniform chunks.
     std::vector<size_t> c_off, c_n;
-    {
-        const size_t n = (size_t)nreduce;
-        std::vector<size_t> head, tail;
-        if (stage_ramp() && !host_overlap && n >= 4 * chunk) {
-            const size_t q = std::max(g, (chunk / 4) / g * g), h = std::max(g, (chunk / 2) / g * g);
-            head = {q, h};
-            tail = {h, q};
-        }
-        size_t mid = n;
-        for (size_t x : head) mid -= x;
-        for (size_t x : tail) mid -= x;
-        if (!tail.empty()) {   // every chunk starts 16 B into the arrays' alignment: the odd elements go last
-            tail.back() += mid % g;
-            mid -= mid % g;
-        }
-        auto add = [&](size_t cnt) {
-            c_off.push_back(c_off.empty() ? 0 : c_off.back() + c_n.back());
-            c_n.push_back(cnt);
-        };
-        for (size_t x : head) add(x);
-        for (size_t done = 0; done < mid; done += chunk) add(std::min(chunk, mid - done));
-        for (size_t x : tail) add(x);
-    }
+    stage_plan((size_t)nreduce, chunk, g, stage_ramp() && !host_overlap, c_off, c_n);
     const size_t nchunks = c_n.size();
     if (collective && !calls_agree(start, logstride, size, nchunks)) return;
     // How each end reaches the device: directly (device memory), by DMA

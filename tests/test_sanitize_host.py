@@ -3,7 +3,8 @@ UndefinedBehaviorSanitizer (gcc, -fno-sanitize-recover: the first report
 fails the run): the symmetric-heap arena (arena.cpp), the intra-node block's
 host barrier and descriptors over forked PEs (node.cpp), the soft x87
 arithmetic the GPU runs for long double (ld80.h), and the copy threads'
-placement over a fake sysfs tree (topology.cpp).  The same harnesses run
+placement over a fake sysfs tree (topology.cpp) and the staging chunk
+schedule (stage_plan.h).  The same harnesses run
 unsanitized, at larger sizes, in test_heap_host.py, test_node_host.py and
 test_ld80_host.py.  GPU-side sanitizers are not available on the MI355X pool."""
 import os
@@ -24,6 +25,8 @@ CASES = {
     "node": ([os.path.join(NATIVE, "test_node_barrier.cpp"), os.path.join(CSRC, "node.cpp")], HIP_LINK,
              ["4", "1000"], "ok 4"),
     "ld80": ([os.path.join(NATIVE, "test_ld80.cpp")], [], ["300000"], "ok 300000"),
+    # the host staging pipeline's chunk schedule (stage_plan.h)
+    "stage_plan": ([os.path.join(NATIVE, "test_stage_plan.cpp")], [], [], "ok "),
     # the copy threads' placement (staging.cpp: cache domains of the GPU's node)
     "topology": ([os.path.join(NATIVE, "test_topology.cpp"), os.path.join(CSRC, "topology.cpp")], [],
                  ["{tmp}/sys"], "ok "),
