@@ -144,6 +144,10 @@ struct FoldArgs {
     // one-workgroup launches of launch_fold_signal: store sig_value here when done
     unsigned long long *sig_word;
     unsigned long long sig_value;
+    // a copy (nins == 1) may store to a second destination too
+    // (launch_copy2_signal: a small blocking result into HBM and into the
+    // mirrored heap's view in one launch); nullptr otherwise
+    void *out2;
 };
 
 // The end of a one-workgroup fold that signals the host (launch_fold_signal):
@@ -180,11 +184,15 @@ __device__ __forceinline__ void fold_body(const FoldArgs &args) {
             for (int k = 1; k < nins; ++k)
                 acc = Op<T, OP>::ap(acc, static_cast<const T *>(args.ins[k])[i]);
             out[i] = acc;
+            if constexpr (NIN == 1)
+                if (args.out2) static_cast<T *>(args.out2)[i] = acc;
         }
     }
     if (args.nvec == 0) return;
 
     u32x4 *out = reinterpret_cast<u32x4 *>(static_cast<T *>(args.out) + args.head);
+    u32x4 *out2 = NIN == 1 && args.out2 ? reinterpret_cast<u32x4 *>(static_cast<T *>(args.out2) + args.head)
+                                        : nullptr;
     const size_t nvec = args.nvec;
     const size_t step = (size_t)gridDim.x * kBlock * UNROLL;
     for (size_t base = (size_t)blockIdx.x * kBlock * UNROLL; base < nvec;
@@ -247,6 +255,10 @@ __device__ __forceinline__ void fold_body(const FoldArgs &args) {
             }
 #pragma unroll
             for (int u = 0; u < UNROLL; ++u) st16<NT>(out + v0 + u * kBlock, acc[u]);
+            if constexpr (NIN == 1)
+                if (out2)
+#pragma unroll
+                    for (int u = 0; u < UNROLL; ++u) st16<NT>(out2 + v0 + u * kBlock, acc[u]);
         } else {
             // last partial chunk: one vector at a time, guarded
             for (int u = 0; u < UNROLL; ++u) {
@@ -258,6 +270,8 @@ __device__ __forceinline__ void fold_body(const FoldArgs &args) {
                     acc = apply16<T, OP>(acc, ld16<NT>(reinterpret_cast<const u32x4 *>(
                                                  static_cast<const T *>(args.ins[k]) + args.head) + v));
                 st16<NT>(out + v, acc);
+                if constexpr (NIN == 1)
+                    if (out2) st16<NT>(out2 + v, acc);
             }
         }
     }
@@ -674,6 +688,21 @@ hipError_t launch_fold_signal(int type, int op, void *out, const void *const *in
         ptrs[k + 1] = ins[k];
     }
     return dispatch(type, op, a, ptrs, nins + 1, n, stream);
+}
+
+hipError_t launch_copy2_signal(int type, void *out, void *out2, const void *in, size_t n, hipStream_t stream,
+                               const HostSignal &sig) {
+    if (!op_on_device(type, SHMEMX_OP_SUM) || !out || !out2 || !in || !sig.word) return hipErrorInvalidValue;
+    if (n == 0) return launch_host_signal(sig, stream);
+    FoldArgs a{};
+    a.out = out;
+    a.out2 = out2;
+    a.nins = 1;
+    a.ins[0] = in;
+    a.sig_word = sig.word;
+    a.sig_value = sig.value;
+    const void *ptrs[3] = {out, out2, in};   // the vector body needs all three on one alignment
+    return dispatch(type, SHMEMX_OP_SUM, a, ptrs, 3, n, stream);
 }
 
 hipError_t launch_host_signal(const HostSignal &sig, hipStream_t stream) {

@@ -476,6 +476,14 @@ void *device_operand(const void *p, size_t bytes) {
     return g_heap.base + off;
 }
 
+const void *current_host_bytes(const void *p, size_t bytes) {
+    if (!bytes || !in_view(p) ||
+        bytes > g_heap.arena.capacity() - (uint64_t)(static_cast<const char *>(p) - g_heap.view))
+        return nullptr;
+    const uint64_t off = (uint64_t)(static_cast<const char *>(p) - g_heap.view);
+    return mirror::view_current(off, bytes) ? mirror::alias_base() + off : nullptr;
+}
+
 const void *device_operand_bytes(const void *p, size_t bytes) {
     if (!in_view(p) || bytes > g_heap.arena.capacity() - (uint64_t)(static_cast<const char *>(p) - g_heap.view))
         return p;

@@ -142,6 +142,10 @@ class SameStreamFlush {
 // A blocking call's small source: only its own bytes that the host wrote go
 // to HBM (mirror::flush_bytes), no state change; returns the HBM twin.
 const void *device_operand_bytes(const void *p, size_t bytes);
+// A host-view operand [p, p + bytes) whose view bytes are current
+// (mirror::view_current): the same bytes through the view's alias (readable
+// by host code without a fault), else nullptr.
+const void *current_host_bytes(const void *p, size_t bytes);
 // The device address of the view's page-locked alias at host-view address
 // p (bytes inside one alias region), or nullptr.
 void *alias_device(const void *p, size_t bytes);

@@ -54,6 +54,11 @@ hipError_t launch_fold_signal(int type, int op, void *out, const void *const *in
 // the signal itself, after its own stores drained and a system-scope
 // release)?
 bool copy_one_workgroup(int type, const void *dst, const void *src, size_t n);
+// A copy (launch_fold with nins == 1) of n elements of `type` from `in` to
+// both `out` and `out2` in one launch, then sig as launch_fold_signal stores
+// it (a small blocking result into HBM and into the mirrored heap's view).
+hipError_t launch_copy2_signal(int type, void *out, void *out2, const void *in, size_t n, hipStream_t stream,
+                               const HostSignal &sig);
 // The one-thread marker kernel alone: stores sig once everything enqueued
 // before it on the stream has completed.
 hipError_t launch_host_signal(const HostSignal &sig, hipStream_t stream);

@@ -351,6 +351,15 @@ size_t flush_bytes(uint64_t off, size_t bytes) {
     return touched;
 }
 
+bool view_current(uint64_t off, size_t bytes) {
+    if (!g_view.base || !bytes) return false;
+    Guard g;
+    const size_t b0 = block_of(off), b1 = std::min(block_of(off + bytes - 1) + 1, g_view.nblocks);
+    for (size_t b = b0; b < b1; ++b)
+        if (g_view.state[b] == DEVICE_NEWER || g_view.pending[b]) return false;
+    return true;
+}
+
 bool begin_light_write(uint64_t off, size_t bytes) {
     if (!g_view.base || !bytes) return false;
     Guard g;

@@ -140,6 +140,10 @@ size_t flush_bytes(uint64_t off, size_t bytes);
 // False (nothing changed) if a block is DEVICE_NEWER or has a write in flight:
 // the caller takes begin_device_write instead.
 bool begin_light_write(uint64_t off, size_t bytes);
+// Are the view's bytes [off, off + bytes) current (no overlapped block
+// DEVICE_NEWER, no device write in flight on one), so host code may read
+// them without a fault and they are the operand's value?
+bool view_current(uint64_t off, size_t bytes);
 // The light write has ended and its work completed: `copied` = the call's
 // stream stored the result into the alias; otherwise it is copied back here
 // (Backend::to_host).  Counts the blocks as settled; returns bytes copied.

@@ -529,7 +529,22 @@ void reduce_blocking(int type, int op, void *target, const void *source,
             void *adst = bytes <= lim ? heap::alias_device(target, bytes) : nullptr;
             const bool light = adst && heap::twin(target) != target && heap::twin(source) != source &&
                                copy_one_workgroup(type, adst, heap::twin(target), (size_t)nreduce);
-            const void *s = light ? heap::device_operand_bytes(source, bytes) : heap::device_operand(source, bytes);
+            // PE_size 1 (a copy, reduce-op.c:213-216) on the light path, with
+            // the source's view bytes current: they go through the coherent
+            // bounce buffer (a CPU copy, as small host arrays do) and the copy
+            // kernel reads them there, instead of a DMA to the source's HBM
+            // twin first (its blocks keep their state: a HOST_NEWER block is
+            // flushed whole by the next call that needs it in HBM).  ISx's
+            // nreduce = 1 round: profiles/r05_isx_mirror.txt.
+            const void *cur = light && size == 1 && !g_state.force_collective && bytes <= kSmallHostBytes
+                                  ? heap::current_host_bytes(source, bytes) : nullptr;
+            const void *s = nullptr;
+            if (cur && small_bounce_reserve()) {
+                std::memcpy(g_state.bounce, cur, bytes);
+                s = g_state.bounce;
+            } else {
+                s = light ? heap::device_operand_bytes(source, bytes) : heap::device_operand(source, bytes);
+            }
             trace_reference_overlap(target, source, bytes);   // the caller's addresses
             // blocks of a host-view target: DEVICE_NEWER from before the call
             // (host accesses wait for it), or on the light path unchanged; the
@@ -603,7 +618,10 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
         return;
     }
     const size_t bytes = type_size(type) * (size_t)nreduce;
-    const bool tdev = device_accessible(target), sdev = device_accessible(source);
+    // (the small-message bounce buffer is mapped into the GPU: a source
+    // staged there by the mirrored heap's PE_size 1 light path is read in place)
+    const bool tdev = device_accessible(target),
+               sdev = device_accessible(source) || (source == g_state.bounce && g_state.bounce);
     hipStream_t s = g_state.stream;
     const bool collective = size > 1 || g_state.force_collective;
     shmemx_plan_t plan;
@@ -625,11 +643,9 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
             const HostSignal sig = next_host_signal();
             const void *in[1] = {source};
             if (g_state.settle_dst) {
-                // a small mirrored target: the copy, then the result into the
-                // view's alias by the workgroup that signals
-                const void *res[1] = {target};
-                SHMX_HIP(launch_fold(type, op, target, in, 1, (size_t)nreduce, s));
-                SHMX_HIP(launch_fold_signal(type, op, g_state.settle_dst, res, 1, (size_t)nreduce, s, sig));
+                // a small mirrored target: one copy kernel stores the result
+                // into HBM and into the view's alias, and its workgroup signals
+                SHMX_HIP(launch_copy2_signal(type, target, g_state.settle_dst, source, (size_t)nreduce, s, sig));
             } else {
                 SHMX_HIP(launch_fold_signal(type, op, target, in, 1, (size_t)nreduce, s, sig));
             }

@@ -930,9 +930,21 @@ elif scenario == "mirrored":
             break
     st = shm.mirror_stats(reset=True)
     ncases += 1
+    # (one PE: PE_size 1, a copy: the source goes through the coherent bounce
+    # buffer, so nothing is flushed; its block stays HOST_NEWER)
+    flushed_ok = st["blocks_flushed"] >= 20 if npes > 1 else st["blocks_flushed"] == 0
     if (st["write_faults"] or st["read_faults"] or st["blocks_device_newer"] or st["blocks_fetched"]
-            or st["blocks_settled"] < 20 or st["blocks_flushed"] < 20):
+            or st["blocks_settled"] < 20 or not flushed_ok):
         fails.append(f"mirrored light path: 20 ISx rounds changed block states: {st}")
+    if npes == 1:
+        # the source's host-written bytes never went to HBM: a stream-ordered
+        # call on it (device side) flushes its block first and sees them
+        sv[0] = 424242
+        shm.reduce_on_stream("longlong", "sum", t8, s8, 1, 0, 0, 1, "auto", 0)
+        torch.cuda.synchronize()
+        ncases += 1
+        if int(tv[0]) != 424242:
+            fails.append(f"mirrored light path: a stream-ordered call after the bounce rounds read {int(tv[0])}")
     # a light call that fails (this PE outside the set, or a set past npes)
     # writes nothing: the host's own bytes of the target stay, though its
     # block was never flushed to HBM
