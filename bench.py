@@ -1527,6 +1527,24 @@ def main():
             guarded("configs", lambda: config_extras(world, stream, barrier, max_over_ranks,
                                                      a.extras_max_nreduce))
             guarded("latency", lambda: latency_extras(world, barrier, max_over_ranks))
+
+            def isx_mirrored_round():
+                """ISx's nreduce = 1 round (a host store, shmem_longlong_sum_to_all,
+                a host load: examples/ISx/SHMEM/isx.c:615-624) on the library's
+                default mirrored heap, timed in a child process (the heap mode
+                is per process; this one hands out HBM addresses)."""
+                import subprocess
+                env = dict(os.environ)
+                env.pop("SHMEMX_HEAP_MEMORY", None)   # the library's default: mirrored
+                r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "isx_mirror_latency.py"), "2000"],
+                                   capture_output=True, text=True, timeout=120, env=env)
+                found = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+                if r.returncode != 0 or not found:
+                    return f"error: exit {r.returncode}: {r.stderr[-300:]}"
+                d = json.loads(found[-1])
+                return {k: d[k] for k in ("round_us", "call_us", "host_load_us", "rounds",
+                                          "mirror_stats_per_round")} | {"tool": "tools/isx_mirror_latency.py"}
+            guarded("isx_mirrored_round", isx_mirrored_round)
     elif a.extras:
         for alt in ("rccl", "allreduce", "a2a", "gather"):
             if alt == algo_used:
