@@ -1191,6 +1191,27 @@ elif scenario == "big":
     extra["big_bytes_per_pe"] = nbytes
     shm.free(BIG_TGT)
     shm.free(BIG_SRC)
+elif scenario == "ramp":
+    # Run with $SHMEMX_STAGE_CHUNK_MB=1: host arrays of a few MiB take the
+    # staging pipeline with its quarter / half chunks at both ends
+    # (stage_plan.h), pageable and in place, odd lengths included, every
+    # type width, on the world and a partial set; and pinned (page-locked)
+    # arrays through the same schedule
+    for t, op, n in (("double", "sum", (5 << 20) // 8 + 3), ("int", "xor", (6 << 20) // 4 + 1),
+                     ("short", "max", (4 << 20) // 2 + 5), ("complexd", "sum", (3 << 20) // 16 + 1)):
+        for mode in ("host", "hostinplace"):
+            for st in ((0, 0, npes), (npes - 1, 0, 1)):
+                seed += 1
+                run_case(t, op, n, st, "auto", mode, seed)
+    n = (5 << 20) // 8 + 7
+    srcs = oracle.sources("long", 1, npes, n, base_seed=0x7A3)
+    want = oracle.reduce_sim("long", "sum", srcs, 0, 0, npes)[pe]
+    src = torch.from_numpy(srcs[pe].copy()).pin_memory()
+    tgt = torch.zeros(n, dtype=torch.int64).pin_memory()
+    shm.to_all("long", "sum", tgt, src, n, 0, 0, npes)
+    ncases += 1
+    if not np.array_equal(tgt.numpy(), want) or shm.last_error():
+        fails.append("pinned long sum through the ramped staging pipeline wrong")
 elif scenario == "heapcheck":
     # one world call on heap objects (segment or, when no PE has a segment,
     # private blocks alike on every PE), checked against the oracle

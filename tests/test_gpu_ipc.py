@@ -526,6 +526,22 @@ def test_mirrored_view_fetch_waits_for_non_blocking_stream(tmp_path):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("transport", ["ipc", "rccl"])
+def test_staging_chunk_ramp(tmp_path, transport):
+    """Host arrays through the staging pipeline with 1 MiB chunks, so calls
+    of a few MiB get the ramped schedule (quarter and half chunks at both
+    ends, stage_plan.h): pageable out of place and in place, pinned, odd
+    lengths, 2- to 16-byte elements, world and one-member sets, against the
+    oracle on 2 PEs."""
+    env = {"SHMEMX_TRANSPORT": transport, "SHMEMX_STAGE_CHUNK_MB": "1"}
+    if transport == "rccl":
+        env["FAKE_RCCL"] = os.path.join(HERE, "native", "libfake_rccl.so")
+    for r in run_pes(tmp_path, 2, "ramp", env, timeout=300):
+        assert r["ncases"] > 0
+        assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("transport", ["ipc", "rccl"])
 def test_algorithm_settings_differing_across_pes_is_fatal(tmp_path, transport):
     """An algorithm setting exported on one PE only ($SHMEM_REDUCE_ALGO here)
     would make the PEs plan different schedules for the same call: shmem_init
