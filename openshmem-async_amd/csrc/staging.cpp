@@ -621,7 +621,7 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
     // (the small-message bounce buffer is mapped into the GPU: a source
     // staged there by the mirrored heap's PE_size 1 light path is read in place)
     const bool tdev = device_accessible(target),
-               sdev = device_accessible(source) || (source == g_state.bounce && g_state.bounce);
+               sdev = (source == g_state.bounce && g_state.bounce) || device_accessible(source);
     hipStream_t s = g_state.stream;
     const bool collective = size > 1 || g_state.force_collective;
     shmemx_plan_t plan;
