@@ -198,7 +198,11 @@ enum {
 };
 
 /* Exchange algorithms (DESIGN.md "Multi-GPU").
- *   AUTO    RCCL for what RCCL reduces exactly as specified, A2A otherwise
+ *   AUTO    on the whole job RCCL (ALLREDUCE up to 4 MiB) for what RCCL
+ *           reduces exactly as specified, A2A otherwise; a partial set takes
+ *           A2A ($SHMEMX_AUTO_PARTIAL may name rccl / allreduce: the set's own
+ *           communicator, so far run against the RCCL test double only);
+ *           float / double / long double min and max take GATHER (below)
  *   RCCL    ncclReduceScatter + ncclAllGather (+ ncclAllReduce on the
  *           <P*16-byte tail); RCCL-native type/op only; the whole job on the
  *           world communicator, a partial set on its own members-only
@@ -230,7 +234,11 @@ enum {
  *           blocking call then aborts with a FATAL line.
  * With $SHMEMX_TRANSPORT=ipc there is no RCCL communicator: AUTO means
  * DIRECT, GATHER runs as a DIRECT-style kernel in each PE's own order, and
- * RCCL / A2A / ALLREDUCE are ENOTSUP; SIGNAL runs on both transports. */
+ * RCCL / A2A / ALLREDUCE are ENOTSUP; SIGNAL runs on both transports.
+ * Float, double and long double min / max: a<b?a:b under NaN and +-0 gives
+ * each PE its own reference answer (reduce-op.c:130-142, 219-248), so on
+ * these six pairs every algorithm folds in the calling PE's own order: A2A
+ * runs as GATHER, DIRECT and SIGNAL read every member's whole source. */
 enum {
     SHMEMX_ALGO_AUTO = 0, SHMEMX_ALGO_RCCL, SHMEMX_ALGO_A2A,
     SHMEMX_ALGO_GATHER, SHMEMX_ALGO_ALLREDUCE, SHMEMX_ALGO_DIRECT, SHMEMX_ALGO_SIGNAL,
@@ -277,7 +285,11 @@ int shmemx_reduce_on_stream(int type, int op, void *target, const void *source,
 /* The local element-wise fold, reduce-op.c:231-235 as one HIP kernel:
  *   acc[i] = op(acc[i], in[i])                              (fold2)
  *   out[i] = op(...op(op(ins[0][i], ins[1][i]), ins[2][i])..., ins[nins-1][i])
- * out may alias ins[0].  Device pointers, stream-ordered. */
+ * out may alias ins[0].  Device pointers, stream-ordered.  These local folds
+ * (and shmemx_gather_on_stream) need no shmem_init and leave the calling
+ * thread's current HIP device as it was; with a NULL stream after shmem_init
+ * they launch on the PE's device.  Every other entry point makes the PE's
+ * device current on the calling thread (hipSetDevice) and leaves it so. */
 int shmemx_fold_on_stream(int type, int op, void *acc, const void *in,
                           size_t nelems, void *stream);
 int shmemx_fold_n_on_stream(int type, int op, void *out,
@@ -310,8 +322,11 @@ int shmemx_fold_set_tuning(int max_blocks, int nontemporal, int unroll);
  * the library's RCCL communicator (ncclCommRegister), so RCCL may use
  * collectives' heap operands in place instead of staging them through its
  * own buffers.  Off by default: the N > 1 bench times the RCCL algorithms
- * both ways (extras.rccl_registered) before it is adopted.  Every PE should
- * call it alike.  ENOTSUP without an RCCL communicator or an HBM segment. */
+ * both ways (extras.rccl_registered) before it is adopted.  A collective over
+ * the whole job (the PEs agree with an ncclAllReduce that every one of them
+ * registered): every PE must call it, in the same order as the other world
+ * collectives, or the callers hang.  ENOTSUP without an RCCL communicator or
+ * an HBM segment. */
 int shmemx_rccl_register_heap(int on);
 
 /* The kernel clock: with on != 0, every launch of the fold family (the

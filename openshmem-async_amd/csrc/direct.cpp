@@ -18,10 +18,12 @@
 // barrier has passed (node_sync).  Every PE ends with the reference's
 // PE_start result.
 //
-// Own order (SHMEMX_ALGO_GATHER on the IPC transport): every PE folds the
-// whole array in its own reference order, src_me first, then the other
-// members ascending (reduce-op.c:219-248), reading (P-1) peer arrays: the
-// reference's per-PE bits on every PE.
+// Own order (SHMEMX_ALGO_GATHER on the IPC transport, and every call on the
+// float / double / long double min and max pairs, own_order_pair): every PE
+// folds the whole array in its own reference order, src_me first, then the
+// other members ascending (reduce-op.c:219-248), reading (P-1) peer arrays:
+// the reference's per-PE bits on every PE.  Small arrays take the fused one
+// shot with the inputs in that order.
 //
 // Synchronisation is the reference's: a barrier before the peers' sources
 // are read (reduce-op.c:217) and one after the targets are final (:250),
@@ -371,8 +373,8 @@ namespace {
 // DIRECT's one shot as one fused launch (launch_signal_fold): every member's
 // source (heap or staged scratch, per the descriptors) and every member's
 // heap segment (the signal counters) mapped, then the launch and one wait.
-int direct_fused(int type, int op, char *tgt, size_t n, int start, int step, int P,
-                 const std::vector<node::Desc> &desc, bool stage_tgt, hipStream_t s) {
+int direct_fused(int type, int op, char *tgt, size_t n, int start, int step, int P, int m,
+                 bool own_order, const std::vector<node::Desc> &desc, bool stage_tgt, hipStream_t s) {
     std::vector<std::pair<node::Region, int>> regs;
     for (int i = 0; i < P; ++i) {
         regs.emplace_back(static_cast<node::Region>(desc[i].src.region), start + i * step);
@@ -388,9 +390,14 @@ int direct_fused(int type, int op, char *tgt, size_t n, int start, int step, int
     const size_t sz = type_size(type);
     char *const scratch_tgt = g_scratch.base + g_scratch.bytes / 2;
     fa.out = stage_tgt ? scratch_tgt : tgt;
+    // set order, or mine (src_me first, then the others ascending)
+    auto src_of = [&](int i) {
+        return node::peer_base(static_cast<node::Region>(desc[i].src.region), start + i * step) + desc[i].src.off;
+    };
+    int k = 0;
+    if (own_order) fa.ins[k++] = src_of(m);
     for (int i = 0; i < P; ++i)
-        fa.ins[i] = node::peer_base(static_cast<node::Region>(desc[i].src.region), start + i * step) +
-                    desc[i].src.off;
+        if (!own_order || i != m) fa.ins[k++] = src_of(i);
     fa.nins = P;
     fa.n = n;
     // The host spins on a page-locked word instead of waiting for the
@@ -484,10 +491,11 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     const size_t cmax = std::max(g, (half / sz) / g * g);   // elements per staged chunk
     auto pe_of = [&](int i) { return start + i * step; };
     // Small arrays: one shot — every member folds the whole array itself (in
-    // set order, so all agree) and writes only its own target: one kernel
-    // and two barriers instead of two kernels and three.  Same decision on
-    // every member (n is collective).
-    const bool one_shot = !own_order && bytes <= oneshot_bytes();
+    // set order, so all agree, or each in its own) and writes only its own
+    // target: one kernel and two barriers instead of two kernels and three.
+    // Same decision on every member (n is collective).  Own order is the one
+    // shot's schedule at every size.
+    const bool one_shot = bytes <= oneshot_bytes();
     const bool local_write = own_order || one_shot;
 
     // Where my operands live for the peers.  A source that partially
@@ -520,15 +528,15 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     // bit 3: "I can take the fused two-shot launch" (source and target in my
     // heap segment, one chunk)
     const bool single = n <= cmax;
-    const bool twoshot_size = !own_order && !one_shot && bytes <= fused_twoshot_bytes();
+    const bool twoshot_size = !local_write && bytes <= fused_twoshot_bytes();
     d.count = (stage_src || stage_tgt ? 1 : 0) | (partial && tgt > src ? 2 : 0) |
-              (one_shot && single && fused_oneshot_enabled() && heap::signal_area() ? 4 : 0) |
+              (one_shot && single && P <= kMaxFoldInputs && fused_oneshot_enabled() && heap::signal_area() ? 4 : 0) |
               (twoshot_size && single && !stage_src && !stage_tgt && heap::signal_area() ? 8 : 0);
     // aux: the size limits this PE decided with ($SHMEMX_DIRECT_ONESHOT_KB,
     // $SHMEMX_FUSED_TWOSHOT_KB / shmemx_set_fused_twoshot_kb), in KiB.  They
     // pick the schedule (one shot or two, fused or not) and with it the
     // number of barriers, so members that disagree on them must not start it.
-    if (!own_order) d.aux = (uint64_t)(oneshot_bytes() >> 10) << 32 | (uint64_t)(fused_twoshot_bytes() >> 10);
+    d.aux = (uint64_t)(oneshot_bytes() >> 10) << 32 | (uint64_t)(fused_twoshot_bytes() >> 10);
     node::put_desc(d);
     if (single && stage_src)
         SHMX_HIP(hipMemcpyAsync(g_scratch.base, src, bytes, hipMemcpyDefault, s));
@@ -537,7 +545,7 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     auto read_descs = [&] {
         for (int i = 0; i < P; ++i) desc[i] = i == m ? d : node::get_desc(pe_of(i));
     };
-    if (!own_order) {
+    {
         // The descriptors first, with no fence, on every call whatever its
         // size (so the barrier sequence never depends on a local setting).
         // Every member then sees the same descriptors and takes the same
@@ -568,15 +576,12 @@ int direct_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
             const int bit = one_shot ? 4 : 8;
             bool fuse = true;
             for (int i = 0; i < P; ++i) fuse &= (desc[i].count & bit) != 0;
-            if (fuse && one_shot) return direct_fused(type, op, tgt, n, start, step, P, desc, stage_tgt, s);
+            if (fuse && one_shot)
+                return direct_fused(type, op, tgt, n, start, step, P, m, own_order, desc, stage_tgt, s);
             if (fuse) return direct_fused2(type, op, tgt, n, start, step, P, m, desc, s);
         }
         // my source (and its staging) is complete; reduce-op.c:217
         node_sync(start, step, P, s, &g_phase_us[kEntryWait], &g_phase_us[kEntryBarrier]);
-    } else {
-        // my source (and its staging) is complete; reduce-op.c:217
-        node_sync(start, step, P, s, &g_phase_us[kEntryWait], &g_phase_us[kEntryBarrier]);
-        read_descs();
     }
 
     // Every member reads the same descriptors, so all cut the same chunks

@@ -382,6 +382,12 @@ __global__ void host_signal_kernel(unsigned long long *word, unsigned long long 
 // completed, its kernels' end-of-kernel releases included), 0.3-0.8 us
 // faster per small call than the one-thread kernel above, which
 // $SHMEMX_SIGNAL_WRITEVALUE=0 restores (profiles/r05_marker_ab.txt).
+// Either marker publishes a multi-block result only through the preceding
+// kernel's end-of-kernel release, which is system scope (HIP's default for
+// a dispatch) and writes back every XCD's L2: the marker kernel's own
+// release reaches only the XCD it ran on, so it would not cover such a
+// result either.  One-workgroup folds store the signal themselves after
+// their own system-scope release.
 hipError_t enqueue_marker(unsigned long long *word, unsigned long long value, hipStream_t stream) {
     static const bool packet = [] {
         const char *e = std::getenv("SHMEMX_SIGNAL_WRITEVALUE");
@@ -408,8 +414,7 @@ hipError_t launch_typed(const FoldArgs &a0, hipStream_t stream) {
     a.sig_word = nullptr;
     const hipError_t e = launch_typed_grid<T, OP, NT>(a, stream);
     if (e != hipSuccess) return e;
-    (void)enqueue_marker(a0.sig_word, a0.sig_value, stream);
-    return hipGetLastError();
+    return enqueue_marker(a0.sig_word, a0.sig_value, stream);
 }
 
 template <typename T, int OP, int NT>
@@ -516,9 +521,9 @@ hipError_t launch_copy_nt(const FoldArgs &a0, hipStream_t stream) {
     else
         launch_k(kKindCopy, fold_kernel<T, SHMEMX_OP_SUM, 1, kUnrollCopyLarge, NT>, dim3((unsigned)blocks),
                  dim3(kBlock), stream, a);
-    if (a0.sig_word && !self_signal)
-        (void)enqueue_marker(a0.sig_word, a0.sig_value, stream);
-    return hipGetLastError();
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !a0.sig_word || self_signal) return e;
+    return enqueue_marker(a0.sig_word, a0.sig_value, stream);
 }
 
 template <typename T>

@@ -389,6 +389,23 @@ static bool rccl_native(int type, int op) {
     }
 }
 
+// The six pairs whose reference answer depends on the calling PE beyond
+// rounding: min and max of float, double and long double.  a<b?a:b
+// (reduce-op.c:130-142) returns its second operand when either one is a NaN
+// or both are zeros (+0 and -0 compare equal), and PE k folds src_k first,
+// then the other members ascending (:219-248); so wherever an element's
+// inputs hold a NaN or both signed zeros, PE k's answer can differ from
+// PE_start's by a whole value (2 PEs, sources 1.0 and NaN: PE 0 gets
+// min(1.0, NaN) = NaN, PE 1 gets min(NaN, 1.0) = 1.0).  No schedule that
+// hands every member one shared result can give that, so for these pairs
+// every algorithm folds in the calling PE's own order: every member reads
+// every member's whole source ((P-1)·S per PE, against 2(P-1)/P·S for a
+// shared result).
+bool own_order_pair(int type, int op) {
+    return (op == SHMEMX_OP_MIN || op == SHMEMX_OP_MAX) &&
+           (type == SHMEMX_TYPE_FLOAT || type == SHMEMX_TYPE_DOUBLE || type == SHMEMX_TYPE_LONGDOUBLE);
+}
+
 static ncclRedOp_t rccl_op(int op) {
     switch (op) {
     case SHMEMX_OP_SUM: return ncclSum;
@@ -494,17 +511,30 @@ int make_plan(int type, int op, int nreduce, int start, int logstride,
     const bool set_rccl = world || (set_comms_enabled() && !set_comm_refused(start, logstride, size) &&
                                     (!t_capturing || set_comm_cached(start, logstride, size)));
     const bool rccl_ok = set_rccl && rccl_native(type, op) && !g_state.ipc_only;
+    // each member's own fold order (own_order_pair): GATHER's exchange, or
+    // DIRECT / SIGNAL reading every member's whole source
+    const bool own = P > 1 && own_order_pair(type, op);
     if (algo == SHMEMX_ALGO_AUTO && P > 1) {
         const int t = auto_table_algo(world, n * sz);
         const bool pull_ok = g_state.node_shared && P <= kMaxFoldInputs && !t_planning_capture;
         if (((t == SHMEMX_ALGO_RCCL || t == SHMEMX_ALGO_ALLREDUCE) && rccl_ok) ||
-            (t == SHMEMX_ALGO_A2A && !g_state.ipc_only) || (t == SHMEMX_ALGO_DIRECT && pull_ok) ||
+            (t == SHMEMX_ALGO_A2A && !g_state.ipc_only && !own) || (t == SHMEMX_ALGO_DIRECT && pull_ok) ||
             t == SHMEMX_ALGO_GATHER)
             algo = t;
     }
+    if (algo == SHMEMX_ALGO_AUTO && own) algo = SHMEMX_ALGO_GATHER;
+    // A2A's owner hands one result to every member: for these pairs its
+    // exchange is GATHER's
+    if (algo == SHMEMX_ALGO_A2A && own) algo = SHMEMX_ALGO_GATHER;
     if (algo == SHMEMX_ALGO_AUTO) {
         if (g_state.ipc_only) algo = SHMEMX_ALGO_DIRECT;
-        else if (!rccl_ok) algo = SHMEMX_ALGO_A2A;
+        // A partial set keeps A2A under the built-in rule: the reference's
+        // PE_start bits for float sums too, and no blocking communicator
+        // set-up at a set's first call.  Its members-only RCCL communicator
+        // (set_comm.cpp, so far run against the RCCL test double only) is
+        // taken when asked for: an explicit rccl / allreduce, or
+        // $SHMEMX_AUTO_PARTIAL naming one.
+        else if (!rccl_ok || !world) algo = SHMEMX_ALGO_A2A;
         // Small arrays are latency-bound: one RCCL all-reduce (one launch,
         // and RCCL's own small-message all-reduce algorithms) instead of
         // reduce-scatter + all-gather (+ a tail all-reduce).
@@ -543,9 +573,9 @@ int make_plan(int type, int op, int nreduce, int start, int logstride,
         break;
     }
     case SHMEMX_ALGO_DIRECT:
-    case SHMEMX_ALGO_SIGNAL: {   // slice per member; no workspace
-        long long c = (n + P - 1) / P;
-        p->chunk = (c + g - 1) / g * g;
+    case SHMEMX_ALGO_SIGNAL: {   // slice per member (own order: all of it); no workspace
+        const long long c = (n + P - 1) / P;
+        p->chunk = own ? n : (c + g - 1) / g * g;
         break;
     }
     default:  // GATHER (IPC transport: read in place, no workspace)
@@ -585,12 +615,12 @@ bool stream_capturing(hipStream_t s) {
     return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
 }
 
-static void ws_acquire(hipStream_t s) {
+void ws_acquire(hipStream_t s) {
     if (g_state.ws_stream && g_state.ws_stream != s && !stream_capturing(s))
         SHMX_HIP(hipStreamWaitEvent(s, g_state.ws_event, 0));
 }
 
-static void ws_release(hipStream_t s) {
+void ws_release(hipStream_t s) {
     if (stream_capturing(s)) return;
     if (!g_state.ws_event) SHMX_HIP(hipEventCreateWithFlags(&g_state.ws_event, hipEventDisableTiming));
     SHMX_HIP(hipEventRecord(g_state.ws_event, s));
@@ -663,22 +693,24 @@ int reduce_device(int type, int op, void *target, const void *source,
     if (rc) return set_error(rc);
     if (nreduce == 0) return SHMEMX_OK;
     const bool collective = size > 1 || g_state.force_collective;
+    const bool own = size > 1 && own_order_pair(type, op);
     if (collective && p.algo == SHMEMX_ALGO_SIGNAL) {
         if (log_enabled(LOG_REDUCTION))
-            trace(LOG_REDUCTION, "type %d op %d nreduce %d set (%d,%d,%d) member %d algo signal",
-                  type, op, nreduce, start, logstride, size, p.member);
+            trace(LOG_REDUCTION, "type %d op %d nreduce %d set (%d,%d,%d) member %d algo signal%s",
+                  type, op, nreduce, start, logstride, size, p.member, own ? " (own order)" : "");
         return signal_reduce(type, op, static_cast<char *>(target), static_cast<const char *>(source),
-                             nreduce, start, logstride, p, s);
+                             nreduce, start, logstride, p, own, s);
     }
     const bool over_ipc = p.algo == SHMEMX_ALGO_DIRECT ||
                           (p.algo == SHMEMX_ALGO_GATHER && g_state.ipc_only);
     if (collective && over_ipc) {
+        const bool own_order = p.algo == SHMEMX_ALGO_GATHER || own;
         if (log_enabled(LOG_REDUCTION))
-            trace(LOG_REDUCTION, "type %d op %d nreduce %d set (%d,%d,%d) member %d algo %s",
+            trace(LOG_REDUCTION, "type %d op %d nreduce %d set (%d,%d,%d) member %d algo %s%s",
                   type, op, nreduce, start, logstride, size, p.member,
-                  p.algo == SHMEMX_ALGO_DIRECT ? "direct" : "gather (ipc)");
+                  p.algo == SHMEMX_ALGO_DIRECT ? "direct" : "gather (ipc)", own_order ? " (own order)" : "");
         return direct_reduce(type, op, static_cast<char *>(target), static_cast<const char *>(source),
-                             nreduce, start, logstride, p, p.algo == SHMEMX_ALGO_GATHER, s);
+                             nreduce, start, logstride, p, own_order, s);
     }
     if (collective && !g_state.comm) return set_error(SHMEMX_ENOINIT);
     const size_t sz = (size_t)p.elem_size;
@@ -1092,16 +1124,32 @@ int shmemx_reduce_on_stream(int type, int op, void *target, const void *source,
                             logPE_stride, PE_size, algo, stream);
 }
 
-// The local folds need no shmem_init (they run on the caller's stream); after
-// it, a NULL stream means the PE's device, as for every other entry point.
-static void bind_if_inited() {
-    if (g_state.inited) bind_device();
-}
+// The local folds need no shmem_init (they run on the caller's stream) and
+// leave the calling thread's current device as they found it: a
+// caller's stream carries its own device; after shmem_init a NULL stream
+// means the PE's device, made current for the launch and then restored.
+class LocalDevice {
+  public:
+    explicit LocalDevice(void *stream) {
+        if (stream || !g_state.inited) return;
+        if (hipGetDevice(&prev_) != hipSuccess || prev_ == g_state.device) {
+            prev_ = -1;
+            return;
+        }
+        SHMX_HIP(hipSetDevice(g_state.device));
+    }
+    ~LocalDevice() {
+        if (prev_ >= 0) (void)hipSetDevice(prev_);
+    }
+
+  private:
+    int prev_ = -1;
+};
 
 int shmemx_fold_on_stream(int type, int op, void *acc, const void *in,
                           size_t nelems, void *stream) {
     t_last_error = SHMEMX_OK;
-    bind_if_inited();
+    const LocalDevice dev(stream);
     if (!op_on_device(type, op)) return set_error(op_valid(type, op) ? SHMEMX_ENOTSUP : SHMEMX_EINVAL);
     if (nelems == 0) return SHMEMX_OK;
     if (!acc || !in) return set_error(SHMEMX_EINVAL);
@@ -1115,7 +1163,7 @@ static int fold_n(int type, int op, void *out, const void *const *ins, int nins,
                   void *stream, bool peers) {
     auto launch = peers ? launch_fold_peers : launch_fold;
     t_last_error = SHMEMX_OK;
-    bind_if_inited();
+    const LocalDevice dev(stream);
     if (!op_on_device(type, op)) return set_error(op_valid(type, op) ? SHMEMX_ENOTSUP : SHMEMX_EINVAL);
     if (nins < 1 || !ins) return set_error(SHMEMX_EINVAL);
     if (nelems == 0) return SHMEMX_OK;
@@ -1148,7 +1196,7 @@ int shmemx_fold_n_peers_on_stream(int type, int op, void *out, const void *const
 int shmemx_gather_on_stream(const void *const *srcs, void *const *dsts, const size_t *bytes,
                             int nseg, void *stream) {
     t_last_error = SHMEMX_OK;
-    bind_if_inited();
+    const LocalDevice dev(stream);
     if (nseg < 0 || nseg > kMaxFoldInputs || (nseg > 0 && (!srcs || !dsts || !bytes)))
         return set_error(SHMEMX_EINVAL);
     for (int i = 0; i < nseg; ++i)
@@ -1162,6 +1210,10 @@ int shmemx_reduce_plan(int type, int op, int nreduce, int PE_start,
                        int logPE_stride, int PE_size, int pe, int npes,
                        int algo, shmemx_plan_t *plan) {
     if (!plan) return SHMEMX_EINVAL;
+    // make_plan reads this process's set-communicator cache (set_comm.cpp),
+    // which another thread's first RCCL call on a set may be filling: under
+    // the library lock, as every entry point
+    std::lock_guard<std::recursive_mutex> lk(g_mu);
     return make_plan(type, op, nreduce, PE_start, logPE_stride, PE_size, pe, npes, algo, plan);
 }
 

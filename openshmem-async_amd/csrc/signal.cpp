@@ -36,6 +36,10 @@
 //   barrier; fold all of every source -> my target; barrier — as ONE fused
 //   launch (launch_signal_fold: the fence, both handshakes and the fold in
 //   one kernel, with a self-resetting grid barrier).
+// Own order (float / double / long double min and max, own_order_pair): the
+//   one shot at every size, each member folding src_me first, then the other
+//   members ascending (reduce-op.c:219-248); in place, into the private
+//   temporary, copied over the target after the second barrier.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -92,7 +96,7 @@ unsigned int signal_error() {
 }
 
 int signal_reduce(int type, int op, char *tgt, const char *src, int nreduce, int start,
-                  int logstride, const shmemx_plan_t &p, hipStream_t s) {
+                  int logstride, const shmemx_plan_t &p, bool own_order, hipStream_t s) {
     const int P = p.nmembers, m = p.member, step = 1 << logstride;
     if (!node::up() || P > kMaxFoldInputs) return set_error(SHMEMX_ENOTSUP);
     const size_t sz = (size_t)p.elem_size;
@@ -115,14 +119,22 @@ int signal_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
     if (!signal_args(start, step, P, &sa)) return set_error(SHMEMX_ENOTSUP);
     std::vector<char *> hb(P);
     for (int i = 0; i < P; ++i) hb[i] = node::peer_base(node::kHeap, start + i * step);
+    // every whole source, in set order, or in my own (src_me first, then
+    // the other members ascending: reduce-op.c:219-248)
     const void *ins[kMaxFoldInputs];
+    {
+        int k = 0;
+        if (own_order) ins[k++] = hb[m] + soff;
+        for (int i = 0; i < P; ++i)
+            if (!own_order || i != m) ins[k++] = hb[i] + soff;
+    }
     if (tgt != src && bytes <= oneshot_bytes() && fused_oneshot_enabled()) {
         // barrier, fold of every whole source, barrier: one fused launch
         SignalFoldArgs fa{};
         fa.sig = sa;
         fa.gsync = fence_records().gsync;
         fa.out = tgt;
-        for (int i = 0; i < P; ++i) fa.ins[i] = hb[i] + soff;
+        for (int i = 0; i < P; ++i) fa.ins[i] = ins[i];
         fa.nins = P;
         fa.n = n;
         SHMX_HIP(launch_signal_fold(type, op, fa, s));   // reduce-op.c:217-250
@@ -133,11 +145,27 @@ int signal_reduce(int type, int op, char *tgt, const char *src, int nreduce, int
         SHMX_HIP(launch_sys_fence(s, sa.seen));
         SHMX_HIP(launch_signal(sa, s));
     };
-    if (tgt != src && bytes <= oneshot_bytes()) {   // the one shot, unfused
+    if (tgt != src && (bytes <= oneshot_bytes() || own_order)) {   // the one shot, unfused
         barrier();   // reduce-op.c:217
-        for (int i = 0; i < P; ++i) ins[i] = hb[i] + soff;
         SHMX_HIP(launch_fold_peers(type, op, tgt, ins, P, n, s));
         barrier();   // reduce-op.c:250
+        return SHMEMX_OK;
+    }
+    if (own_order) {
+        // in place: the peers read my source (= my target) until the second
+        // barrier, so the fold goes to the private temporary (the
+        // reference's own temporary target, reduce-op.c:187-203, 251-259).
+        // A captured call cannot allocate it: ENOTSUP before any barrier
+        // (the peers' barriers then time out, as for any refused operand).
+        if (stream_capturing(s) && g_state.tmp_bytes < bytes) return set_error(SHMEMX_ENOTSUP);
+        void *t = grow(g_state.tmp, g_state.tmp_bytes, bytes);
+        if (!t) return set_error(SHMEMX_ENOMEM);
+        ws_acquire(s);
+        barrier();   // reduce-op.c:217
+        SHMX_HIP(launch_fold_peers(type, op, t, ins, P, n, s));
+        barrier();   // reduce-op.c:250
+        SHMX_HIP(hipMemcpyAsync(tgt, t, bytes, hipMemcpyDeviceToDevice, s));
+        ws_release(s);
         return SHMEMX_OK;
     }
     const size_t g = sz >= 16 ? 1 : 16 / sz;

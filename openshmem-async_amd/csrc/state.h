@@ -144,6 +144,14 @@ bool device_accessible(const void *ptr);
 bool host_pinned(const void *ptr);
 void *grow(void *&buf, size_t &have, size_t need);   // grow-only device buffer
 bool stream_capturing(hipStream_t s);
+// The workspaces (ws, tmp) serve every stream: a use on stream s first waits
+// for the last use when that was on another stream, and records itself.
+void ws_acquire(hipStream_t s);
+void ws_release(hipStream_t s);
+// min / max of float, double, long double: the reference's answer depends on
+// the calling PE's own fold order (runtime.cpp), so every multi-PE algorithm
+// folds these in that order
+bool own_order_pair(int type, int op);
 // out = left fold of ins[0..nins) in groups of kMaxFoldInputs (any nins);
 // peers: the inputs are in other GPUs' HBM (launch_fold_peers)
 void fold_chain(int type, int op, void *out, const void **ins, int nins, size_t n, hipStream_t s,
@@ -203,8 +211,9 @@ void node_done(int start, int step, int P, hipStream_t s, double *stream_us = nu
 bool map_regions(const std::vector<std::pair<node::Region, int>> &regs, int start, int step, int P);
 // SIGNAL algorithm (signal.cpp): DIRECT's pulls with device-side barriers,
 // stream-ordered and graph-capturable; symmetric-heap operands only.
+// own_order: every member folds the whole array in its own reference order.
 int signal_reduce(int type, int op, char *tgt, const char *src, int nreduce, int start,
-                  int logstride, const shmemx_plan_t &p, hipStream_t s);
+                  int logstride, const shmemx_plan_t &p, bool own_order, hipStream_t s);
 // After the stream has drained: 0, or 1 if a SIGNAL barrier timed out, 2 if
 // a fence before one missed an XCD.  (Clears it.)
 unsigned int signal_error();

@@ -147,6 +147,23 @@ def sources(type_name: str, kind: int, npes: int, n: int, base_seed: int = 0x5EE
     return out
 
 
+def special_sources(type_name: str, npes: int, n: int, seed: int) -> np.ndarray:
+    """[npes, n] sources of float / double / long double drawn from NaNs of
+    both signs, both zeros, +-1, 2, +-inf and the smallest normal: the inputs
+    on which a<b?a:b / a>b?a:b (reduce-op.c:130-142) make each PE's answer
+    depend on its own fold order (reduce-op.c:219-248)."""
+    dt = NP_DTYPE[type_name]
+    if type_name == "longdouble":
+        nan = np.longdouble("nan")
+        pool = np.array([nan, -nan, 0.0, -0.0, 1.0, -1.0, 2.0, np.inf, -np.inf,
+                         np.finfo(np.longdouble).tiny], dtype=dt)
+    else:
+        pool = np.array([np.nan, -np.nan, 0.0, -0.0, 1.0, -1.0, 2.0, np.inf, -np.inf,
+                         np.finfo(dt).tiny], dtype=dt)
+    idx = (splitmix64(seed, npes * n) % np.uint64(len(pool))).astype(np.int64)
+    return np.ascontiguousarray(pool[idx].reshape(npes, n))
+
+
 # --------------------------------------------------------------- the oracle
 def reduce_sim(type_name: str, op: str, srcs: np.ndarray, PE_start: int, logPE_stride: int,
                PE_size: int, targets: np.ndarray | None = None) -> np.ndarray:

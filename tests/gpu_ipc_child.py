@@ -61,12 +61,33 @@ def active_sets():
     return s
 
 
+# min / max of float, double, long double: a<b?a:b under NaN and +-0 makes
+# each PE's reference answer depend on its own fold order (reduce-op.c:130-142,
+# 219-248), and every algorithm gives each PE that answer (runtime.cpp
+# own_order_pair)
+OWN_ORDER = {(t, o) for t in ("float", "double", "longdouble") for o in ("min", "max")}
+
+
+def elements_differing(t, a, b):
+    """How many elements of a and b differ in their value bytes (long double:
+    the 10 bytes of the x87 value)."""
+    if not len(a):
+        return 0
+    w = 10 if t == "longdouble" else a.itemsize
+    return int((a.view(np.uint8).reshape(len(a), -1)[:, :w] != b.view(np.uint8).reshape(len(b), -1)[:, :w])
+               .any(axis=1).sum())
+
+
 def expected(t, op, srcs, st, algo):
     start, log, size = st
     ref = oracle.reduce_sim(t, op, srcs, start, log, size)
-    # DIRECT / SIGNAL / A2A: PE_start's fold order on every member; GATHER: each
-    # PE's own.  RCCL / ALLREDUCE: RCCL's order (the test double's ring and
-    # rotated orders), held against PE_start's fold within the stated bound.
+    # DIRECT / SIGNAL / A2A: PE_start's fold order on every member; GATHER, and
+    # every algorithm on the OWN_ORDER pairs: each PE's own.  RCCL / ALLREDUCE:
+    # RCCL's order (the test double's ring and rotated orders), held against
+    # PE_start's fold within the stated bound.
+    if size > 1 and (t, op) in OWN_ORDER:
+        extra["own_order_differs"] = extra.get("own_order_differs", 0) + elements_differing(t, ref[pe], ref[start])
+        return ref[pe]
     return ref[start] if algo != "gather" else ref[pe]
 
 
@@ -126,11 +147,13 @@ def read(ptr, t, n):
     return a
 
 
-def run_case(t, op, n, st, algo, mode, seed, expect_algo=None):
+def run_case(t, op, n, st, algo, mode, seed, expect_algo=None, special=False):
     """One collective call; every PE runs the same sequence, non-members skip.
-    expect_algo: the algorithm `auto` resolved to, for the fold order."""
+    expect_algo: the algorithm `auto` resolved to, for the fold order.
+    special: NaN / +-0 sources (oracle.special_sources)."""
     global ncases
-    srcs = oracle.sources(t, 1, npes, n, base_seed=seed)
+    srcs = oracle.special_sources(t, npes, n, seed) if special else \
+        oracle.sources(t, 1, npes, n, base_seed=seed)
     if not member(*st):
         return
     ncases += 1
@@ -619,7 +642,8 @@ elif scenario == "refops":
     # (tests/golden/ref_element_ops.json: reduce-op.c:71-150 compiled from its
     # text).  2 PEs: PE 0's source is the fixture's a, PE 1's is b, for all 44
     # pairs on special values and random bits.  DIRECT and SIGNAL give every PE
-    # PE_start's order, op(a, b); own-order GATHER gives PE 1 op(b, a).  The
+    # PE_start's order, op(a, b); own-order GATHER, and every algorithm on the
+    # float / double / long double min and max, give PE 1 op(b, a).  The
     # one-shot/two-shot and fused/unfused schedules come from the test's env.
     import base64
     with open(os.path.join(HERE, "golden", "ref_element_ops.json")) as f:
@@ -632,7 +656,8 @@ elif scenario == "refops":
         for op, o in c["ops"].items():
             for algo in ("direct", "signal", "gather"):
                 ncases += 1
-                key = "ba" if (algo == "gather" and pe == 1) else "ab"
+                own = algo == "gather" or (t, op) in OWN_ORDER
+                key = "ba" if (own and pe == 1) else "ab"
                 want = np.frombuffer(base64.b64decode(o[key]), dtype=dt)
                 heap_write(HEAP_SRC, mine, mine.nbytes)
                 heap_write(HEAP_TGT, np.full(mine.nbytes, 0xAB, np.uint8), mine.nbytes)
@@ -649,6 +674,34 @@ elif scenario == "refops":
                 if not ok or shm.last_error():
                     fails.append(f"refops {t} {op} algo={algo}: differs from the reference "
                                  f"(last_error {shm.last_error()})")
+elif scenario == "ownorder":
+    # min / max of float, double and long double on NaN / +-0 sources, where
+    # each PE's reference answer depends on its own fold order: every
+    # algorithm the transport has (auto first), every active set, one-shot
+    # (fused) and larger sizes, heap / in-place / device operands; every PE
+    # against its own oracle result.  extra["own_order_differs"] counts the
+    # elements where that differs from PE_start's (the test requires > 0).
+    rccl = os.environ.get("SHMEMX_TRANSPORT") != "ipc"
+    algos = ("auto", "a2a", "gather", "direct", "signal") if rccl else ("auto", "gather", "direct", "signal")
+    for t in ("float", "double", "longdouble"):
+        for op in ("min", "max"):
+            for st in active_sets():
+                for algo in algos:
+                    for n, mode in ((1013, "heap"), (70001, "inplace"), (40007, "device")):
+                        if algo == "signal" and mode == "device":
+                            mode = "heap"
+                        try:
+                            shm.plan(t, op, n, *st, st[0], npes, algo)
+                        except shm.ShmemError:
+                            continue
+                        seed += 1
+                        run_case(t, op, n, st, algo, mode, seed, special=True)
+        if not rccl:
+            extra["auto_algo"] = shm.plan(t, "min", 1013, 0, 0, npes, pe, npes, "auto").algo
+    # the blocking drop-in entry point on host arrays, auto
+    for t in ("float", "double"):
+        seed += 1
+        run_case(t, "max", 4103, (0, 0, npes), "auto", "host", seed, special=True)
 elif scenario == "config0":
     # BASELINE.json configs[0]: shmem_int_sum_to_all, nreduce = 1024, on 2 PEs
     # (the reference's "oshrun loopback"), through the C entry point itself
@@ -1359,6 +1412,8 @@ fences["fused_calls"] = stats["fused_calls"]
 if (scenario in ("full", "signal") and npes > 1 and os.environ.get("SHMEMX_DIRECT_ONESHOT_KB") != "0"
         and os.environ.get("SHMEMX_FUSED_ONESHOT") != "0" and not stats["fused_calls"]):
     fails.append("no one-shot call ran as a fused launch")
+if scenario == "ownorder" and npes > 1 and not stats["fused_calls"]:
+    fails.append("no own-order one-shot call ran as a fused launch")
 # and mid-size heap calls (100003 doubles; SIGNAL's 70001-element cases) as one
 # fused two-shot launch
 fences["fused_twoshot_calls"] = stats["fused_twoshot_calls"]

@@ -179,19 +179,31 @@ def test_plan_algorithm_selection(shm):
     assert P("double", "sum", (4 << 20) // 8, 0, 0, 8, 3, 8).algo == "allreduce"
     assert P("long", "max", 1000, 0, 0, 4, 0, 4).algo == "allreduce"
     assert P("int", "prod", 1000, 0, 0, 2, 1, 2).algo == "allreduce"
-    # bitwise (no RCCL op), float min/max (NaN semantics), short (no RCCL type),
-    # complex -> A2A
-    for t, o in [("long", "xor"), ("int", "and"), ("double", "min"), ("float", "max"),
-                 ("short", "sum"), ("complexd", "prod")]:
+    # bitwise (no RCCL op), short (no RCCL type), complex -> A2A
+    for t, o in [("long", "xor"), ("int", "and"), ("short", "sum"), ("complexd", "prod")]:
         assert P(t, o, 1000, 0, 0, 4, 2, 4).algo == "a2a", (t, o)
-    # strided or partial sets: RCCL on the set's members-only communicator for
-    # the RCCL-native pairs (set_comm.cpp), A2A for the rest
-    assert P("double", "sum", 1000, 0, 1, 4, 2, 8).algo == "allreduce"
-    assert P("double", "sum", 1000, 1, 0, 3, 2, 8).algo == "allreduce"
-    assert P("double", "sum", 1 << 20, 1, 0, 3, 2, 8).algo == "rccl"
+    # float / double / long double min and max: each PE's own fold order
+    # (a<b?a:b under NaN and +-0), so GATHER under auto and for an explicit
+    # a2a; DIRECT and SIGNAL plan the whole array on every member
+    for t in ("float", "double", "longdouble"):
+        for o in ("min", "max"):
+            assert P(t, o, 1000, 0, 0, 4, 2, 4).algo == "gather", (t, o)
+            assert P(t, o, 1000, 0, 0, 4, 2, 4, "a2a").algo == "gather", (t, o)
+            for a in ("direct", "signal"):
+                q = P(t, o, 1000, 0, 0, 4, 2, 4, a)
+                assert q.algo == a and q.chunk == 1000, (t, o, a)
+    assert P("double", "min", 1000, 0, 0, 4, 2, 4, "direct").chunk == 1000
+    assert P("double", "sum", 1000, 0, 0, 4, 2, 4, "direct").chunk == 250
+    # strided or partial sets: A2A under the built-in rule (PE_start bits, no
+    # communicator set-up); the set's members-only RCCL communicator
+    # (set_comm.cpp) when asked for by name
+    assert P("double", "sum", 1000, 0, 1, 4, 2, 8).algo == "a2a"
+    assert P("double", "sum", 1000, 1, 0, 3, 2, 8).algo == "a2a"
+    assert P("double", "sum", 1 << 20, 1, 0, 3, 2, 8).algo == "a2a"
     assert P("double", "sum", 1000, 1, 0, 3, 2, 8, "rccl").algo == "rccl"
+    assert P("double", "sum", 1000, 1, 0, 3, 2, 8, "allreduce").algo == "allreduce"
     assert P("long", "xor", 1000, 1, 0, 3, 2, 8).algo == "a2a"
-    assert P("float", "min", 1000, 0, 1, 4, 2, 8).algo == "a2a"
+    assert P("float", "min", 1000, 0, 1, 4, 2, 8).algo == "gather"
     # explicit choices
     assert P("double", "sum", 1000, 0, 0, 4, 2, 4, "gather").algo == "gather"
     assert P("double", "sum", 1000, 0, 0, 4, 2, 4, "a2a").algo == "a2a"
@@ -213,7 +225,8 @@ def test_plan_errors(shm):
             P("double", "sum", *args)
         assert e.value.code == code, args
     assert P("longdouble", "sum", 10, 0, 0, 1, 0, 1).algo in ("a2a", "rccl")
-    assert P("longdouble", "max", 10, 0, 0, 4, 1, 4).algo == "a2a"   # no RCCL type
+    assert P("longdouble", "max", 10, 0, 0, 4, 1, 4).algo == "gather"   # own order
+    assert P("longdouble", "sum", 10, 0, 0, 4, 1, 4).algo == "a2a"   # no RCCL type
     with pytest.raises(shm.ShmemError) as e:
         P("double", "xor", 10, 0, 0, 1, 0, 1)
     assert e.value.code == 1

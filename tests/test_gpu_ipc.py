@@ -140,6 +140,31 @@ def test_ipc_reference_element_ops_two_pes(tmp_path, schedule):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("transport,npes", [("ipc", 2), ("ipc", 3), ("ipc", 8), ("rccl", 2), ("rccl", 3),
+                                            ("rccl", 8)])
+def test_own_order_min_max_on_nan_and_signed_zeros(tmp_path, transport, npes):
+    """min / max of float, double and long double on NaN / +-0 sources
+    (oracle.special_sources), where a<b?a:b gives PE k a different answer
+    from PE_start's (reduce-op.c:130-142, 219-248): every PE gets its OWN
+    reference result under auto and every explicit algorithm of the
+    transport, every active set, fused one-shot and larger sizes, heap,
+    in-place and device operands (the RCCL transport on the RCCL test
+    double).  The inputs discriminate: the PEs' reference answers differ
+    from PE_start's on many elements, so a schedule that hands every member
+    PE_start's result fails here."""
+    env = {"SHMEMX_TRANSPORT": transport, "SHMEMX_HEAP_MEMORY": "device"}
+    if transport == "rccl":
+        env["FAKE_RCCL"] = os.path.join(HERE, "native", "libfake_rccl.so")
+    reports = run_pes(tmp_path, npes, "ownorder", env)
+    for r in reports:
+        assert r["ncases"] > 0
+        assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
+    assert sum(r["own_order_differs"] for r in reports) > 1000
+    # PE_start itself folds in set order; every other PE differs somewhere
+    assert all(r["own_order_differs"] > 0 for r in reports if r["pe"] > 0)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("transport,heap", [("ipc", "device"), ("ipc", "mirrored"), ("rccl", "device")])
 def test_baseline_config0_int_sum_1024_two_pes(tmp_path, transport, heap):
     """BASELINE.json configs[0]: shmem_int_sum_to_all, nreduce = 1024, 2 PEs,
@@ -235,7 +260,8 @@ def test_rccl_transport_with_rccl_double(tmp_path, npes):
     RCCL — all against the oracle: bit for bit, except float sum / prod
     through RCCL's collectives, which the double folds in ring order (not
     PE_start's) and which must lie within the stated ULP bound.  Partial sets
-    take RCCL on their members-only communicators."""
+    take A2A under auto and RCCL's collectives on their members-only
+    communicators when named."""
     fake = os.path.join(HERE, "native", "libfake_rccl.so")
     assert os.path.exists(fake), "tests/native/libfake_rccl.so not built (make -C tests/native)"
     # at 3 PEs with the heap segment registered with RCCL at its first
@@ -275,8 +301,10 @@ def test_set_comms_cap(tmp_path, cap):
     communicator the others are not building; every call against the oracle
     (4 PE processes, RCCL test double)."""
     fake = os.path.join(HERE, "native", "libfake_rccl.so")
+    # auto takes a partial set's communicator only when the table asks for it
     reports = run_pes(tmp_path, 4, "setcap", {"SHMEMX_TRANSPORT": "rccl", "FAKE_RCCL": fake,
-                                             "SHMEMX_SET_COMMS_MAX": cap}, timeout=300)
+                                             "SHMEMX_SET_COMMS_MAX": cap,
+                                             "SHMEMX_AUTO_PARTIAL": "0:allreduce,4194304:rccl"}, timeout=300)
     for r in reports:
         assert r["ncases"] > 0
         assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"

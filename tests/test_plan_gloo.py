@@ -13,6 +13,10 @@ received shards in the order the HIP kernel uses:
   GATHER every source -> every member; fold me first, then ascending
                                        -> must equal the reference PE me
                                           result, bit for bit
+         (float / double / long double min and max plan every algorithm
+         this way: a2a turns into gather, DIRECT and SIGNAL read every
+         member's whole source; kind 2 = NaN / +-0 sources on which PE k's
+         reference answer differs from PE_start's)
   RCCL   main = P * chunk elements reduce-scattered (each shard folded in
          ring order, from member m + 1 round to m, as RCCL's ring does) +
          all-gathered, the tail all-reduced (descending member order)
@@ -55,7 +59,8 @@ CASES = [
     ("complexf", "sum", 1, 5, None, "gather"),
     ("double", "prod", 0, 3, None, "a2a"),     # fewer elements than PEs
     ("double", "sum", 0, 0, None, "a2a"),      # nreduce = 0
-    ("int", "min", 1, 300, "strided", "auto"),   # partial sets: RCCL on their own communicator
+    ("int", "min", 1, 300, "strided", "auto"),   # partial sets: A2A under auto
+    ("int", "min", 1, 300, "strided", "allreduce"),   # ... RCCL on their own communicator when named
     ("double", "sum", 0, 300, "offset", "auto"),
     ("double", "sum", 1, 4103, "strided", "rccl"),
     ("float", "sum", 1, 4099, "offset", "rccl"),
@@ -69,7 +74,16 @@ CASES = [
     ("float", "max", 1, 3, None, "signal"),      # fewer elements than PEs
     ("int", "prod", 1, 0, None, "direct"),
     ("longdouble", "sum", 0, 257, "offset", "signal"),
+    # min / max of float, double, long double on NaN / +-0 inputs (kind 2):
+    # each member's own reference answer under every algorithm
+    ("float", "min", 2, 1001, None, "auto"),
+    ("double", "max", 2, 777, "offset", "a2a"),
+    ("longdouble", "min", 2, 129, "strided", "direct"),
+    ("float", "max", 2, 300, None, "signal"),
+    ("double", "min", 2, 65, None, "gather"),
+    ("longdouble", "max", 2, 1000, None, "auto"),
 ]
+OWN_ORDER = {(t, o) for t in ("float", "double", "longdouble") for o in ("min", "max")}
 
 
 def _free_port():
@@ -127,8 +141,16 @@ def _run_case(dist, shm, oracle, rank, world, case):
     t, op, kind, n, setkind, algo = case
     s = _set_for(setkind, world)
     members = [s[0] + i * (1 << s[1]) for i in range(s[2])]
-    srcs = oracle.sources(t, kind, world, n, base_seed=0x5EED0000 + n)
+    if kind == 2:
+        srcs = oracle.special_sources(t, world, n, 0x5EED0000 + n)
+    else:
+        srcs = oracle.sources(t, kind, world, n, base_seed=0x5EED0000 + n)
     want = oracle.reduce_sim(t, op, srcs, *s)
+    own = (t, op) in OWN_ORDER and len(members) > 1
+    if kind == 2 and len(members) > 1:
+        # the inputs discriminate: some member's reference answer differs
+        # from PE_start's, so a shared result would fail this case
+        assert any(_bits(want[q], t) != _bits(want[members[0]], t) for q in members), case
     if rank not in members:
         with pytest.raises(shm.ShmemError):
             shm.plan(t, op, n, *s, rank, world, algo)
@@ -139,7 +161,7 @@ def _run_case(dist, shm, oracle, rank, world, case):
     out = np.zeros(n, dtype=dt)
     if P == 1:
         out[:] = src
-    elif p.algo in ("a2a", "direct", "signal"):
+    elif p.algo in ("a2a", "direct", "signal") and not own:
         c = p.chunk
         cnt = [max(0, min(c, n - i * c)) for i in range(P)]
         lo = m * c
@@ -157,14 +179,15 @@ def _run_case(dist, shm, oracle, rank, world, case):
             if i != m and cnt[i]:
                 out[i * c:i * c + cnt[i]] = got[members[i]].view(dt)
         assert _bits(out, t) == _bits(want[members[0]], t), case
-    elif p.algo == "gather":
+    elif p.algo == "gather" or own:
+        assert p.algo != "a2a", case
         sends = {members[i]: src for i in range(P) if i != m}
         recvs = {members[i]: n * dt.itemsize for i in range(P) if i != m}
         got = _exchange(dist, rank, sends, recvs) if n else {}
         full = np.stack([src if i == m else got[members[i]].view(dt) for i in range(P)]) \
             if n else np.zeros((P, 0), dt)
         out = oracle.reduce_sim(t, op, full, 0, 0, P)[m]
-        assert out.tobytes() == want[rank].tobytes(), case
+        assert _bits(out, t) == _bits(want[rank], t), case
     elif p.algo == "allreduce":
         # one all-reduce: every member gets the whole reduction, in RCCL's
         # order (here: descending member order, unlike the reference's)
