@@ -311,13 +311,6 @@ int shmemx_fold_n_peers_on_stream(int type, int op, void *out,
 int shmemx_gather_on_stream(const void *const *srcs, void *const *dsts,
                             const size_t *bytes, int nseg, void *stream);
 
-/* Fold-kernel launch shape (defaults from $SHMEMX_FOLD_MAX_BLOCKS,
- * $SHMEMX_FOLD_NT, $SHMEMX_FOLD_UNROLL): grid cap (0 = no cap), non-temporal
- * mode (-1 = by size, the default: both non-temporal once the arrays exceed
- * the 256 MiB Infinity Cache; else bit 0 loads, bit 1 stores), 16-byte
- * vectors per lane per input of the 2-input fold (2, 4 or 8; default 4). */
-int shmemx_fold_set_tuning(int max_blocks, int nontemporal, int unroll);
-
 /* Register (on != 0) or deregister the symmetric heap's HBM segment with
  * the library's RCCL communicator (ncclCommRegister), so RCCL may use
  * collectives' heap operands in place instead of staging them through its

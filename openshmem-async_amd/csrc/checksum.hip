@@ -99,7 +99,7 @@ constexpr int kShards = 16;
 constexpr int kLine = 16;                       // 128 B between counters
 constexpr int kTop = kShards * kLine;           // the top counter's word
 constexpr int kPartials = (kShards + 1) * kLine;   // first partial's word
-template <bool LD, int UNROLL>
+template <bool LD>
 __global__ __launch_bounds__(kCkBlock) void checksum_kernel(const unsigned char *data, size_t nwords,
                                                             size_t tail, unsigned long long *work,
                                                             unsigned long long *out,
@@ -117,16 +117,9 @@ __global__ __launch_bounds__(kCkBlock) void checksum_kernel(const unsigned char 
     // VALU-heavy enough to share the bound with HBM).
     uint64_t c = (2 * (uint64_t)tid + 1) * kPhi;
     const uint64_t dc = 2 * (uint64_t)nthr * kPhi;
-    size_t i = tid;
-    if (UNROLL == 2) {
-        // two vectors in flight per lane per trip
-        for (; i + nthr < npairs; i += 2 * nthr, c += 2 * dc) {
-            const u32x4 a = __builtin_nontemporal_load(v + i);
-            const u32x4 b = __builtin_nontemporal_load(v + i + nthr);
-            h ^= mix_pair<LD>(a, c) ^ mix_pair<LD>(b, c + dc);
-        }
-    }
-    for (; i < npairs; i += nthr, c += dc)
+    // (two vectors in flight per lane per trip measured no faster:
+    // profiles/r03_checksum_mix_lab.txt)
+    for (size_t i = tid; i < npairs; i += nthr, c += dc)
         h ^= mix_pair<LD>(__builtin_nontemporal_load(v + i), c);
     if (tid == 0) {
         if (nwords & 1) {  // odd word count (only when !LD)
@@ -241,26 +234,15 @@ hipError_t launch_checksum(int type, const void *ptr, size_t n, unsigned long lo
     size_t blocks = (nwords / 2 + kCkBlock - 1) / kCkBlock;
     // 2048 workgroups: 44.6 us at 32 Mi doubles against 45.3 at 4096 (fewer
     // arrivals); 1024 and fewer lose bytes in flight (profiles/r03_checksum.txt)
-    static const size_t cap = [] {
-        const char *e = std::getenv("SHMEMX_CHECKSUM_BLOCKS");   // tuning experiments
-        const long v = e ? std::atol(e) : 0;
-        return v > 0 && v <= kChecksumMaxBlocks ? (size_t)v : (size_t)2048;
-    }();
-    if (blocks > cap) blocks = cap;
+    constexpr size_t kCap = 2048;
+    if (blocks > kCap) blocks = kCap;
     if (blocks < 1) blocks = 1;
     const unsigned char *p = static_cast<const unsigned char *>(ptr);
-    static const int unroll = [] {
-        const char *e = std::getenv("SHMEMX_CHECKSUM_UNROLL");   // tuning experiments
-        return e && std::atoi(e) == 2 ? 2 : 1;
-    }();
     if (ld)
-        hipLaunchKernelGGL((checksum_kernel<true, 1>), dim3((unsigned)blocks), dim3(kCkBlock), 0, stream, p,
-                           nwords, tail, work, out, epoch);
-    else if (unroll == 2)
-        hipLaunchKernelGGL((checksum_kernel<false, 2>), dim3((unsigned)blocks), dim3(kCkBlock), 0, stream, p,
+        hipLaunchKernelGGL(checksum_kernel<true>, dim3((unsigned)blocks), dim3(kCkBlock), 0, stream, p,
                            nwords, tail, work, out, epoch);
     else
-        hipLaunchKernelGGL((checksum_kernel<false, 1>), dim3((unsigned)blocks), dim3(kCkBlock), 0, stream, p,
+        hipLaunchKernelGGL(checksum_kernel<false>, dim3((unsigned)blocks), dim3(kCkBlock), 0, stream, p,
                            nwords, tail, work, out, epoch);
     return hipGetLastError();
 }

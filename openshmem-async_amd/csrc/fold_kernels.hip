@@ -283,8 +283,11 @@ __global__ __launch_bounds__(kBlock) void fold_kernel(FoldArgs args) {
     signal_host_done(args);
 }
 
-// 16-B vectors per lane per input for the runtime-nins kernel.
+// 16-B vectors per lane per input for the runtime-nins kernel, and for the
+// two-input fold (2 and 8 measured no faster at 32-64 Mi elements:
+// DESIGN_history.md §4.2).
 constexpr int kUnrollN = 4;
+constexpr int kUnrollFold2 = 4;
 
 // The P-input fold over inputs that live in the peers' HBM (DIRECT's and
 // SIGNAL's fold phase).  The runtime-nins kernel above issues input k + 1's
@@ -356,46 +359,34 @@ __global__ __launch_bounds__(kBlock) void fold_peers_kernel(FoldArgs args) {
 }
 
 
+// One chunk of kBlock x unroll vectors per block (persistent grids, caps and
+// XCD remaps measured no faster: DESIGN_history.md §4.2); the scalar-only
+// case (inputs of different alignment) grid-strides over at most 2048 blocks.
 static size_t grid_for(const FoldArgs &a, int unroll) {
-    const FoldTuning &tune = fold_tuning();
     size_t work_blocks;
     if (a.nvec > 0)
         work_blocks = (a.nvec + (size_t)kBlock * unroll - 1) / ((size_t)kBlock * unroll);
     else
         work_blocks = (a.head + a.tail + kBlock - 1) / kBlock;
-    // The scalar-only case (inputs of different alignment) is capped hard; the
-    // vector body runs one chunk per block unless a cap is set.
-    size_t cap = tune.max_blocks > 0 ? (size_t)tune.max_blocks : (size_t)1 << 30;
-    if (a.nvec == 0 && cap > 2048) cap = 2048;
+    const size_t cap = a.nvec == 0 ? 2048 : (size_t)1 << 30;
     size_t blocks = work_blocks < cap ? work_blocks : cap;
     if (blocks < 1) blocks = 1;
     if (blocks > (size_t)INT_MAX) blocks = INT_MAX;
     return blocks;
 }
 
-__global__ void host_signal_kernel(unsigned long long *word, unsigned long long value) {
-    if (threadIdx.x == 0) __hip_atomic_store(word, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 // The marker after the work: the stream's own value write (the command
 // processor stores the word once everything before it on the stream has
 // completed, its kernels' end-of-kernel releases included), 0.3-0.8 us
-// faster per small call than the one-thread kernel above, which
-// $SHMEMX_SIGNAL_WRITEVALUE=0 restores (profiles/r05_marker_ab.txt).
-// Either marker publishes a multi-block result only through the preceding
-// kernel's end-of-kernel release, which is system scope (HIP's default for
-// a dispatch) and writes back every XCD's L2: the marker kernel's own
-// release reaches only the XCD it ran on, so it would not cover such a
-// result either.  One-workgroup folds store the signal themselves after
-// their own system-scope release.
+// faster per small call than a one-thread kernel storing it
+// (profiles/r05_marker_ab.txt).  It publishes a multi-block result only
+// through the preceding kernel's end-of-kernel release, which is system
+// scope (HIP's default for a dispatch) and writes back every XCD's L2 (a
+// marker kernel's own release would reach only the XCD it ran on, so it
+// would not cover such a result either).  One-workgroup folds store the
+// signal themselves after their own system-scope release.
 hipError_t enqueue_marker(unsigned long long *word, unsigned long long value, hipStream_t stream) {
-    static const bool packet = [] {
-        const char *e = std::getenv("SHMEMX_SIGNAL_WRITEVALUE");
-        return !(e && *e == '0');
-    }();
-    if (packet) return hipStreamWriteValue64(stream, word, value, 0);
-    hipLaunchKernelGGL(host_signal_kernel, dim3(1), dim3(64), 0, stream, word, value);
-    return hipGetLastError();
+    return hipStreamWriteValue64(stream, word, value, 0);
 }
 
 template <typename T, int OP, int NT>
@@ -408,7 +399,7 @@ hipError_t launch_typed(const FoldArgs &a0, hipStream_t stream) {
     if (!a0.sig_word) return launch_typed_grid<T, OP, NT>(a0, stream);
     // the grid launch_typed_grid will use (fold_kernel in every case but
     // the peers kernel, which never signals)
-    const int u = a0.nins != 2 ? kUnrollN : std::is_same<T, ld80>::value ? 4 : fold_tuning().unroll;
+    const int u = a0.nins != 2 ? kUnrollN : kUnrollFold2;
     if (!a0.peers && grid_for(a0, u) == 1) return launch_typed_grid<T, OP, NT>(a0, stream);
     FoldArgs a = a0;
     a.sig_word = nullptr;
@@ -420,22 +411,10 @@ hipError_t launch_typed(const FoldArgs &a0, hipStream_t stream) {
 template <typename T, int OP, int NT>
 hipError_t launch_typed_grid(const FoldArgs &a, hipStream_t stream) {
     if (a.nins == 2) {
-        // the two-input fold (reduce-op.c:231-235): the hot kernel.  The
-        // soft-float long double kernels exist at unroll 4 only.
-        if constexpr (std::is_same<T, ld80>::value) {
-            launch_k(kKindFold, fold_kernel<T, OP, 2, 4, NT>, dim3((unsigned)grid_for(a, 4)), dim3(kBlock),
-                     stream, a);
-        } else {
-            const int u = fold_tuning().unroll;
-            const dim3 grid((unsigned)grid_for(a, u));
-            if (u == 2)
-                launch_k(kKindFold, fold_kernel<T, OP, 2, 2, NT>, grid, dim3(kBlock), stream, a);
-            else if (u == 8)
-                launch_k(kKindFold, fold_kernel<T, OP, 2, 8, NT>, grid, dim3(kBlock), stream, a);
-            else
-                launch_k(kKindFold, fold_kernel<T, OP, 2, 4, NT>, grid, dim3(kBlock), stream, a);
-        }
-    } else if (a.peers && !kHeavyOp<T, OP> && (NT == 0 || NT == 3)) {
+        // the two-input fold (reduce-op.c:231-235): the hot kernel
+        launch_k(kKindFold, fold_kernel<T, OP, 2, kUnrollFold2, NT>, dim3((unsigned)grid_for(a, kUnrollFold2)),
+                 dim3(kBlock), stream, a);
+    } else if (a.peers && !kHeavyOp<T, OP>) {
         if (a.nins <= 4)
             launch_k(kKindPeers, fold_peers_kernel<T, OP, 4, NT>,
                      dim3((unsigned)grid_for(a, peers_unroll(4))), dim3(kBlock), stream, a);
@@ -461,27 +440,16 @@ hipError_t launch_typed_grid(const FoldArgs &a, hipStream_t stream) {
 // default's stores evict those lines and pay their write-back); from a clean
 // cache the default leads by 5-7 %, back to back the two tie.  So
 // non-temporal, whose worst case is the better one, from 32 MiB up; below
-// it a call is launch-bound and the default keeps L2/MALL hits.
+// it a call is launch-bound and the default keeps L2/MALL hits.  (Loads or
+// stores alone non-temporal, and the sc0/sc1 bits, measured no better:
+// profiles/r03_policy_lab*.txt.)
 constexpr size_t kNtThresholdBytes = size_t(32) << 20;
 
 template <typename T, int OP>
 hipError_t launch_nt(const FoldArgs &a, hipStream_t stream) {
-    int mode = fold_tuning().nontemporal;
-    if (mode < 0) {
-        const size_t n = a.head + a.nvec * (16 / sizeof(T)) + a.tail;
-        mode = (size_t)(a.nins + 1) * n * sizeof(T) >= kNtThresholdBytes ? 3 : 0;
-    }
-    if constexpr (std::is_same<T, ld80>::value) {  // fewer soft-float variants
-        return mode ? launch_typed<T, OP, 3>(a, stream) : launch_typed<T, OP, 0>(a, stream);
-    } else {
-        if (a.peers) return mode ? launch_typed<T, OP, 3>(a, stream) : launch_typed<T, OP, 0>(a, stream);
-        switch (mode & 3) {
-        case 0: return launch_typed<T, OP, 0>(a, stream);
-        case 1: return launch_typed<T, OP, 1>(a, stream);
-        case 2: return launch_typed<T, OP, 2>(a, stream);
-        default: return launch_typed<T, OP, 3>(a, stream);
-        }
-    }
+    const size_t n = a.head + a.nvec * (16 / sizeof(T)) + a.tail;
+    return (size_t)(a.nins + 1) * n * sizeof(T) >= kNtThresholdBytes ? launch_typed<T, OP, 3>(a, stream)
+                                                                      : launch_typed<T, OP, 0>(a, stream);
 }
 
 // The copy (nins == 1: reduce-op.c:213-216, the whole PE_size = 1 call, and
@@ -528,12 +496,9 @@ hipError_t launch_copy_nt(const FoldArgs &a0, hipStream_t stream) {
 
 template <typename T>
 hipError_t launch_copy(const FoldArgs &a, hipStream_t stream) {
-    int mode = fold_tuning().nontemporal;
-    if (mode < 0) {
-        const size_t n = a.head + a.nvec * (16 / sizeof(T)) + a.tail;
-        mode = 2 * n * sizeof(T) >= kNtThresholdBytes ? 3 : 0;
-    }
-    return mode ? launch_copy_nt<T, 3>(a, stream) : launch_copy_nt<T, 0>(a, stream);
+    const size_t n = a.head + a.nvec * (16 / sizeof(T)) + a.tail;
+    return 2 * n * sizeof(T) >= kNtThresholdBytes ? launch_copy_nt<T, 3>(a, stream)
+                                                  : launch_copy_nt<T, 0>(a, stream);
 }
 
 template <typename T>
@@ -569,17 +534,6 @@ hipError_t launch_cplx_ops(int op, const FoldArgs &a, hipStream_t s) {
 }
 
 }  // namespace
-
-FoldTuning &fold_tuning() {
-    static FoldTuning t = [] {
-        FoldTuning r{0, -1, 4};
-        if (const char *e = std::getenv("SHMEMX_FOLD_MAX_BLOCKS")) r.max_blocks = std::atoi(e);
-        if (const char *e = std::getenv("SHMEMX_FOLD_NT")) r.nontemporal = std::atoi(e);
-        if (const char *e = std::getenv("SHMEMX_FOLD_UNROLL")) r.unroll = std::atoi(e);
-        return r;
-    }();
-    return t;
-}
 
 size_t type_size(int type) {
     switch (type) {
@@ -679,7 +633,7 @@ hipError_t launch_fold(int type, int op, void *out, const void *const *ins,
 
 bool copy_one_workgroup(int type, const void *dst, const void *src, size_t n) {
     const size_t sz = type_size(type);
-    if (!sz || !n || fold_tuning().max_blocks < 0) return false;
+    if (!sz || !n) return false;
     const uintptr_t off = reinterpret_cast<uintptr_t>(dst) & 15u;
     if (off % sz != 0 || (reinterpret_cast<uintptr_t>(src) & 15u) != off)
         return n <= (size_t)kBlock;                    // all scalar: ceil(n / kBlock) blocks

@@ -175,14 +175,5 @@ hipError_t launch_checksum(int type, const void *ptr, size_t n, unsigned long lo
 int kernel_timing(int on);
 int kernel_times(double *us, int *kind, int max, unsigned long long *dropped);
 
-// Tuning knobs for the fold kernels (initialised from the environment:
-// SHMEMX_FOLD_MAX_BLOCKS, SHMEMX_FOLD_NT, SHMEMX_FOLD_UNROLL; changed at run
-// time by shmemx_fold_set_tuning).
-struct FoldTuning {
-    int max_blocks;   // grid cap; 0 = one chunk of 256 x unroll vectors per block
-    int nontemporal;  // -1 auto by size; else bit 0: nt loads, bit 1: nt stores
-    int unroll;       // 2, 4 or 8 16-B vectors per lane per input (2-input fold)
-};
-FoldTuning &fold_tuning();
 
 }  // namespace shmx

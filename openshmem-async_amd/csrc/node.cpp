@@ -30,7 +30,8 @@ struct RegionSlot {
 struct PeSlot {
     RegionSlot region[kNumRegions];
     Desc desc;
-    std::atomic<int> vote;   // agree()
+    std::atomic<int> vote;       // agree()
+    std::atomic<int> gpu_numa;   // the GPU's NUMA node + 1 (0 = unknown)
 };
 
 struct Shared {
@@ -258,6 +259,17 @@ void put_desc(const Desc &d) {
 Desc get_desc(int q) {
     return g_node.sh ? g_node.sh->pe[q].desc : Desc{};
 }
+
+void put_gpu_numa(int nd) {
+    if (g_node.sh) g_node.sh->pe[g_node.pe].gpu_numa.store(nd < 0 ? 0 : nd + 1, std::memory_order_release);
+}
+
+int gpu_numa(int q) {
+    if (!g_node.sh || q < 0 || q >= g_node.npes) return -1;
+    return g_node.sh->pe[q].gpu_numa.load(std::memory_order_acquire) - 1;
+}
+
+int npes() { return g_node.sh ? g_node.npes : 0; }
 
 }  // namespace node
 }  // namespace shmx

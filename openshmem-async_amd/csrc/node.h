@@ -74,5 +74,12 @@ bool agree(int start, int step, int P, bool ok);
 void put_desc(const Desc &d);
 Desc get_desc(int pe);
 
+// The NUMA node of each PE's GPU (-1 unknown), published by every PE before
+// shmem_init's first barrier: the staging copy threads of the PEs that share
+// a NUMA node take different cache domains (staging.cpp).
+void put_gpu_numa(int node);
+int gpu_numa(int pe);
+int npes();   // PEs attached to the block (0 if it is down)
+
 }  // namespace node
 }  // namespace shmx

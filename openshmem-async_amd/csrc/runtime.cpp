@@ -130,9 +130,7 @@ void wait_host_signal(const HostSignal &sig, hipStream_t s) {
     // while a kernel is still retiring costs ~9 us more than the retiring
     // itself; polling hipStreamQuery until the stream is idle is worse still
     // (profiles/r03_latency_ab.txt): there the stream wait is the wait.
-    // $SHMEMX_HOST_SIGNAL=0: stream waits everywhere (A/B and a way out).
-    static const bool on = env_int("SHMEMX_HOST_SIGNAL", nullptr, 1) != 0;
-    if (!on || !g_state.return_on_signal) {
+    if (!g_state.return_on_signal) {
         SHMX_HIP(hipStreamSynchronize(s));
         return;
     }
@@ -201,8 +199,7 @@ static const char *const kPlanSettings[] = {
     "SHMEM_REDUCE_ALGO",        "SHMEMX_AUTO_FULL",         "SHMEMX_AUTO_PARTIAL",
     "SHMEMX_ALLREDUCE_MAX_KB",  "SHMEMX_DIRECT_ONESHOT_KB", "SHMEMX_FUSED_TWOSHOT_KB",
     "SHMEMX_FUSED_ONESHOT",     "SHMEMX_SET_COMMS",         "SHMEMX_SET_COMMS_MAX",
-    "SHMEMX_STAGE_CHUNK_MB",    "SHMEMX_STAGE_RAMP",        "SHMEMX_DIRECT_SCRATCH_MB",
-    "SHMEMX_TRANSPORT"};
+    "SHMEMX_STAGE_CHUNK_MB",    "SHMEMX_DIRECT_SCRATCH_MB", "SHMEMX_TRANSPORT"};
 
 static std::string plan_settings() {
     std::string t;
@@ -278,6 +275,7 @@ static int init_locked(int pe, int npes, int device, const void *uid) {
         // file is removed only once every PE has read it); the name can go
         // then, so a job that dies leaves nothing in /dev/shm.
         if (attached) {
+            node::put_gpu_numa(gpu_numa_node(device));   // (staging.cpp's copy threads)
             node::barrier(0, 1, npes);
             if (pe == 0) node::unlink_name();
         }
@@ -1224,15 +1222,6 @@ long shmemx_set_fused_twoshot_kb(long kb) {
     }
     std::lock_guard<std::recursive_mutex> lk(g_mu);
     return set_fused_twoshot_kb(kb);
-}
-
-int shmemx_fold_set_tuning(int max_blocks, int nontemporal, int unroll) {
-    if (max_blocks < 0 || (unroll != 2 && unroll != 4 && unroll != 8)) return set_error(SHMEMX_EINVAL);
-    FoldTuning &t = fold_tuning();
-    t.max_blocks = max_blocks;
-    t.nontemporal = nontemporal < 0 ? -1 : (nontemporal & 3);
-    t.unroll = unroll;
-    return SHMEMX_OK;
 }
 
 int shmemx_rccl_register_heap(int on) {

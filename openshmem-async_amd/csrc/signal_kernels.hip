@@ -420,23 +420,17 @@ __global__ __launch_bounds__(kBlock) void signal_fold2_kernel(SignalFoldArgs a) 
     }
 }
 
-// Blocks of the fused launches ($SHMEMX_FUSED_BLOCKS, 8 ... kFenceBlocks;
-// every XCD must still get one: the entry check counts them).
-unsigned fused_blocks() {
-    static const unsigned b = [] {
-        const char *e = std::getenv("SHMEMX_FUSED_BLOCKS");
-        const int v = e ? std::atoi(e) : kFenceBlocks;
-        return (unsigned)(v < 8 ? 8 : v > kFenceBlocks ? kFenceBlocks : v);
-    }();
-    return b;
-}
+// Blocks of the fused launches: kFenceBlocks, so every XCD gets 8 (the entry
+// check counts them); 8-32 blocks measured within 1 us of it
+// (profiles/r05_fused_blocks.txt).
+constexpr unsigned kFusedBlocks = kFenceBlocks;
 
 template <typename T, int OP>
 hipError_t sf_launch(const SignalFoldArgs &a, hipStream_t s) {
     if (a.two_shot)
-        hipLaunchKernelGGL((signal_fold2_kernel<T, OP>), dim3(fused_blocks()), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL((signal_fold2_kernel<T, OP>), dim3(kFusedBlocks), dim3(kBlock), 0, s, a);
     else
-        hipLaunchKernelGGL((signal_fold_kernel<T, OP>), dim3(fused_blocks()), dim3(kBlock), 0, s, a);
+        hipLaunchKernelGGL((signal_fold_kernel<T, OP>), dim3(kFusedBlocks), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
 

@@ -10,11 +10,10 @@
 #include <immintrin.h>
 #include <pthread.h>
 #include <sched.h>
-#include <sys/mman.h>
-#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <array>
 #include <fstream>
 #include <sstream>
 #include <string>
@@ -46,27 +45,12 @@ constexpr size_t kRingSlots = 4;     // page-locked bounce slots per direction
 // asynchronously; they go through kRingSlots page-locked slots per direction,
 // filled and emptied by a small pool of CPU threads, so the CPU copies of
 // one chunk overlap the PCIe transfers and device work of its neighbours.
-// $SHMEMX_RING_THP=1: the ring is an anonymous mapping advised to use
-// transparent huge pages, faulted in, then page-locked with hipHostRegister
-// (fewer TLB misses for the CPU copies through it); default: hipHostMalloc.
-static bool ring_thp() {
-    static const bool on = [] {
-        const char *e = std::getenv("SHMEMX_RING_THP");
-        return e && *e == '1';
-    }();
-    return on;
-}
-
+// (A THP-backed ring registered with hipHostRegister measured the same:
+// profiles/r05_e2e_nt.txt.)
 void ring_free() {
     if (!g_state.ring) return;
-    if (g_state.ring_map) {
-        (void)hipHostUnregister(g_state.ring);
-        munmap(g_state.ring_map, g_state.ring_map_bytes);
-    } else {
-        (void)hipHostFree(g_state.ring);
-    }
-    g_state.ring = g_state.ring_map = nullptr;
-    g_state.ring_map_bytes = 0;
+    (void)hipHostFree(g_state.ring);
+    g_state.ring = nullptr;
     g_state.ring_slot = 0;
 }
 
@@ -77,25 +61,6 @@ static bool ring_reserve(size_t slot_bytes) {
         ring_free();
     }
     const size_t bytes = 2 * kRingSlots * slot_bytes;
-    if (ring_thp()) {
-        constexpr size_t kHuge = size_t(2) << 20;
-        const size_t map = bytes + kHuge;
-        void *m = mmap(nullptr, map, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-        if (m != MAP_FAILED) {
-            char *p = reinterpret_cast<char *>((reinterpret_cast<uintptr_t>(m) + kHuge - 1) & ~(kHuge - 1));
-            (void)madvise(p, bytes, MADV_HUGEPAGE);
-            std::memset(p, 0, bytes);
-            if (hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess) {
-                g_state.ring = p;
-                g_state.ring_map = m;
-                g_state.ring_map_bytes = map;
-                g_state.ring_slot = slot_bytes;
-                return true;
-            }
-            (void)hipGetLastError();
-            munmap(m, map);
-        }
-    }
     if (hipHostMalloc(&g_state.ring, bytes, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         g_state.ring = nullptr;
@@ -141,40 +106,36 @@ static void copy_bytes(char *dst, const char *src, size_t n, bool nt) {
     else std::memcpy(dst, src, n);
 }
 
-// $SHMEMX_COPY_NT: which staging copies of pageable arrays use streaming
-// stores — bit 0 the source into the page-locked ring (read next by the H2D
-// DMA), bit 1 the ring out into the caller's target; default 2: the out
-// gang's 4 threads copy 94 against 81 GB/s with them in the copy lab, and the
-// pipeline averages 36.0 against 34.9 GiB/s over interleaved runs, with the
-// smaller dip (profiles/r05_e2e_nt.txt); into the ring they lose (30.3
+// Streaming stores for the ring's out-copy into the caller's target only: the
+// out gang's 4 threads copy 94 against 81 GB/s with them in the copy lab, and
+// the pipeline averages 36.0 against 34.9 GiB/s over interleaved runs, with
+// the smaller dip (profiles/r05_e2e_nt.txt); into the ring they lose (30.3
 // against 36.2: the H2D DMA reads the slot right after).
-// $SHMEMX_STAGE_RAMP=0: uniform staging chunks (no quarter / half chunks at
-// the pipeline's ends)
-static bool stage_ramp() {
-    static const bool on = [] {
-        const char *e = std::getenv("SHMEMX_STAGE_RAMP");
-        return !(e && *e == '0');
-    }();
-    return on;
-}
+constexpr bool kNtIn = false, kNtOut = true;
 
-static int copy_nt_mask() {
-    static const int m = [] {
-        const char *e = std::getenv("SHMEMX_COPY_NT");
-        return e && *e ? (std::atoi(e) & 3) : 2;
-    }();
-    return m;
-}
+static std::vector<int> allowed_cpus();
+static const std::vector<std::vector<int>> &copy_threads();
 
 namespace {
+void pin_thread(std::thread &t, const std::vector<int> &cpus) {
+    if (cpus.empty()) return;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    for (int c : cpus) CPU_SET(c, &set);
+    (void)pthread_setaffinity_np(t.native_handle(), sizeof set, &set);
+}
+
 class CopyPool {
   public:
+    // the staging budget (copy_threads): worker i on thread i's domain (the
+    // caller does piece 0 where it runs)
     CopyPool() {
-        unsigned hw = std::thread::hardware_concurrency();
-        nthreads_ = hw >= 16 ? 8 : (hw >= 4 ? hw / 2 : 1);
-        if (const char *e = std::getenv("SHMEMX_COPY_THREADS"))
-            nthreads_ = std::max(1, std::min(64, std::atoi(e)));
-        for (unsigned i = 1; i < nthreads_; ++i) workers_.emplace_back([this, i] { run(i); });
+        const std::vector<std::vector<int>> &plan = copy_threads();
+        nthreads_ = (unsigned)plan.size();
+        for (unsigned i = 1; i < nthreads_; ++i) {
+            workers_.emplace_back([this, i] { run(i); });
+            pin_thread(workers_.back(), plan[i]);
+        }
     }
     ~CopyPool() {
         {
@@ -250,22 +211,6 @@ void parallel_copy(void *dst, const void *src, size_t bytes, bool nt) {
     pool.copy(dst, src, bytes, nt);
 }
 
-// The CPUs the staging copy gangs run on ($SHMEMX_COPY_CPUS): "spread" (the
-// default) = each copy thread in its own cache domain of the GPU's NUMA node
-// (spread_domains: 36.8-37.7 GiB/s on three boxes where the scheduler's
-// placement gave 27.2-37.7, profiles/r05_e2e_spread.txt); "all" =
-// unpinned; "gpu" = this process's allowed CPUs on the GPU's NUMA node, any
-// of them; "data" = per call, each gang on the node of the caller's array it
-// reads or writes; or an explicit list "a-b,c".  An empty result (no NUMA or
-// cache information, no allowed CPU there) leaves the threads unpinned.
-static const std::string &copy_cpus_mode() {
-    static const std::string m = [] {
-        const char *e = std::getenv("SHMEMX_COPY_CPUS");
-        return std::string(e && *e ? e : "spread");
-    }();
-    return m;
-}
-
 // this process's allowed CPUs
 static std::vector<int> allowed_cpus() {
     cpu_set_t set;
@@ -280,18 +225,10 @@ static std::vector<int> allowed_cpus() {
 // allowed CPUs of NUMA node `node` (empty if unknown)
 static std::vector<int> node_cpus(int node) { return topo::node_cpus("/sys", node, allowed_cpus()); }
 
-// NUMA node of the page holding `p` (move_pages with no target: a query), or -1
-static int page_node(const void *p) {
-    void *page = reinterpret_cast<void *>(reinterpret_cast<uintptr_t>(p) & ~uintptr_t(4095));
-    int status = -1;
-    if (syscall(SYS_move_pages, 0, 1UL, &page, nullptr, &status, 0) != 0) return -1;
-    return status >= 0 ? status : -1;
-}
-
-// NUMA node of the PE's GPU (its PCI device's numa_node), or -1
-static int gpu_numa_node() {
+// NUMA node of a GPU (its PCI device's numa_node), or -1
+int gpu_numa_node(int device) {
     char bus[64] = {0};
-    if (hipDeviceGetPCIBusId(bus, sizeof bus, g_state.device) != hipSuccess) {
+    if (hipDeviceGetPCIBusId(bus, sizeof bus, device) != hipSuccess) {
         (void)hipGetLastError();
         return -1;
     }
@@ -303,27 +240,44 @@ static int gpu_numa_node() {
     return node;
 }
 
-// The last-level-cache domains (CCDs on EPYC) of the GPU's NUMA node, each as
-// this process's allowed CPUs in it, in domain order: each copy thread is
-// confined to one domain, so the threads use different domains' paths to
-// memory instead of the scheduler's placement, which may stack several on one
-// CCD or put them on the other socket (profiles/r05_e2e_spread.txt); within a
-// domain the scheduler still picks an idle core.  Empty if the topology is
-// unknown.
-static std::vector<std::vector<int>> spread_domains() {
-    const int node = gpu_numa_node();
-    return node >= 0 ? topo::cache_domains("/sys", node_cpus(node)) : std::vector<std::vector<int>>{};
-}
-
-static std::vector<int> copy_cpus() {
-    const std::string &mode = copy_cpus_mode();
-    if (mode == "all" || mode == "data" || mode == "spread") return {};
-    if (mode == "gpu") return node_cpus(gpu_numa_node());
-    const std::vector<int> allowed = allowed_cpus();
-    std::vector<int> out;
-    for (int c : topo::parse_cpulist(mode))
-        if (std::find(allowed.begin(), allowed.end(), c) != allowed.end()) out.push_back(c);
-    return out;
+// The staging copy threads of this PE, as CPU sets (topo::plan_copy_threads),
+// made once: the job's CPU budget (the cgroup quota, else this process's
+// allowed CPUs) shared by the PEs on the node, at most 8 per PE
+// ($SHMEMX_COPY_THREADS: that many, as given), each thread confined to its
+// own last-level-cache domain (CCD) of the GPU's NUMA node, offset by the PE's
+// rank among the PEs whose GPUs share that node.  One thread per domain runs
+// 36.8-37.7 GiB/s where the scheduler's placement gave 27.2-37.7 (one PE,
+// profiles/r05_e2e_spread.txt); with every PE putting its thread i on domain i
+// (round 5), eight PEs stacked theirs on the same CCDs, and 8 x 15 threads
+// against a 16-CPU quota ran pageable at 0.53 of pinned.
+// Within a domain the scheduler picks an idle core; an unknown topology
+// leaves the threads unpinned.
+static const std::vector<std::vector<int>> &copy_threads() {
+    static const std::vector<std::vector<int>> plan = [] {
+        const char *e = std::getenv("SHMEMX_COPY_THREADS");
+        const unsigned want = e && *e ? (unsigned)std::max(2, std::min(64, std::atoi(e))) : 8u;
+        const std::vector<int> allowed = allowed_cpus();
+        const int quota = topo::cgroup_cpu_quota("/sys/fs/cgroup");
+        const int budget = e && *e ? 0 : quota > 0 ? std::min(quota, (int)allowed.size()) : (int)allowed.size();
+        const int mine = gpu_numa_node(g_state.device);
+        int pes = 1, rank = 0;
+        if (node::up()) {
+            pes = node::npes();
+            for (int q = 0; q < g_state.pe; ++q) rank += node::gpu_numa(q) == mine ? 1 : 0;
+        }
+        const std::vector<std::vector<int>> domains =
+            mine >= 0 ? topo::cache_domains("/sys", node_cpus(mine)) : std::vector<std::vector<int>>{};
+        std::vector<std::vector<int>> p = topo::plan_copy_threads(want, budget, pes, rank, domains);
+        if (log_enabled(LOG_INFO)) {
+            std::string l;
+            for (const auto &x : p) l += x.empty() ? "- " : std::to_string(x.front()) + "+" + std::to_string(x.size() - 1) + " ";
+            trace(LOG_INFO, "staging copy threads: %zu (CPU budget %d over %d PEs, quota %d; rank %d on NUMA node "
+                  "%d of %zu cache domains), first CPU+others of each: %s", p.size(), budget, pes, quota, rank,
+                  mine, domains.size(), l.c_str());
+        }
+        return p;
+    }();
+    return plan;
 }
 
 namespace {
@@ -335,18 +289,12 @@ namespace {
 // doing both in turn left each copy waiting for the other).
 class CopyGang {
   public:
-    // cpus: every worker may run on any of them; per_thread (if not empty):
-    // worker i on the CPUs of per_thread[i % size]
-    CopyGang(unsigned n, const std::vector<int> &cpus, const std::vector<std::vector<int>> &per_thread = {})
-        : n_(std::max(1u, n)) {
+    // worker i on the CPUs of per_thread[i] (empty: unpinned)
+    explicit CopyGang(const std::vector<std::vector<int>> &per_thread)
+        : n_(std::max<unsigned>(1u, (unsigned)per_thread.size())) {
         for (unsigned i = 0; i < n_; ++i) {
             workers_.emplace_back([this, i] { run(i); });
-            const std::vector<int> &mine = per_thread.empty() ? cpus : per_thread[i % per_thread.size()];
-            if (mine.empty()) continue;
-            cpu_set_t set;
-            CPU_ZERO(&set);
-            for (int c : mine) CPU_SET(c, &set);
-            (void)pthread_setaffinity_np(workers_.back().native_handle(), sizeof set, &set);
+            if (i < per_thread.size()) pin_thread(workers_.back(), per_thread[i]);
         }
     }
     ~CopyGang() {
@@ -356,16 +304,6 @@ class CopyGang {
         }
         cv_.notify_all();
         for (auto &t : workers_) t.join();
-    }
-    // run the next copies on these CPUs (empty: leave as is)
-    void pin(const std::vector<int> &cpus) {
-        if (cpus.empty() || cpus == pinned_) return;
-        wait();
-        cpu_set_t set;
-        CPU_ZERO(&set);
-        for (int c : cpus) CPU_SET(c, &set);
-        for (auto &t : workers_) (void)pthread_setaffinity_np(t.native_handle(), sizeof set, &set);
-        pinned_ = cpus;
     }
     void start(void *dst, const void *src, size_t bytes, bool nt) {
         wait();
@@ -401,7 +339,6 @@ class CopyGang {
         }
     }
     unsigned n_;
-    std::vector<int> pinned_;
     std::vector<std::thread> workers_;
     std::mutex mu_;
     std::condition_variable cv_, done_;
@@ -414,42 +351,18 @@ class CopyGang {
     bool nt_ = false;
 };
 
-// The staging pipeline's two gangs, made on first use: $SHMEMX_COPY_THREADS
-// (default 8) split between them.
+// The staging pipeline's two gangs, made on first use: this PE's copy
+// threads (copy_threads) alternate between them, the in gang taking threads
+// 0, 2, 4, ... and the out gang 1, 3, 5, ..., so no two share a domain
+// while there are domains enough.
 CopyGang &gang(int which) {
-    static unsigned total = [] {
-        unsigned n = 8;
-        if (const char *e = std::getenv("SHMEMX_COPY_THREADS")) n = (unsigned)std::max(2, std::min(64, std::atoi(e)));
-        return n;
+    static const std::array<std::vector<std::vector<int>>, 2> halves = [] {
+        const std::vector<std::vector<int>> &all = copy_threads();
+        std::array<std::vector<std::vector<int>>, 2> h;
+        for (size_t i = 0; i < all.size(); ++i) h[i % 2].push_back(all[i]);
+        return h;
     }();
-    static const std::vector<int> cpus = [] {
-        std::vector<int> c = copy_cpus();
-        if (log_enabled(LOG_INFO)) {
-            std::string l;
-            for (int x : c) l += std::to_string(x) + " ";
-            trace(LOG_INFO, "staging copy gangs on CPUs: %s", c.empty() ? "(unpinned)" : l.c_str());
-        }
-        return c;
-    }();
-    // spread: the in gang takes every other domain from the first, the out
-    // gang the ones between, so no two copy threads share a domain while
-    // there are domains enough
-    static const std::vector<std::vector<int>> spread = [] {
-        std::vector<std::vector<int>> d =
-            copy_cpus_mode() == "spread" ? spread_domains() : std::vector<std::vector<int>>{};
-        if (!d.empty() && log_enabled(LOG_INFO)) {
-            std::string l;
-            for (const auto &x : d) l += std::to_string(x.front()) + "+" + std::to_string(x.size() - 1) + " ";
-            trace(LOG_INFO, "staging copy threads one per cache domain (first CPU+others): %s", l.c_str());
-        }
-        return d;
-    }();
-    auto half = [](const std::vector<std::vector<int>> &all, size_t first) {
-        std::vector<std::vector<int>> h;
-        for (size_t i = first; i < all.size(); i += 2) h.push_back(all[i]);
-        return h.empty() ? all : h;
-    };
-    static CopyGang in(total / 2, cpus, half(spread, 0)), out(total - total / 2, cpus, half(spread, 1));
+    static CopyGang in(halves[0]), out(halves[1]);
     return which == 0 ? in : out;
 }
 }  // namespace
@@ -494,16 +407,11 @@ static bool calls_agree(int start, int logstride, int size, size_t ncalls) {
 static void reduce_blocking_impl(int type, int op, void *target, const void *source, int nreduce,
                                  int start, int logstride, int size, bool trace_call);
 
-// A blocking call's host-view target up to this many bytes is copied back
-// into the view before the call returns ($SHMEMX_MIRROR_SETTLE_KB, default
-// 256 KiB, the bounce path's size; 0 = never): its blocks come back CLEAN.
-static size_t mirror_settle_limit() {
-    static const size_t lim = [] {
-        const char *e = std::getenv("SHMEMX_MIRROR_SETTLE_KB");
-        return (e ? (size_t)std::strtoull(e, nullptr, 10) : (size_t)256) << 10;
-    }();
-    return lim;
-}
+// A blocking call's host-view target up to this many bytes (the bounce
+// path's size) is copied back into the view before the call returns: its
+// blocks come back CLEAN (ISx's round 42.8 -> 30.1 us, the host load 19.9 ->
+// 0.26 us: profiles/r04_isx_mirror.txt).
+static size_t mirror_settle_limit() { return kSmallHostBytes; }
 
 // The blocking entry point body: host- or device-resident arrays.  Operands
 // in the mirrored heap's host view run on their HBM twins (heap.h).
@@ -801,10 +709,11 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
     // overwritten under a later chunk's H2D: no pipelining then
     const bool host_overlap = !tdev && !sdev && overlap(target, source, bytes);
     if (host_overlap) chunk = (size_t)nreduce;
-    // The chunk schedule (elements, stage_plan.h), the same on every PE
-    // (calls_agree compares its length); $SHMEMX_STAGE_RAMP=0: uniform chunks.
+    // The chunk schedule (elements, stage_plan.h: quarter and half chunks at
+    // both ends, +1.1 %, profiles/r05_e2e_ramp.txt), the same on every PE
+    // (calls_agree compares its length).
     std::vector<size_t> c_off, c_n;
-    stage_plan((size_t)nreduce, chunk, g, stage_ramp() && !host_overlap, c_off, c_n);
+    stage_plan((size_t)nreduce, chunk, g, !host_overlap, c_off, c_n);
     const size_t nchunks = c_n.size();
     if (collective && !calls_agree(start, logstride, size, nchunks)) return;
     // How each end reaches the device: directly (device memory), by DMA
@@ -836,23 +745,17 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
     // DMA and the fold of the chunks between them.  Slot reuse: the in-copy
     // of chunk k waits for the H2D of chunk k - kRingSlots (event), the D2H of
     // chunk k for the out-copy of chunk k - kRingSlots (host side).
-    const bool nt_in = copy_nt_mask() & 1, nt_out = copy_nt_mask() & 2;
-    if (copy_cpus_mode() == "data") {
-        // each gang on the NUMA node of the caller's array it touches
-        if (in_bounce) gang(0).pin(node_cpus(page_node(source)));
-        if (out_bounce) gang(1).pin(node_cpus(page_node(target)));
-    }
     auto count_of_chunk = [&](size_t k) { return c_n[k]; };
     auto start_in = [&](size_t k) {
         const size_t slot = k % kRingSlots;
         if (k >= kRingSlots) SHMX_HIP(hipEventSynchronize(ev_in_slot[slot]));
-        gang(0).start(ring_in(slot), hsrc + c_off[k] * sz, count_of_chunk(k) * sz, nt_in);
+        gang(0).start(ring_in(slot), hsrc + c_off[k] * sz, count_of_chunk(k) * sz, kNtIn);
     };
     size_t out_started = 0;   // out-copies started; all but the last are complete
     auto start_out = [&]() {
         const size_t j = out_started++;
         SHMX_HIP(hipEventSynchronize(ev_out_slot[j % kRingSlots]));
-        gang(1).start(htgt + c_off[j] * sz, ring_out(j % kRingSlots), count_of_chunk(j) * sz, nt_out);
+        gang(1).start(htgt + c_off[j] * sz, ring_out(j % kRingSlots), count_of_chunk(j) * sz, kNtOut);
     };
     // the out-copy of chunk j has completed (starting the ones before it)
     auto out_done = [&](size_t j) {

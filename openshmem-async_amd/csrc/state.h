@@ -68,8 +68,6 @@ struct State {
     size_t cws_tgt_bytes = 0;
     void *ring = nullptr;      // page-locked bounce ring (large pageable arrays)
     size_t ring_slot = 0;
-    void *ring_map = nullptr;  // the ring's own mapping when registered (SHMEMX_RING_THP)
-    size_t ring_map_bytes = 0;
     void *bounce = nullptr;    // page-locked host bounce buffers (small messages)
     size_t bounce_bytes = 0;
     hipStream_t h2d = nullptr;  // staging copy streams and their chunk events
@@ -129,6 +127,7 @@ void set_comms_release();
 // nt: streaming (non-temporal) stores, for a destination nothing reads soon
 void parallel_copy(void *dst, const void *src, size_t bytes, bool nt = false);
 void ring_free();   // the staging ring (staging.cpp), at finalize
+int gpu_numa_node(int device);   // NUMA node of a HIP device's PCI function, or -1
 // The plan of one call (shmemx_reduce_plan) and the device-resident engine
 // (runtime.cpp); the host staging of the blocking entry points (staging.cpp)
 // runs the engine chunk by chunk.

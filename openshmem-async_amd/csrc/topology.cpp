@@ -57,5 +57,34 @@ std::vector<std::vector<int>> cache_domains(const std::string &sysroot, const st
     return out;
 }
 
+int cgroup_cpu_quota(const std::string &cgroot) {
+    long long quota = -1, period = 0;
+    {
+        std::ifstream v2(cgroot + "/cpu.max");
+        std::string q;
+        if (v2 >> q >> period) quota = q == "max" ? -1 : std::atoll(q.c_str());
+    }
+    if (period <= 0) {
+        std::ifstream qf(cgroot + "/cpu/cpu.cfs_quota_us"), pf(cgroot + "/cpu/cpu.cfs_period_us");
+        if (!(qf >> quota) || !(pf >> period)) return 0;
+    }
+    if (quota <= 0 || period <= 0) return 0;
+    return (int)((quota + period - 1) / period);
+}
+
+std::vector<std::vector<int>> plan_copy_threads(unsigned want, int budget, int pes_on_host, int rank,
+                                                const std::vector<std::vector<int>> &domains) {
+    unsigned n = want < 2 ? 2 : want;
+    if (budget > 0 && pes_on_host > 0) {
+        const unsigned share = (unsigned)(budget / pes_on_host);
+        n = std::max(2u, std::min(n, share));
+    }
+    std::vector<std::vector<int>> out(n);
+    if (domains.empty()) return out;
+    const size_t nd = domains.size(), base = (size_t)(rank < 0 ? 0 : rank) * n;
+    for (unsigned i = 0; i < n; ++i) out[i] = domains[(base + i) % nd];
+    return out;
+}
+
 }  // namespace topo
 }  // namespace shmx

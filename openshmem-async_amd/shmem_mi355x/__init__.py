@@ -124,8 +124,6 @@ def lib() -> ctypes.CDLL:
     L.shmemx_get_stream.restype = vp
     L.shmemx_set_algo.argtypes = [i]
     L.shmemx_set_algo.restype = i
-    L.shmemx_fold_set_tuning.argtypes = [i, i, i]
-    L.shmemx_fold_set_tuning.restype = i
     L.shmemx_rccl_register_heap.argtypes = [i]
     L.shmemx_rccl_register_heap.restype = i
     L.shmemx_set_comms.restype = i
@@ -349,11 +347,6 @@ def plan(type_name: str, op: str, nreduce: int, PE_start: int, logPE_stride: int
     inv = {v: k for k, v in ALGOS.items()}
     return PlanInfo(inv[p.algo], p.member, p.nmembers, p.elem_size, p.chunk, p.main,
                     p.tail, p.ws_bytes)
-
-
-def set_fold_tuning(max_blocks: int = 0, nontemporal: int = -1, unroll: int = 4) -> None:
-    """Launch shape of the fold kernels (grid cap, nt loads/stores, unroll)."""
-    _check(lib().shmemx_fold_set_tuning(max_blocks, nontemporal, unroll), "shmemx_fold_set_tuning")
 
 
 def rccl_register_heap(on: bool) -> None:

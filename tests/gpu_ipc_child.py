@@ -942,7 +942,7 @@ elif scenario == "mirrored":
                        srcs[:, :nb // 8], world, ran32):
             fails.append("mirrored: write(2) after shmemx_mirror_acquire wrote wrong bytes")
     ncases += 1
-    # a SMALL result (<= $SHMEMX_MIRROR_SETTLE_KB, 256 KiB) comes back into the
+    # a SMALL result (<= 256 KiB) comes back into the
     # view before the blocking call returns: write(2) of it works with no
     # shmemx_mirror_acquire, the blocks are CLEAN, and the
     # copy-back moved only the result's bytes

@@ -94,6 +94,76 @@ int main(int argc, char **argv) {
     CHECK(cache_domains(root, {64, 999}).empty());
     CHECK(cache_domains(root, {}).empty());
 
+    // cgroup_cpu_quota: v2 cpu.max, v1 cfs files, no limit
+    put(root + "/cg2/cpu.max", "1600000 100000");
+    CHECK(cgroup_cpu_quota(root + "/cg2") == 16);
+    put(root + "/cg2b/cpu.max", "150000 100000");       // 1.5 CPUs: 2 busy at most
+    CHECK(cgroup_cpu_quota(root + "/cg2b") == 2);
+    put(root + "/cg2c/cpu.max", "max 100000");
+    CHECK(cgroup_cpu_quota(root + "/cg2c") == 0);
+    put(root + "/cg1/cpu/cpu.cfs_quota_us", "800000");
+    put(root + "/cg1/cpu/cpu.cfs_period_us", "100000");
+    CHECK(cgroup_cpu_quota(root + "/cg1") == 8);
+    put(root + "/cg1n/cpu/cpu.cfs_quota_us", "-1");
+    put(root + "/cg1n/cpu/cpu.cfs_period_us", "100000");
+    CHECK(cgroup_cpu_quota(root + "/cg1n") == 0);
+    CHECK(cgroup_cpu_quota(root + "/nowhere") == 0);
+
+    // plan_copy_threads: one PE alone keeps 8 threads, one per domain of its
+    // GPU's node, in domain order
+    {
+        const auto p = plan_copy_threads(8, 16, 1, 0, d);
+        CHECK(p.size() == 8);
+        bool ok = p.size() == 8;
+        for (size_t i = 0; ok && i < p.size(); ++i) ok = p[i] == d[i];
+        CHECK(ok);
+    }
+    // 8 PEs on the host (4 per NUMA node, as an 8-GPU MI355X node), a 16-CPU
+    // quota: 2 threads each, 16 in all; the 4 PEs of one node cover its 8
+    // domains with no two threads on one domain
+    {
+        size_t total = 0;
+        for (int node = 0; node < 2; ++node) {
+            const auto dn = cache_domains(root, node_cpus(root, node, all));
+            std::set<int> firsts;
+            for (int rank = 0; rank < 4; ++rank) {
+                const auto p = plan_copy_threads(8, 16, 8, rank, dn);
+                CHECK(p.size() == 2);
+                total += p.size();
+                for (const auto &cpus : p) {
+                    CHECK(!cpus.empty());
+                    if (!cpus.empty()) CHECK(firsts.insert(cpus.front()).second);   // a fresh domain
+                }
+            }
+            CHECK(firsts.size() == 8);
+        }
+        CHECK(total <= 16);
+    }
+    // 8 PEs on one node's GPU (the one-GPU rehearsal): 2 threads each over 8
+    // domains, each domain twice at most (16 threads, 8 domains)
+    {
+        std::vector<int> uses(256, 0);
+        for (int rank = 0; rank < 8; ++rank)
+            for (const auto &cpus : plan_copy_threads(8, 16, 8, rank, d)) uses[cpus.front()]++;
+        int most = 0;
+        for (int u : uses) most = u > most ? u : most;
+        CHECK(most == 2);
+    }
+    // a quota smaller than 2 per PE still leaves one thread per gang; no
+    // quota information (budget 0) keeps the per-PE count; unknown topology:
+    // unpinned threads
+    CHECK(plan_copy_threads(8, 4, 8, 3, d).size() == 2);
+    CHECK(plan_copy_threads(8, 0, 8, 3, d).size() == 8);
+    {
+        const auto p = plan_copy_threads(8, 64, 2, 1, {});
+        CHECK(p.size() == 8 && p[0].empty() && p[7].empty());
+    }
+    // 2 PEs with 32 CPUs: 8 each, the second PE's 8 after the first's (wrapping)
+    {
+        const auto p0 = plan_copy_threads(8, 32, 2, 0, d), p1 = plan_copy_threads(8, 32, 2, 1, d);
+        CHECK(p0.size() == 8 && p1.size() == 8 && p1[0] == d[0] && p0[0] == d[0]);
+    }
+
     // this machine's /sys, when it has one: the domains partition the node's CPUs
     std::ifstream probe("/sys/devices/system/node/node0/cpulist");
     if (probe) {

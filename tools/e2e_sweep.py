@@ -24,6 +24,6 @@ def node_of(a):
     libc.syscall(279, 0, ctypes.c_ulong(1), ctypes.byref(page), None, ctypes.byref(status), 0)
     return status.value
 print(f"threads={os.environ.get('SHMEMX_COPY_THREADS','dflt')} chunkMB={os.environ.get('SHMEMX_STAGE_CHUNK_MB','dflt')} "
-      f"nt={os.environ.get('SHMEMX_COPY_NT','dflt')} nodes src {node_of(src)} tgt {node_of(tgt)} cpu {os.sched_getaffinity(0).__len__()} "
+      f"nodes src {node_of(src)} tgt {node_of(tgt)} cpu {os.sched_getaffinity(0).__len__()} "
       f"{t*1e3:.2f} ms {n*8/t/2**30:.1f} GiB/s (min {n*8/max(ts)/2**30:.1f} max {n*8/min(ts)/2**30:.1f}) "
       f"ok={bool((tgt==src).all())}", flush=True)

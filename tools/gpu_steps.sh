@@ -14,21 +14,14 @@
 #   pmc_kernels    every shipped kernel (tools/pmc_kernels.py): trace + FETCH/WRITE passes
 #   soak           the randomized multi-PE soak (tests/gpu_ipc_child.py "soak"),
 #                  $SOAK_SEEDS x $SOAK_ITERS draws
-#   isx_mirror     tools/isx_mirror_latency.py with and without the small-result settle
+#   isx_mirror     tools/isx_mirror_latency.py, plain and with the collective schedule forced
 #   mirror_cost    tools/mirror_cost_probe: page-protection changes and block flushes
-# $TAG names the round's files (default r05).
+# $TAG names the round's files (default r06).
 #   small_calls    tools/small_call_probe.py plain and under rocprofv3 (1 PE; IPC / RCCL collective schedule forced)
-#   e2e_numa       the pageable e2e with the copy gangs pinned to the GPU's NUMA node (gpu) or not (all)
-#   fused_blocks   tools/small_call_probe.py on DIRECT's fused one shot per $SHMEMX_FUSED_BLOCKS
-#   copy_lab       tools/copy_lab: host copies through the staging slot, 4/8/16 threads
-#   e2e_nt         tools/e2e_sweep.py per $E2E_CHUNK x $E2E_THREADS x $E2E_NT (chunk MiB, copy threads, NT mask)
 #   ceiling        tools/stream_lab: copy / read / fill ceilings beside the fold
 #   write          tools/stream_lab: write-only shapes (what bounds the fold's stores)
 #   fold2, copy2, gs  tools/stream_lab: fold / copy shapes the write-only lab suggests
 #   copy           tools/copy_probe.py under a rocprofv3 kernel trace: the library's copy kernel
-#   midsize        the mid-size fold: tools/stream_lab fold shapes and the library's
-#                  fold after a read-only flush (cold_midsize_probe.py), under
-#                  rocprofv3 kernel traces, per size
 #   rehearse2      bench.py N = 2 on the IPC transport, both ranks on this GPU
 #   rehearse8      the same with 8 ranks
 #   rehearse_rccl  bench.py N = $REH_N (2) on the RCCL transport against the RCCL test double
@@ -52,7 +45,7 @@ json_line() {   # json_line <log> <json>: the bench line alone, as a JSON file
 }
 
 BENCH_HEAD="python3 bench.py --steps 20 --warmup 5 --extras 0 --no-cpu-baseline"
-TAG=${TAG:-r05}
+TAG=${TAG:-r06}
 
 for step in "$@"; do
     case $step in
@@ -92,17 +85,9 @@ for step in "$@"; do
             grep -E "PASSED|FAILED|passed|failed" $O/soak_$seed.log | tail -6
         done ;;
     isx_mirror)
-        SHMEMX_MIRROR_SETTLE_KB=0 run 120 $O/isx_mirror_before.json python3 tools/isx_mirror_latency.py 3000
-        run 120 $O/isx_mirror_after.json python3 tools/isx_mirror_latency.py 3000
-        SHMEMX_FORCE_COLLECTIVE=1 SHMEMX_MIRROR_SETTLE_KB=0 run 120 $O/isx_mirror_coll_before.json python3 tools/isx_mirror_latency.py 2000
-        SHMEMX_FORCE_COLLECTIVE=1 run 120 $O/isx_mirror_coll_after.json python3 tools/isx_mirror_latency.py 2000
-        cat $O/isx_mirror_*.json ;;
-    e2e_nt)   # the pageable host-resident path: copy threads x streaming-store mask
-        for ch in ${E2E_CHUNK:-16}; do for th in ${E2E_THREADS:-8 16}; do for nt in ${E2E_NT:-0 1 2 3}; do
-            SHMEMX_STAGE_CHUNK_MB=$ch SHMEMX_COPY_THREADS=$th SHMEMX_COPY_NT=$nt run 120 $O/e2e_nt_${ch}_${th}_${nt}.txt \
-                python3 tools/e2e_sweep.py
-            cat $O/e2e_nt_${ch}_${th}_${nt}.txt
-        done; done; done ;;
+        run 120 $O/isx_mirror.json python3 tools/isx_mirror_latency.py 3000
+        SHMEMX_FORCE_COLLECTIVE=1 run 120 $O/isx_mirror_coll.json python3 tools/isx_mirror_latency.py 2000
+        cat $O/isx_mirror*.json ;;
     small_calls)   # configs[0]'s call at n 1/1024/4096, heap and host operands, wall (C timer) and kernel time
         for mode in plain ipc_coll rccl_coll; do
             envs=""; [ $mode = ipc_coll ] && envs="SHMEMX_TRANSPORT=ipc SHMEMX_FORCE_COLLECTIVE=1"
@@ -116,22 +101,6 @@ for step in "$@"; do
                 || cp $O/small_calls_${mode}_trace/*/*kernel_stats.csv $O/small_calls_${mode}_kernel_stats.csv
             cut -d, -f1-5 $O/small_calls_${mode}_kernel_stats.csv | cut -c1-220
         done ;;
-    fused_blocks)   # DIRECT's fused one shot at 1 PE (IPC, collective forced) per grid size
-        for b in ${FB_BLOCKS:-64 32 16 8 64}; do
-            SHMEMX_FUSED_BLOCKS=$b SHMEMX_TRANSPORT=ipc SHMEMX_FORCE_COLLECTIVE=1 run 120 $O/fused_blocks_$b.json \
-                python3 tools/small_call_probe.py 3000
-            echo "blocks $b: $(grep '^{' $O/fused_blocks_$b.json | cut -c1-400)"
-        done ;;
-    e2e_numa)   # the pageable path with the copy gangs pinned to the GPU's NUMA node or not, alternating
-        for f in /sys/devices/system/node/node*/cpulist; do echo "$f: $(cat $f)"; done
-        python3 -c "import ctypes;h=ctypes.CDLL('libamdhip64.so');b=ctypes.create_string_buffer(64);h.hipDeviceGetPCIBusId(b,64,0);import sys;bus=b.value.decode().lower();print('GPU', bus, 'numa_node', open('/sys/bus/pci/devices/'+bus+'/numa_node').read().strip())" || true
-        cat /sys/kernel/mm/transparent_hugepage/enabled || true
-        for rep in 1 2 3; do for cpus in ${E2E_CPUS:-all gpu data}; do for thp in ${E2E_THP:-0}; do
-            SHMEMX_RING_THP=$thp SHMEMX_COPY_CPUS=$cpus run 120 $O/e2e_numa_${cpus}_${thp}_$rep.txt python3 tools/e2e_sweep.py
-            echo "cpus=$cpus ring_thp=$thp $(grep threads $O/e2e_numa_${cpus}_${thp}_$rep.txt)"
-        done; done; done ;;
-    copy_lab)   # host memcpy vs streaming stores through a 16 MiB slot (no GPU)
-        for t in 4 8 16; do run 120 $O/copy_lab_$t.txt ./tools/copy_lab $t 256 5; cat $O/copy_lab_$t.txt; done ;;
     mirror_cost) run 120 $O/mirror_cost.txt ./tools/mirror_cost_probe 2000; cat $O/mirror_cost.txt ;;
     ceiling)
         for nd in 33554432 67108864; do
@@ -147,16 +116,6 @@ for step in "$@"; do
         run 300 $O/copy_probe.txt rocprofv3 --kernel-trace --stats -d $O/copy_probe -o t --output-format csv \
             -- python3 tools/copy_probe.py
         grep copy $O/copy_probe.txt; python3 tools/trace_by_grid.py $O/copy_probe fold_kernel ;;
-    midsize)
-        for nd in 524288 2097152 8388608; do
-            run 300 $O/midsize_lab_$nd.txt rocprofv3 --kernel-trace --stats -d $O/midsize_lab_$nd -o t \
-                --output-format csv -- ./tools/stream_lab $nd 3 20 fold
-            python3 tools/trace_by_grid.py $O/midsize_lab_$nd > $O/midsize_lab_${nd}_trace.txt
-        done
-        run 300 $O/midsize_probe.txt rocprofv3 --kernel-trace --stats -d $O/midsize_probe -o t --output-format csv \
-            -- python3 tools/cold_midsize_probe.py 20 read,warm 1048576,4194304,16777216 -1
-        python3 tools/trace_by_grid.py $O/midsize_probe fold_kernel > $O/midsize_probe_trace.txt
-        cat $O/midsize_probe.txt | grep config; cat $O/midsize_probe_trace.txt ;;
     rehearse2|rehearse8)
         np=${step#rehearse}
         q=4; [ "$np" -gt 4 ] && q=2     # 8 processes' queues on one GPU (tests/test_gpu_ipc.py)

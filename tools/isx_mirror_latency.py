@@ -3,11 +3,11 @@ its bucket size into a shmem_malloc'd long long with a plain host store, calls
 shmem_longlong_sum_to_all(nreduce = 1) (examples/ISx/SHMEM/isx.c:615-624),
 then reads the total with a plain host load.  One PE here (the copy path of
 reduce-op.c:213-216); $SHMEMX_FORCE_COLLECTIVE=1 runs the collective schedule
-instead.  Run with $SHMEMX_MIRROR_SETTLE_KB=0 (the result left DEVICE_NEWER:
-the host load faults and fetches its 64 KiB block) and unset (the light path:
-only the source's 8 written bytes go up, no block changes state or
-protection, and the call's last kernel stores the result into the view as
-well) to see what each costs.
+instead.  The light path: only the source's 8 written bytes go up, no block
+changes state or protection, and the call's last kernel stores the result
+into the view as well (profiles/r04_isx_mirror.txt has the cost of the
+result left DEVICE_NEWER instead: the host load faults and fetches its 64 KiB
+block).
 
     python tools/isx_mirror_latency.py [rounds]
 Prints one JSON line: medians in microseconds of the call alone, the host
@@ -52,7 +52,6 @@ for r in range(rounds + 50):
         shm.mirror_stats(reset=True)
 st = shm.mirror_stats(reset=True)
 print(json.dumps({
-    "settle_kb": os.environ.get("SHMEMX_MIRROR_SETTLE_KB", "256 (default)"),
     "force_collective": os.environ.get("SHMEMX_FORCE_COLLECTIVE", "0"),
     "rounds": rounds, "call_us": round(statistics.median(call) * 1e6, 2),
     "host_load_us": round(statistics.median(load) * 1e6, 2),
