@@ -218,9 +218,10 @@ def test_auto_table_from_environment(tmp_path, table):
         expect = [["double", "sum", 16, 0, 0, 4, "allreduce"],
                   ["double", "sum", 1 << 20, 0, 0, 4, "rccl"],
                   ["long", "xor", 4096, 0, 0, 4, "a2a"],
-                  # a partial set: RCCL on its members-only communicator
-                  ["double", "sum", 4099, 0, 1, 2, "allreduce"],
-                  ["double", "sum", 1 << 20, 1, 0, 3, "rccl"],
+                  ["float", "max", 4099, 0, 0, 4, "gather"],       # each PE's own order
+                  # a partial set: A2A (its own RCCL communicator only when named)
+                  ["double", "sum", 4099, 0, 1, 2, "a2a"],
+                  ["double", "sum", 1 << 20, 1, 0, 3, "a2a"],
                   ["long", "xor", 4099, 1, 0, 3, "a2a"]]
     env.update({"SHMEMX_TRANSPORT": "rccl", "FAKE_RCCL": fake, "AUTO_EXPECT": json.dumps(expect)})
     reports = run_pes(tmp_path, 4, "autotable", env, timeout=300)
