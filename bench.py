@@ -472,6 +472,8 @@ def latency_extras(world, barrier, max_over_ranks):
     import numpy as np
     out = {}
     psync = np.full(128, -1, dtype=np.int64)
+    if hasattr(shm, "service_stats"):
+        shm.service_stats(reset=True)
     for n in (1, 64, 4096):
         for where in ("host", "device"):
             if where == "host":
@@ -496,6 +498,34 @@ def latency_extras(world, barrier, max_over_ranks):
                 out[f"longlong_sum_n{n}_{where}_from_c_us"] = {
                     "median": round(max_over_ranks(statistics.median(ct)), 2),
                     "min": round(max_over_ranks(min(ct)), 2)}
+    # BASELINE configs[0]'s call, shmem_int_sum_to_all, at n = 1 / 1024 / 4096:
+    # against the reference CPU's 3.0 / 3.9 / 8.8 us (cpu_baseline.table);
+    # at PE_size 1 up to 32 KiB it is the resident service workgroup's
+    # (csrc/service.hip), which these counters show
+    if hasattr(shm, "service_stats"):
+        out["service_stats_longlong"] = shm.service_stats(reset=True)
+    for n in (1, 1024, 4096):
+        for where in ("host", "device"):
+            if where == "host":
+                src = np.arange(n, dtype=np.int32)
+                tgt = np.zeros(n, dtype=np.int32)
+            else:
+                src = torch.arange(n, dtype=torch.int32, device="cuda")
+                tgt = torch.zeros(n, dtype=torch.int32, device="cuda")
+                torch.cuda.synchronize()
+            barrier()
+            ct = call_times_us("int", "sum", tgt, src, n, 0, 0, world, psync, 5, 500)
+            if ct:
+                out[f"int_sum_n{n}_{where}_from_c_us"] = {
+                    "median": round(max_over_ranks(statistics.median(ct)), 2),
+                    "p10": round(max_over_ranks(sorted(ct)[len(ct) // 10]), 2),
+                    "min": round(max_over_ranks(min(ct)), 2)}
+            want = np.arange(n, dtype=np.int32) * (world if world > 1 else 1)
+            got = tgt if where == "host" else tgt.cpu().numpy()
+            if world == 1 and not np.array_equal(got, want):
+                out[f"int_sum_n{n}_{where}_error"] = "wrong result"
+    if hasattr(shm, "service_stats"):
+        out["service_stats_int"] = shm.service_stats(reset=True)
     out["from_c_note"] = ("*_from_c_us: the same blocking call timed call by call from C "
                           "(tools/call_timer.c), without the Python caller's overhead")
     return out

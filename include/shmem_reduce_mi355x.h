@@ -333,6 +333,17 @@ int shmemx_rccl_register_heap(int on);
  * launches past the 4096 that went untimed to *dropped (may be NULL); it
  * returns how many were written and starts over.  Off by default; timing
  * does not change what runs. */
+/* The resident service workgroup (DESIGN.md §6 "Small messages"): a
+ * blocking one-member call (PE_size 1, a copy) of at most 32 KiB is done by
+ * one workgroup that stays on the GPU polling a host-coherent mailbox, with
+ * no kernel launch, whenever the legacy default stream and the library's
+ * stream have no work left; it leaves after 200 us without a request (so a
+ * program's hipDeviceSynchronize waits that long at most) and at
+ * shmem_finalize.  $SHMEMX_SERVICE=0 turns it off.  Stats: out[0] calls
+ * served, out[1] launches of the workgroup, out[2] calls that found a stream
+ * busy and launched their copy instead; returns how many were written. */
+int shmemx_service_stats(unsigned long long *out, int nout, int reset);
+
 int shmemx_kernel_timing(int on);
 int shmemx_kernel_times(double *us, int *kind, int max, unsigned long long *dropped);
 

@@ -193,7 +193,7 @@ void ensure_fence() {
     SHMX_HIP(hipMalloc(&gs, 2 * sizeof(unsigned int)));
     SHMX_HIP(hipMemset(gs, 0, 2 * sizeof(unsigned int)));
     g_fence.gsync = static_cast<unsigned int *>(gs);
-    SHMX_HIP(hipDeviceSynchronize());
+    device_sync();
     g_fence.host_seen = static_cast<unsigned int *>(h);
     g_fence.dev_seen = static_cast<unsigned int *>(d);
     g_fence.dev_stats = static_cast<unsigned long long *>(st);
@@ -327,7 +327,7 @@ int direct_stats(double *out, int nout, bool reset) {
     for (int i = 0; i < kNumPhases; ++i) all[1 + i] = g_phase_us[i];
     unsigned long long dev[2] = {0, 0};
     if (g_fence.dev_stats) {
-        SHMX_HIP(hipDeviceSynchronize());
+        device_sync();
         SHMX_HIP(hipMemcpy(dev, g_fence.dev_stats, sizeof dev, hipMemcpyDeviceToHost));
     }
     all[1 + kNumPhases] = g_fence.host_checks;

@@ -153,7 +153,7 @@ void record_writer(void *stream) {
 void wait_writers() {
     std::lock_guard<std::mutex> lk(g_wmu);
     if (g_sync_device) {
-        SHMX_HIP(hipDeviceSynchronize());
+        device_sync();
         g_sync_device = false;
         for (Writer &w : g_writers) w.armed = false;
         return;
@@ -326,7 +326,7 @@ bool ensure_segment() {
         // every block starts CLEAN; otherwise only the signal area is zeroed
         const uint64_t zero_from = mirrored() ? 0 : bytes - kSignalBytes;
         SHMX_HIP(hipMemset(g_heap.base + zero_from, 0, bytes - zero_from));
-        SHMX_HIP(hipDeviceSynchronize());
+        device_sync();
         node::publish(node::kHeap, p, bytes);   // peers map it after the allocation's barrier
         if (mirrored()) {
             if (!mirror::create(g_heap.arena.capacity(), mirror::Backend{mir_to_device, mir_to_host,
@@ -399,7 +399,7 @@ bool free(void *p) {
     if (in_view(p)) return g_heap.arena.free((uint64_t)(static_cast<char *>(p) - g_heap.view));
     auto it = g_heap.priv.find(p);
     if (it == g_heap.priv.end()) return false;
-    SHMX_HIP(hipDeviceSynchronize());
+    device_sync();
     SHMX_HIP(priv_free(it->second.base));
     g_heap.priv.erase(it);
     return true;
@@ -534,7 +534,7 @@ DeviceWrite::DeviceWrite(void *p, size_t bytes, void *stream, bool light)
 void DeviceWrite::close(bool copied) {
     if (!open_) return;
     open_ = false;
-    record_writer(stream_);
+    if (!done_) record_writer(stream_);
     if (light_) mirror::end_light_write(off_, bytes_, copied);
     else mirror::end_device_write(off_, bytes_);
 }

@@ -98,6 +98,9 @@ class DeviceWrite {
     DeviceWrite &operator=(const DeviceWrite &) = delete;
     void *ptr() const { return dev_; }
     bool light() const { return light_; }
+    // the write has completed (a blocking call waited for its work): close()
+    // records no writer event to wait for
+    void completed() { stream_ = nullptr; done_ = true; }
     // record the writer and end the write in flight (the destructor's work);
     // a light write's result goes into the view here unless `copied`
     void close(bool copied = false);
@@ -122,6 +125,7 @@ class DeviceWrite {
     bool open_;
     bool fresh_ = false;
     bool light_ = false;
+    bool done_ = false;
 };
 // While one lives (a blocking call, whose every kernel and copy runs on the
 // library stream): flushes of host-view blocks to HBM are enqueued on that

@@ -590,7 +590,7 @@ void *grow(void *&buf, size_t &have, size_t need) {
     if (need <= have) return buf;
     if (buf) {
         // the old buffer may still be in use on any caller stream
-        SHMX_HIP(hipDeviceSynchronize());
+        device_sync();
         SHMX_HIP(hipFree(buf));
         buf = nullptr;
         have = 0;
@@ -948,6 +948,7 @@ void pshmem_finalize(void) {
     std::lock_guard<std::recursive_mutex> lk(g_mu);
     if (!g_state.inited) return;
     (void)hipStreamSynchronize(g_state.stream);
+    service_release();
     // collective: no PE frees memory its peers may still be reading
     if (node::up()) node::barrier(0, 1, g_state.npes);
     if (g_state.comm && g_state.rccl_reg) (void)ncclCommDeregister(g_state.comm, g_state.rccl_reg);

@@ -57,7 +57,7 @@ void ring_free() {
 static bool ring_reserve(size_t slot_bytes) {
     if (g_state.ring && g_state.ring_slot >= slot_bytes) return true;
     if (g_state.ring) {
-        SHMX_HIP(hipDeviceSynchronize());
+        device_sync();
         ring_free();
     }
     const size_t bytes = 2 * kRingSlots * slot_bytes;
@@ -484,6 +484,10 @@ void reduce_blocking(int type, int op, void *target, const void *source,
             // settle()'s copy-back, and the next call on another stream, must
             // not read HBM before it has landed
             if (failed) SHMX_HIP(hipStreamSynchronize(g_state.stream));
+            // every blocking call returns with its work complete: no writer
+            // event on the library stream (it would keep the stream busy for
+            // the next call's service check, service.hip)
+            t.completed();
             t.settle(mirror_settle_limit(), copied || (failed && t.light()));
             return;
         }
@@ -545,9 +549,15 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
     if (tdev && sdev) {
         if (collective && bytes > kSmallHostBytes && !calls_agree(start, logstride, size, 1)) return;
         if (plan.nmembers == 1 && !collective && !overlap(target, source, bytes)) {
-            // a one-member set is a copy (reduce-op.c:213-216), and the copy
-            // kernel tells the host itself when it is done (one workgroup;
-            // a marker kernel otherwise): no stream wait
+            // a one-member set is a copy (reduce-op.c:213-216): up to 4 KiB by
+            // the resident service workgroup when the streams it is ordered
+            // after are idle (no launch; service.hip), else the copy kernel,
+            // which tells the host itself when it is done (one workgroup; a
+            // marker kernel otherwise): no stream wait either way
+            if (bytes <= kServiceMaxBytes && service_copy(target, g_state.settle_dst, source, bytes)) {
+                if (g_state.settle_dst) g_state.settled = true;
+                return;
+            }
             const HostSignal sig = next_host_signal();
             const void *in[1] = {source};
             if (g_state.settle_dst) {
@@ -617,15 +627,18 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
             if (!rc && !tdev) std::memcpy(target, bout, bytes);
             return;
         }
-        // the copy kernel signals the host when its stores have landed
-        const HostSignal sig = next_host_signal();
-        SHMX_HIP(launch_fold_signal(type, op, t, in, 1, (size_t)nreduce, s, sig));
-        wait_host_signal(sig, s);
+        // the service workgroup (service.hip), or the copy kernel, which
+        // signals the host when its stores have landed
+        if (!(bytes <= kServiceMaxBytes && service_copy(t, nullptr, in[0], bytes))) {
+            const HostSignal sig = next_host_signal();
+            SHMX_HIP(launch_fold_signal(type, op, t, in, 1, (size_t)nreduce, s, sig));
+            wait_host_signal(sig, s);
+        }
         if (!tdev) std::memcpy(target, bout, bytes);
         return;
     }
     if (bytes > g_state.stage_bytes) {
-        SHMX_HIP(hipDeviceSynchronize());
+        device_sync();
         if (g_state.stage_src) SHMX_HIP(hipFree(g_state.stage_src));
         if (g_state.stage_tgt) SHMX_HIP(hipFree(g_state.stage_tgt));
         g_state.stage_src = g_state.stage_tgt = nullptr;

@@ -128,6 +128,16 @@ void set_comms_release();
 void parallel_copy(void *dst, const void *src, size_t bytes, bool nt = false);
 void ring_free();   // the staging ring (staging.cpp), at finalize
 int gpu_numa_node(int device);   // NUMA node of a HIP device's PCI function, or -1
+// The resident service workgroup (service.hip): a small one-member blocking
+// call's copy (reduce-op.c:213-216) done by a workgroup that is already on
+// the GPU, polling a host-coherent mailbox, instead of a launch.  dst2: a
+// second destination or null.  false = not taken (the legacy or library
+// stream still has work, or $SHMEMX_SERVICE=0): the caller launches.
+constexpr size_t kServiceMaxBytes = size_t(32) << 10;
+bool service_copy(void *dst, void *dst2, const void *src, size_t bytes);
+void service_quiesce();   // the workgroup leaves now, if it is up
+void service_release();   // shmem_finalize (and at exit)
+void device_sync();       // service_quiesce, then hipDeviceSynchronize
 // The plan of one call (shmemx_reduce_plan) and the device-resident engine
 // (runtime.cpp); the host staging of the blocking entry points (staging.cpp)
 // runs the engine chunk by chunk.

@@ -178,6 +178,8 @@ def lib() -> ctypes.CDLL:
     L.shmemx_mirror_acquire.restype = i
     L.shmemx_direct_stats.argtypes = [ctypes.POINTER(ctypes.c_double), i, i]
     L.shmemx_direct_stats.restype = i
+    L.shmemx_service_stats.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), i, i]
+    L.shmemx_service_stats.restype = i
     L.shmemx_host_register.argtypes = [vp, sz]
     L.shmemx_host_register.restype = i
     L.shmemx_host_unregister.argtypes = [vp]
@@ -440,6 +442,18 @@ def direct_stats(reset: bool = True) -> dict:
     out = {"calls": buf[0]}
     out.update({name: buf[i + 1] for i, name in enumerate(names[:max(0, k - 1)])})
     return out
+
+
+SERVICE_STATS = ("served", "launches", "streams_busy")
+
+
+def service_stats(reset: bool = False) -> dict:
+    """shmemx_service_stats: small one-member blocking calls the resident
+    service workgroup served, its launches, and the calls that found the
+    legacy or library stream busy and launched their copy instead."""
+    buf = (ctypes.c_ulonglong * len(SERVICE_STATS))()
+    k = lib().shmemx_service_stats(buf, len(buf), 1 if reset else 0)
+    return {name: buf[i] for i, name in enumerate(SERVICE_STATS[:max(0, k)])}
 
 
 MIRROR_STATS = ("write_faults", "read_faults", "blocks_flushed", "blocks_fetched",

@@ -36,17 +36,26 @@
         }                                                                                  \
     } while (0)
 
-struct Mailbox {
-    unsigned long long seq;    // written by the host last (release)
+struct alignas(64) Mailbox {
+    // one 64-byte line the device reads; the host writes the fields and
+    // check first, seq last (release)
+    unsigned long long seq;
     unsigned long long quit;
     const void *src;
     void *dst;
     unsigned long long bytes;
-    unsigned long long polls;   // device heartbeat: polls so far (every 1024th)
+    unsigned long long check;   // seq ^ src ^ dst ^ bytes ^ kMix: a torn read shows
     unsigned long long pad[2];
-    unsigned long long done;   // written by the device (system-scope release)
+    // the device's line
+    alignas(64) unsigned long long done;   // (system-scope release)
+    unsigned long long polls;   // heartbeat: polls so far (every 1024th)
 };
+constexpr unsigned long long kMix = 0x9E3779B97F4A7C15ull;
 
+// LINE: wave 0's lanes 0-5 read the mailbox's first line with one load
+// instruction (the descriptor arrives with the sequence number, no second
+// round trip over PCIe); the check word catches a torn read
+template <bool LINE>
 __global__ __launch_bounds__(256) void service_kernel(Mailbox *mb, unsigned long long served,
                                                       unsigned long long idle_ticks) {
     __shared__ unsigned long long s_seq;
@@ -56,7 +65,39 @@ __global__ __launch_bounds__(256) void service_kernel(Mailbox *mb, unsigned long
     unsigned long long last = served, npoll = 0;
     unsigned long long t_last = __builtin_amdgcn_s_memrealtime();
     for (;;) {
-        if (threadIdx.x == 0) {
+        if (LINE && threadIdx.x < 64) {
+            const unsigned long long *line = reinterpret_cast<const unsigned long long *>(mb);
+            const int lane = threadIdx.x;
+            unsigned long long q = 0;
+            for (;;) {
+                const unsigned long long v =
+                    lane < 6 ? __hip_atomic_load(line + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0;
+                q = __shfl(v, 0);
+                const unsigned long long quit = __shfl(v, 1);
+                if (q != last) {
+                    const unsigned long long a = __shfl(v, 2), b = __shfl(v, 3), n = __shfl(v, 4),
+                                             c = __shfl(v, 5);
+                    if ((q ^ a ^ b ^ n ^ kMix) == c) {
+                        if (lane == 0) {
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope: fresh lines
+                            s_src = reinterpret_cast<const unsigned char *>(a);
+                            s_dst = reinterpret_cast<unsigned char *>(b);
+                            s_bytes = n;
+                        }
+                        break;
+                    }
+                    continue;   // torn: read the line again
+                }
+                if (quit || __builtin_amdgcn_s_memrealtime() - t_last > idle_ticks) {
+                    q = 0;
+                    break;
+                }
+                if (lane == 0 && (++npoll & 1023) == 0)
+                    __hip_atomic_store(&mb->polls, npoll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (lane == 0) s_seq = q;
+        } else if (!LINE && threadIdx.x == 0) {
             unsigned long long q = 0;
             for (;;) {
                 q = __hip_atomic_load(&mb->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -181,8 +222,15 @@ int main(int argc, char **argv) {
     // 2. mailbox round trips (idle timeout 200 us)
     const unsigned long long idle_ticks = 200 * 100;   // s_memrealtime: 100 MHz
     unsigned long long seq = 0;
+    bool line_mode = false;
+    // (re)launch: the kernel starts from the last request the previous one
+    // completed, so a request posted while it was leaving is served
     auto launch_service = [&] {
-        hipLaunchKernelGGL(service_kernel, dim3(1), dim3(256), 0, svc, mb, seq, idle_ticks);
+        const unsigned long long served = __atomic_load_n(&mb->done, __ATOMIC_ACQUIRE);
+        if (line_mode)
+            hipLaunchKernelGGL(service_kernel<true>, dim3(1), dim3(256), 0, svc, mb, served, idle_ticks);
+        else
+            hipLaunchKernelGGL(service_kernel<false>, dim3(1), dim3(256), 0, svc, mb, served, idle_ticks);
         CK(hipGetLastError());
     };
     auto post = [&](bool query) {
@@ -195,6 +243,7 @@ int main(int argc, char **argv) {
         mb->dst = dst;
         mb->bytes = bytes;
         ++seq;
+        mb->check = seq ^ reinterpret_cast<uintptr_t>(src) ^ reinterpret_cast<uintptr_t>(dst) ^ bytes ^ kMix;
         __atomic_store_n(&mb->seq, seq, __ATOMIC_RELEASE);
         const volatile unsigned long long *d = &mb->done;
         const double t0 = now_us();
@@ -246,6 +295,35 @@ int main(int argc, char **argv) {
         t.push_back(now_us() - t0);
     }
     report("cold_relaunch", t);
+    // 4. the line-read variant, warm and after idle gaps
+    g_phase = "line";
+    std::fprintf(stderr, "phase %s\n", g_phase);
+    __atomic_store_n(&mb->quit, 1ull, __ATOMIC_RELEASE);
+    {
+        const double t0 = now_us();
+        while (hipStreamQuery(svc) == hipErrorNotReady) watchdog(t0, "service exit before line");
+    }
+    __atomic_store_n(&mb->quit, 0ull, __ATOMIC_RELEASE);
+    line_mode = true;
+    launch_service();
+    t.clear();
+    for (int i = 0; i < reps + 50; ++i) {
+        const double t0 = now_us();
+        post(false);
+        if (i >= 50) t.push_back(now_us() - t0);
+    }
+    report("mailbox_line", t);
+    t.clear();
+    for (int i = 0; i < 200; ++i) {
+        const double ts = now_us();
+        while (now_us() - ts < 400) {
+        }
+        const double t0 = now_us();
+        if (hipStreamQuery(svc) == hipSuccess) launch_service();
+        post(false);
+        t.push_back(now_us() - t0);
+    }
+    report("line_cold", t);
     // correctness: dst holds src's bytes
     std::vector<unsigned char> h(bytes);
     g_phase = "check";
