@@ -340,8 +340,9 @@ int shmemx_rccl_register_heap(int on);
  * stream have no work left; it leaves after 200 us without a request (so a
  * program's hipDeviceSynchronize waits that long at most) and at
  * shmem_finalize.  $SHMEMX_SERVICE=0 turns it off.  Stats: out[0] calls
- * served, out[1] launches of the workgroup, out[2] calls that found a stream
- * busy and launched their copy instead; returns how many were written. */
+ * served, out[1] launches of the workgroup, out[2] / out[3] calls that found
+ * the legacy default stream / the library's stream busy and launched their
+ * copy instead; returns how many were written. */
 int shmemx_service_stats(unsigned long long *out, int nout, int reset);
 
 int shmemx_kernel_timing(int on);

@@ -118,6 +118,7 @@ int barrier_impl(int start, int logstride, int size) {
     SetInfo si;
     if (int rc = set_info(start, logstride, size, si)) return rc;
     hipStream_t s = g_state.stream;
+    g_state.lib_stream_dirty = true;   // until someone sees it drained (service.hip)
     // mirrored heap: the host's stores to symmetric objects reach HBM, where
     // the peers' kernels read them after the barrier
     heap::flush_view();
@@ -164,6 +165,7 @@ int broadcast_impl(size_t esize, void *target, const void *source, size_t nelems
     if (!bytes || !collective(si)) return SHMEMX_OK;  // the root's target is never written
     if ((si.m == root_idx && !source) || (si.m != root_idx && !target)) return set_error(SHMEMX_EINVAL);
     hipStream_t s = g_state.stream;
+    g_state.lib_stream_dirty = true;   // until someone sees it drained (service.hip)
     // mirrored heap: operands in the host view run on their HBM twins (a
     // non-root's target is DEVICE_NEWER from here, heap.h DeviceWrite)
     if (si.m == root_idx) source = heap::device_operand(source, bytes);
@@ -210,6 +212,7 @@ int collect_impl(size_t esize, void *target, const void *source, size_t nelems, 
     SetInfo si;
     if (int rc = set_info(start, logstride, size, si)) return rc;
     hipStream_t s = g_state.stream;
+    g_state.lib_stream_dirty = true;   // until someone sees it drained (service.hip)
     // mirrored heap: operands in the host view run on their HBM twins (the
     // target's length is known only after the counts are exchanged)
     void *const user_target = target;
@@ -287,6 +290,7 @@ int checksum_impl(int type, const void *ptr, size_t nelems, unsigned long long *
     if (int rc = ensure_init()) return rc;
     if (!out || type_size(type) == 0) return set_error(SHMEMX_EINVAL);
     hipStream_t s = g_state.stream;
+    g_state.lib_stream_dirty = true;   // until someone sees it drained (service.hip)
     const size_t bytes = nelems * type_size(type);
     if (bytes) ptr = heap::device_operand(ptr, bytes);   // mirrored heap: the HBM twin
     DevBuf in = device_in(ptr, bytes, g_state.cws_src, g_state.cws_src_bytes, s);
@@ -339,6 +343,8 @@ int exchange_u64(int start, int logstride, int size, unsigned long long mine,
         node::barrier(si.start, si.step, si.P);   // all read before any descriptor changes
     } else if (collective(si)) {
         hipStream_t s = g_state.stream;
+        g_state.lib_stream_dirty = true;
+    g_state.lib_stream_dirty = true;   // until someone sees it drained (service.hip)
         unsigned long long *d = static_cast<unsigned long long *>(
             grow(g_state.token, g_state.token_bytes, sizeof(unsigned long long) * (si.P + 8)));
         if (!d) return set_error(SHMEMX_ENOMEM);

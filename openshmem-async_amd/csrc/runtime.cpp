@@ -132,12 +132,17 @@ void wait_host_signal(const HostSignal &sig, hipStream_t s) {
     // (profiles/r03_latency_ab.txt): there the stream wait is the wait.
     if (!g_state.return_on_signal) {
         SHMX_HIP(hipStreamSynchronize(s));
+        if (s == g_state.stream) g_state.lib_stream_dirty = false;
         return;
     }
     const volatile unsigned long long *w = sig.word;
     const auto t0 = std::chrono::steady_clock::now();
     for (unsigned k = 1;; ++k) {
-        if (*w == sig.value) return;
+        if (*w == sig.value) {
+            // everything enqueued on s before the signal has completed
+            if (s == g_state.stream) g_state.lib_stream_dirty = false;
+            return;
+        }
         __builtin_ia32_pause();
         if ((k & 1023) == 0) {
             // a drained stream (its work is complete whatever the word says)
@@ -148,6 +153,7 @@ void wait_host_signal(const HostSignal &sig, hipStream_t s) {
         }
     }
     SHMX_HIP(hipStreamSynchronize(s));
+    if (s == g_state.stream) g_state.lib_stream_dirty = false;
 }
 
 static int env_int(const char *a, const char *b, int dflt) {
@@ -906,6 +912,7 @@ int reduce_on_stream(int type, int op, void *target, const void *source,
     if (nreduce > 0 && (!device_accessible(heap::twin(target)) || !device_accessible(src)))
         return set_error(SHMEMX_EINVAL);
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : g_state.stream;
+    if (s == g_state.stream) g_state.lib_stream_dirty = true;   // (service.hip)
     if (nreduce >= 0 && op_valid(type, op))
         trace_reference_overlap(target, source, type_size(type) * (size_t)nreduce);
     // the host view of the target is stale from here: a host access to its
@@ -1106,6 +1113,7 @@ int shmemx_host_unregister(void *base) {
 void *shmemx_get_stream(void) {
     std::lock_guard<std::recursive_mutex> lk(g_mu);
     if (ensure_init()) return nullptr;
+    g_state.lib_stream_exported = true;   // the caller may put anything on it (service.hip)
     return g_state.stream;
 }
 

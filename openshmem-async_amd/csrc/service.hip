@@ -20,7 +20,11 @@
 // the library's stream (the buffers a plain HIP program, or PyTorch's
 // default stream, just wrote): the mailbox is used only when both have no
 // work left (hipStreamQuery, 0.17 us for the two), else the call launches
-// its copy on the library stream as before.
+// its copy on the library stream as before.  The library stream is asked
+// only when it may hold work nobody waited for (state.h lib_stream_dirty):
+// after a blocking call the runtime keeps reporting it busy for some
+// microseconds after the work is done, and every next call would then take
+// the launch path, and keep it so.
 //
 // Lifetime.  The workgroup leaves by itself after kIdleUs without a request
 // (every wave reaches that exit: the first wave decides, the workgroup
@@ -170,8 +174,8 @@ struct Service {
     std::chrono::steady_clock::time_point last_use{};
     bool exit_hook = false;
     // shmemx_service_stats: calls served, launches, calls that found the
-    // legacy or library stream busy (and launched their copy instead)
-    unsigned long long served = 0, launches = 0, busy = 0;
+    // legacy / the library stream busy (and launched their copy instead)
+    unsigned long long served = 0, launches = 0, busy_null = 0, busy_lib = 0;
 } g_svc;
 
 bool enabled() {
@@ -242,9 +246,16 @@ bool service_copy(void *dst, void *dst2, const void *src, size_t bytes) {
     if (!enabled() || bytes == 0 || bytes > kServiceMaxBytes || !dst || !src) return false;
     // ordered after the legacy stream and the library stream: only when both
     // have no work left
-    if (!stream_idle(nullptr) || !stream_idle(g_state.stream)) {
-        ++g_svc.busy;
+    if (!stream_idle(nullptr)) {
+        ++g_svc.busy_null;
         return false;
+    }
+    if (g_state.lib_stream_dirty || g_state.lib_stream_exported) {
+        if (!stream_idle(g_state.stream)) {
+            ++g_svc.busy_lib;
+            return false;
+        }
+        g_state.lib_stream_dirty = false;
     }
     if (!ensure()) return false;
     Mailbox *mb = g_svc.mb;
@@ -305,9 +316,10 @@ void device_sync() {
 extern "C" int shmemx_service_stats(unsigned long long *out, int nout, int reset) {
     std::lock_guard<std::recursive_mutex> lk(shmx::g_mu);
     if (!out || nout < 0) return shmx::set_error(SHMEMX_EINVAL), -1;
-    const unsigned long long all[3] = {shmx::g_svc.served, shmx::g_svc.launches, shmx::g_svc.busy};
-    const int k = nout < 3 ? nout : 3;
+    const unsigned long long all[4] = {shmx::g_svc.served, shmx::g_svc.launches, shmx::g_svc.busy_null,
+                                       shmx::g_svc.busy_lib};
+    const int k = nout < 4 ? nout : 4;
     for (int i = 0; i < k; ++i) out[i] = all[i];
-    if (reset) shmx::g_svc.served = shmx::g_svc.launches = shmx::g_svc.busy = 0;
+    if (reset) shmx::g_svc.served = shmx::g_svc.launches = shmx::g_svc.busy_null = shmx::g_svc.busy_lib = 0;
     return k;
 }

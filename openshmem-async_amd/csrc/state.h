@@ -44,6 +44,15 @@ struct State {
     // inside a blocking entry point: wait_host_signal returns as soon as the
     // work's host signal arrives, without seeing the stream idle
     bool return_on_signal = false;
+    // the library stream may hold work nobody has waited for: a
+    // stream-ordered call enqueued on it (cleared when a blocking call's own
+    // work on it, enqueued behind, has been seen complete), or the stream was
+    // handed out (shmemx_get_stream: anything may be on it).  Otherwise every
+    // piece of work on it has completed, and the service workgroup
+    // (service.hip) need not ask the runtime, whose answer lags a kernel's
+    // completion by microseconds.
+    bool lib_stream_dirty = false;
+    bool lib_stream_exported = false;
     // inside a blocking call on a small host-view target (staging.cpp): the
     // device address where the call's last kernel also stores the result (the
     // view's page-locked alias, heap.h DeviceWrite::settle_dst), and whether

@@ -77,11 +77,20 @@ def test_service_ordered_after_the_default_stream(cuda, shm):
         assert shm.last_error() == 0
         assert (dst.cpu().numpy() == rep + 1).all(), rep
     st = shm.service_stats(reset=True)
-    assert st["streams_busy"] >= 1, st
+    assert st["null_stream_busy"] >= 1, st
     # and once the stream is idle the service takes the same call
     torch.cuda.synchronize()
     shm.to_all("double", "sum", dst, big, n, 0, 0, 1)
     assert shm.service_stats(reset=True)["served"] == 1
+    # a call that launched its copy (the stream was busy) does not keep the
+    # next ones off the service: right after it the runtime may still call
+    # the library stream busy, but the library knows its work is done
+    big.fill_(7.0)
+    for _ in range(200):
+        shm.to_all("double", "sum", dst, big, n, 0, 0, 1)
+    st = shm.service_stats(reset=True)
+    assert st["served"] >= 195 and st["library_stream_busy"] == 0, st
+    assert (dst.cpu().numpy() == 7.0).all()
 
 
 def test_service_comes_back_after_idling_out(cuda, shm, oracle):
