@@ -336,13 +336,14 @@ int shmemx_rccl_register_heap(int on);
 /* The resident service workgroup (DESIGN.md §6 "Small messages"): a
  * blocking one-member call (PE_size 1, a copy) of at most 32 KiB is done by
  * one workgroup that stays on the GPU polling a host-coherent mailbox, with
- * no kernel launch, whenever the legacy default stream and the library's
- * stream have no work left; it leaves after 200 us without a request (so a
+ * no kernel launch, after the legacy default stream's and the library
+ * stream's earlier work (the host waits for them first when they still have
+ * some); it leaves after 200 us without a request (so a
  * program's hipDeviceSynchronize waits that long at most) and at
  * shmem_finalize.  $SHMEMX_SERVICE=0 turns it off.  Stats: out[0] calls
  * served, out[1] launches of the workgroup, out[2] / out[3] calls that found
- * the legacy default stream / the library's stream busy and launched their
- * copy instead; returns how many were written. */
+ * the legacy default stream / the library's stream busy and waited for it;
+ * returns how many were written. */
 int shmemx_service_stats(unsigned long long *out, int nout, int reset);
 
 int shmemx_kernel_timing(int on);

@@ -18,13 +18,17 @@
 //
 // Ordering.  A blocking call is ordered after the legacy default stream and
 // the library's stream (the buffers a plain HIP program, or PyTorch's
-// default stream, just wrote): the mailbox is used only when both have no
-// work left (hipStreamQuery, 0.17 us for the two), else the call launches
-// its copy on the library stream as before.  The library stream is asked
-// only when it may hold work nobody waited for (state.h lib_stream_dirty):
-// after a blocking call the runtime keeps reporting it busy for some
-// microseconds after the work is done, and every next call would then take
-// the launch path, and keep it so.
+// default stream, just wrote).  When the runtime reports both idle
+// (hipStreamQuery, 0.17 us for the two) the request is posted at once;
+// otherwise the host first waits for them (hipStreamSynchronize: the same
+// work the launched copy would wait for in stream order on the GPU), then
+// posts.  Launching the copy on the (blocking) library stream instead would
+// keep hipStreamQuery of that stream and of the null stream answering "not
+// ready" for 12 and 31 us after the kernel is done (tools/queue_lab.hip
+// "lag", profiles/r06_queue_lab.txt), so every next back-to-back call would
+// take the launch path too, at 24 us from Python instead of 5.5.  The
+// library stream is asked only when it may hold work nobody waited for
+// (state.h lib_stream_dirty).
 //
 // Lifetime.  The workgroup leaves by itself after kIdleUs without a request
 // (every wave reaches that exit: the first wave decides, the workgroup
@@ -174,7 +178,7 @@ struct Service {
     std::chrono::steady_clock::time_point last_use{};
     bool exit_hook = false;
     // shmemx_service_stats: calls served, launches, calls that found the
-    // legacy / the library stream busy (and launched their copy instead)
+    // legacy / the library stream busy (and waited for it first)
     unsigned long long served = 0, launches = 0, busy_null = 0, busy_lib = 0;
 } g_svc;
 
@@ -244,16 +248,17 @@ bool stream_idle(hipStream_t s) {
 
 bool service_copy(void *dst, void *dst2, const void *src, size_t bytes) {
     if (!enabled() || bytes == 0 || bytes > kServiceMaxBytes || !dst || !src) return false;
-    // ordered after the legacy stream and the library stream: only when both
-    // have no work left
+    // ordered after the legacy stream and the library stream: once both have
+    // no work left (the resident workgroup's own stream, non-blocking, is
+    // not part of the null stream's wait)
     if (!stream_idle(nullptr)) {
         ++g_svc.busy_null;
-        return false;
+        SHMX_HIP(hipStreamSynchronize(nullptr));
     }
     if (g_state.lib_stream_dirty || g_state.lib_stream_exported) {
         if (!stream_idle(g_state.stream)) {
             ++g_svc.busy_lib;
-            return false;
+            SHMX_HIP(hipStreamSynchronize(g_state.stream));
         }
         g_state.lib_stream_dirty = false;
     }

@@ -140,8 +140,9 @@ int gpu_numa_node(int device);   // NUMA node of a HIP device's PCI function, or
 // The resident service workgroup (service.hip): a small one-member blocking
 // call's copy (reduce-op.c:213-216) done by a workgroup that is already on
 // the GPU, polling a host-coherent mailbox, instead of a launch.  dst2: a
-// second destination or null.  false = not taken (the legacy or library
-// stream still has work, or $SHMEMX_SERVICE=0): the caller launches.
+// second destination or null.  Ordered after the legacy and the library
+// stream (waits for them on the host when they still have work).  false =
+// not taken ($SHMEMX_SERVICE=0, or no mailbox): the caller launches.
 constexpr size_t kServiceMaxBytes = size_t(32) << 10;
 bool service_copy(void *dst, void *dst2, const void *src, size_t bytes);
 void service_quiesce();   // the workgroup leaves now, if it is up

@@ -450,8 +450,8 @@ SERVICE_STATS = ("served", "launches", "null_stream_busy", "library_stream_busy"
 def service_stats(reset: bool = False) -> dict:
     """shmemx_service_stats: small one-member blocking calls the resident
     service workgroup served, its launches, and the calls that found the
-    legacy default stream / the library's stream busy and launched their copy
-    instead."""
+    legacy default stream / the library's stream busy and waited for it
+    first."""
     buf = (ctypes.c_ulonglong * len(SERVICE_STATS))()
     k = lib().shmemx_service_stats(buf, len(buf), 1 if reset else 0)
     return {name: buf[i] for i, name in enumerate(SERVICE_STATS[:max(0, k)])}

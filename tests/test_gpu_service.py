@@ -61,9 +61,12 @@ def test_service_copies_every_size_and_alignment(cuda, shm, oracle, t):
 
 def test_service_ordered_after_the_default_stream(cuda, shm):
     """A kernel on the legacy default stream still writing the source when
-    the blocking call starts: the call sees its bytes (the service only runs
-    when that stream is idle; here it finds it busy and the launched copy,
-    stream-ordered after it, runs instead)."""
+    the blocking call starts: the call sees its bytes (the service notices
+    the stream busy and the host waits for it before posting, as the launched
+    copy would wait for it in stream order), and the calls after it go
+    straight to the mailbox again: nothing the library did leaves a stream
+    looking busy (a launch on the blocking library stream would, for 12-31
+    us, and every next back-to-back call would then launch too)."""
     import torch
     shm.init()
     n = 512
@@ -77,20 +80,16 @@ def test_service_ordered_after_the_default_stream(cuda, shm):
         assert shm.last_error() == 0
         assert (dst.cpu().numpy() == rep + 1).all(), rep
     st = shm.service_stats(reset=True)
-    assert st["null_stream_busy"] >= 1, st
-    # and once the stream is idle the service takes the same call
-    torch.cuda.synchronize()
-    shm.to_all("double", "sum", dst, big, n, 0, 0, 1)
-    assert shm.service_stats(reset=True)["served"] == 1
-    # a call that launched its copy (the stream was busy) does not keep the
-    # next ones off the service: right after it the runtime may still call
-    # the library stream busy, but the library knows its work is done
+    assert st["null_stream_busy"] >= 1 and st["served"] == 5, st
     big.fill_(7.0)
+    t0 = time.perf_counter()
     for _ in range(200):
         shm.to_all("double", "sum", dst, big, n, 0, 0, 1)
+    dt = time.perf_counter() - t0
     st = shm.service_stats(reset=True)
-    assert st["served"] >= 195 and st["library_stream_busy"] == 0, st
+    assert st["served"] == 200 and st["null_stream_busy"] <= 2 and st["library_stream_busy"] == 0, st
     assert (dst.cpu().numpy() == 7.0).all()
+    assert dt < 0.02, dt   # 200 calls at mailbox speed (with the fill's wait)
 
 
 def test_service_comes_back_after_idling_out(cuda, shm, oracle):

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -51,9 +52,61 @@ static double now_us() {
         .count();
 }
 
+// mode "lag": after a one-workgroup kernel on a blocking stream has stored
+// its host word, how long do hipStreamQuery(that stream) and
+// hipStreamQuery(null) keep answering "not ready", and what does a
+// hipStreamSynchronize cost at that point?  (median of 500)
+static int lag_mode() {
+    unsigned long long *h = nullptr;
+    CK(hipHostMalloc(reinterpret_cast<void **>(&h), 4096, hipHostMallocCoherent));
+    std::memset(h, 0, 4096);
+    volatile unsigned long long *word = h;
+    hipStream_t b, nb;
+    CK(hipStreamCreate(&b));
+    CK(hipStreamCreateWithFlags(&nb, hipStreamNonBlocking));
+    for (hipStream_t s : {b, nb}) {
+        std::vector<double> q_own, q_null, t_sync;
+        for (int i = 0; i < 600; ++i) {
+            const unsigned long long v = (unsigned long long)i + 1 + (s == nb ? 100000 : 0);
+            hipLaunchKernelGGL(tiny, dim3(1), dim3(64), 0, s, h, v);
+            while (*word != v) {
+            }
+            const double t0 = now_us();
+            double own = -1, nul = -1;
+            while (own < 0 || nul < 0) {
+                const double t = now_us() - t0;
+                if (own < 0 && hipStreamQuery(s) == hipSuccess) own = t;
+                if (nul < 0 && hipStreamQuery(nullptr) == hipSuccess) nul = t;
+                if (t > 1e5) break;
+            }
+            // and a launch whose completion is waited for with a synchronize
+            hipLaunchKernelGGL(tiny, dim3(1), dim3(64), 0, s, h, v + 1000000);
+            while (*word != v + 1000000) {
+            }
+            const double t1 = now_us();
+            CK(hipStreamSynchronize(s));
+            if (i >= 100) {
+                q_own.push_back(own);
+                q_null.push_back(nul);
+                t_sync.push_back(now_us() - t1);
+            }
+        }
+        auto med = [](std::vector<double> v) {
+            std::sort(v.begin(), v.end());
+            return v[v.size() / 2];
+        };
+        std::printf("%s stream: after the host word, own query ready in %.2f us, null query in %.2f us; "
+                    "a synchronize then takes %.2f us (medians)\n",
+                    s == b ? "blocking" : "non-blocking", med(q_own), med(q_null), med(t_sync));
+    }
+    std::printf("ok\n");
+    return 0;
+}
+
 int main(int argc, char **argv) {
     std::setvbuf(stdout, nullptr, _IONBF, 0);
     const std::string mode = argc > 1 ? argv[1] : "plain";
+    if (mode == "lag") return lag_mode();
     CK(hipSetDevice(0));
     unsigned long long *h = nullptr;
     CK(hipHostMalloc(reinterpret_cast<void **>(&h), 4096, hipHostMallocCoherent));

@@ -189,7 +189,12 @@ int main(int argc, char **argv) {
     CK(hipMemset(src, 7, 1 << 20));
     hipStream_t blocking, svc;
     CK(hipStreamCreate(&blocking));
-    CK(hipStreamCreateWithFlags(&svc, hipStreamNonBlocking));
+    {
+        // the library's choice: a non-blocking stream of the greatest priority
+        int lo = 0, hi = 0;
+        CK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        CK(hipStreamCreateWithPriority(&svc, hipStreamNonBlocking, hi));
+    }
     Mailbox *mb = nullptr;
     CK(hipHostMalloc(reinterpret_cast<void **>(&mb), sizeof(Mailbox), hipHostMallocCoherent));
     std::memset(mb, 0, sizeof *mb);
@@ -324,6 +329,49 @@ int main(int argc, char **argv) {
         t.push_back(now_us() - t0);
     }
     report("line_cold", t);
+    // 5. gated posts: the host writes the descriptor and check word, and the
+    // sequence number is stored by the null stream itself
+    // (hipStreamWriteValue64), i.e. once everything enqueued on the legacy
+    // stream before it, and on the blocking streams it waits for, has
+    // completed; alone, and right after a kernel on a blocking stream (whose
+    // retiring keeps hipStreamQuery(null) "not ready" for ~30 us)
+    g_phase = "gated";
+    std::fprintf(stderr, "phase %s\n", g_phase);
+    auto post_gated = [&] {
+        mb->src = src;
+        mb->dst = dst;
+        mb->bytes = bytes;
+        ++seq;
+        mb->check = seq ^ reinterpret_cast<uintptr_t>(src) ^ reinterpret_cast<uintptr_t>(dst) ^ bytes ^ kMix;
+        CK(hipStreamWriteValue64(nullptr, &mb->seq, seq, 0));
+        const volatile unsigned long long *d = &mb->done;
+        const double t0 = now_us();
+        for (unsigned k = 1;; ++k) {
+            if (*d == seq) return;
+            __builtin_ia32_pause();
+            if ((k & 4095) == 0 && hipStreamQuery(svc) == hipSuccess && *d != seq) launch_service();
+            if ((k & 65535) == 0) watchdog(t0, "gated spin");
+        }
+    };
+    if (hipStreamQuery(svc) == hipSuccess) launch_service();
+    t.clear();
+    for (int i = 0; i < reps + 50; ++i) {
+        const double t0 = now_us();
+        post_gated();
+        if (i >= 50) t.push_back(now_us() - t0);
+    }
+    report("gated", t);
+    t.clear();
+    for (int i = 0; i < 500; ++i) {
+        const unsigned long long v = 7000000ull + i;
+        hipLaunchKernelGGL(copy_self, dim3(1), dim3(256), 0, blocking, static_cast<const unsigned char *>(src),
+                           static_cast<unsigned char *>(dst), (unsigned long long)bytes, word, v);
+        while (*vw != v) __builtin_ia32_pause();
+        const double t0 = now_us();
+        post_gated();
+        t.push_back(now_us() - t0);
+    }
+    report("gated_after", t);
     // correctness: dst holds src's bytes
     std::vector<unsigned char> h(bytes);
     g_phase = "check";
