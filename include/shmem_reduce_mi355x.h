@@ -342,8 +342,10 @@ int shmemx_rccl_register_heap(int on);
  * program's hipDeviceSynchronize waits that long at most) and at
  * shmem_finalize.  $SHMEMX_SERVICE=0 turns it off.  Stats: out[0] calls
  * served, out[1] launches of the workgroup, out[2] / out[3] calls that found
- * the legacy default stream / the library's stream busy and waited for it;
- * returns how many were written. */
+ * the legacy default stream / the library's stream busy and waited for it,
+ * out[4] / out[5] nanoseconds summed over the served calls from the check's
+ * start to the post / from the post to the result; returns how many were
+ * written. */
 int shmemx_service_stats(unsigned long long *out, int nout, int reset);
 
 int shmemx_kernel_timing(int on);

@@ -14,7 +14,7 @@
 // a check word catches a torn read), drops stale lines (system-scope
 // acquire), copies, writes back (system-scope release) and stores the
 // sequence number into a second host-coherent line the host spins on:
-// 2.3-2.4 us per round trip in the lab.
+// 2.2-3.8 us per round trip by the phase of the post (below).
 //
 // Ordering.  A blocking call is ordered after the legacy default stream and
 // the library's stream (the buffers a plain HIP program, or PyTorch's
@@ -73,35 +73,54 @@ struct alignas(64) Mailbox {
 };
 static_assert(sizeof(Mailbox) == 128, "two lines");
 
-// Every lane issues its loads of a step (U words, kSvcBlock apart) before
-// its first store, so a 32 KiB copy of 16-byte words is one round of loads
-// in flight, not eight one after another.
+// Global-memory views of the operands (their addresses arrive through LDS,
+// which would leave generic flat accesses otherwise).
+template <typename V>
+using gptr = __attribute__((address_space(1))) V *;
+
+// One pass: lane t moves words t, t + 256, ... (a 32 KiB copy of 16-byte
+// words is 8 per lane).  Every lane issues all its loads before its first
+// store: within a pass of 64 words its wave needs, the loads are
+// unconditional (an index past the end reads the last word again), only the
+// stores are masked, so no load waits for another.
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
 template <typename V>
 __device__ __forceinline__ void copy_as(const unsigned char *src, unsigned char *dst, unsigned char *dst2,
                                         unsigned long long bytes) {
     constexpr int U = 8;
-    const V *s = reinterpret_cast<const V *>(src);
-    V *d = reinterpret_cast<V *>(dst);
-    V *d2 = reinterpret_cast<V *>(dst2);
+    const gptr<const V> s = (gptr<const V>)(src);
+    const gptr<V> d = (gptr<V>)(dst);
+    const gptr<V> d2 = (gptr<V>)(dst2);
     const unsigned long long n = bytes / sizeof(V);
+    // (in a scalar register: the test below is a scalar branch)
+    const unsigned long long wave_first = (unsigned)__builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
     for (unsigned long long base = 0; base < n; base += (unsigned long long)U * kSvcBlock) {
         V v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const unsigned long long i = base + threadIdx.x + (unsigned long long)u * kSvcBlock;
-            if (i < n) v[u] = s[i];
+            if (base + wave_first + (unsigned long long)u * kSvcBlock < n) {
+                const unsigned long long i = base + threadIdx.x + (unsigned long long)u * kSvcBlock;
+                v[u] = s[i < n ? i : n - 1];
+            }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const unsigned long long i = base + threadIdx.x + (unsigned long long)u * kSvcBlock;
             if (i < n) {
                 d[i] = v[u];
-                if (d2) d2[i] = v[u];
+                if (dst2) d2[i] = v[u];
             }
         }
     }
 }
 
+// Wave 0 has one read of the mailbox in flight at a time: a read of host
+// memory takes ~1.2 us, so a request waits for the first read that leaves
+// after it was posted (0 to 1.2 us by the phase of the post; tools/kernel_ab.hip
+// gap sweep, profiles/r06_service_lab.txt).  More reads in flight would hold
+// up the copy's loads and stores behind them: the CU's vector memory path
+// returns in order (measured: 7.3 us per 16-byte request with six in flight).
 __global__ __launch_bounds__(kSvcBlock) void service_kernel(Mailbox *mb, unsigned long long served,
                                                          unsigned long long idle_ticks) {
     __shared__ unsigned long long s_seq, s_bytes;
@@ -154,7 +173,7 @@ __global__ __launch_bounds__(kSvcBlock) void service_kernel(Mailbox *mb, unsigne
         const unsigned long long n = s_bytes;
         const uintptr_t al = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) |
                              reinterpret_cast<uintptr_t>(dst2) | n;
-        if ((al & 15) == 0) copy_as<uint4>(src, dst, dst2, n);
+        if ((al & 15) == 0) copy_as<v4u>(src, dst, dst2, n);
         else if ((al & 7) == 0) copy_as<unsigned long long>(src, dst, dst2, n);
         else if ((al & 3) == 0) copy_as<unsigned>(src, dst, dst2, n);
         else if ((al & 1) == 0) copy_as<unsigned short>(src, dst, dst2, n);
@@ -180,6 +199,9 @@ struct Service {
     // shmemx_service_stats: calls served, launches, calls that found the
     // legacy / the library stream busy (and waited for it first)
     unsigned long long served = 0, launches = 0, busy_null = 0, busy_lib = 0;
+    // nanoseconds summed over the served calls: from entering service_copy
+    // to the post, and from the post to seeing the result done
+    unsigned long long ns_before_post = 0, ns_round_trip = 0;
 } g_svc;
 
 bool enabled() {
@@ -278,6 +300,7 @@ bool service_copy(void *dst, void *dst2, const void *src, size_t bytes) {
     mb->check = q ^ reinterpret_cast<uintptr_t>(src) ^ reinterpret_cast<uintptr_t>(dst) ^
                 reinterpret_cast<uintptr_t>(dst2) ^ (unsigned long long)bytes ^ kMix;
     __atomic_store_n(&mb->seq, q, __ATOMIC_RELEASE);
+    const auto t_post = std::chrono::steady_clock::now();
     const volatile unsigned long long *done = &mb->done;
     for (unsigned k = 1; *done != q; ++k) {
         __builtin_ia32_pause();
@@ -290,6 +313,9 @@ bool service_copy(void *dst, void *dst2, const void *src, size_t bytes) {
     }
     g_svc.last_use = std::chrono::steady_clock::now();
     ++g_svc.served;
+    g_svc.ns_before_post += (unsigned long long)std::chrono::duration_cast<std::chrono::nanoseconds>(t_post - t_begin).count();
+    g_svc.ns_round_trip +=
+        (unsigned long long)std::chrono::duration_cast<std::chrono::nanoseconds>(g_svc.last_use - t_post).count();
     return true;
 }
 
@@ -321,10 +347,11 @@ void device_sync() {
 extern "C" int shmemx_service_stats(unsigned long long *out, int nout, int reset) {
     std::lock_guard<std::recursive_mutex> lk(shmx::g_mu);
     if (!out || nout < 0) return shmx::set_error(SHMEMX_EINVAL), -1;
-    const unsigned long long all[4] = {shmx::g_svc.served, shmx::g_svc.launches, shmx::g_svc.busy_null,
-                                       shmx::g_svc.busy_lib};
-    const int k = nout < 4 ? nout : 4;
+    shmx::Service &v = shmx::g_svc;
+    const unsigned long long all[6] = {v.served, v.launches, v.busy_null, v.busy_lib, v.ns_before_post,
+                                       v.ns_round_trip};
+    const int k = nout < 6 ? nout : 6;
     for (int i = 0; i < k; ++i) out[i] = all[i];
-    if (reset) shmx::g_svc.served = shmx::g_svc.launches = shmx::g_svc.busy_null = shmx::g_svc.busy_lib = 0;
+    if (reset) v.served = v.launches = v.busy_null = v.busy_lib = v.ns_before_post = v.ns_round_trip = 0;
     return k;
 }

@@ -444,7 +444,8 @@ def direct_stats(reset: bool = True) -> dict:
     return out
 
 
-SERVICE_STATS = ("served", "launches", "null_stream_busy", "library_stream_busy")
+SERVICE_STATS = ("served", "launches", "null_stream_busy", "library_stream_busy", "ns_before_post",
+                 "ns_round_trip")
 
 
 def service_stats(reset: bool = False) -> dict:
