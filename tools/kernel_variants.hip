@@ -1,0 +1,788 @@
+// Lab: variants of the service kernel against the lab's line-read kernel,
+// same host code (what the library kernel's extra 0.4 us is):
+//   A  the library's kernel (csrc/service.hip, extracted when this file was made)
+//   B  A with 1024 threads (earlier: each lane's loads all issued before
+//      its stores, unconditional and clamped: 2.89 vs 2.63 us at 8 KiB)
+//   C  the kernel before that with the lab's plain copy loops
+//      (an earlier B, reading six words instead of seven, tied with it)
+//   D  four polling waves reading the mailbox line with scalar loads in
+//      staggered time slots, twelve copy waves handed the request through LDS
+//   G  D with the claiming poller dropping stale lines itself (no second
+//      hand-over between copy waves); (E, eight polling waves in slots of
+//      0.17 us, was no better than D)
+//   lab  tools/service_lab.hip's line-read kernel
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+namespace A {
+constexpr unsigned long long kMix = 0x9E3779B97F4A7C15ull;
+constexpr unsigned kIdleUs = 200;
+constexpr int kSvcBlock = 256;
+
+// Written by the host: the first line (seq last, with release); by the
+// device: the second.
+struct alignas(64) Mailbox {
+    unsigned long long seq;
+    unsigned long long quit;
+    const void *src;
+    void *dst;
+    void *dst2;   // a second destination (the mirrored heap's view), or null
+    unsigned long long bytes;
+    unsigned long long check;   // seq ^ src ^ dst ^ dst2 ^ bytes ^ kMix
+    unsigned long long pad;
+    alignas(64) unsigned long long done;
+};
+static_assert(sizeof(Mailbox) == 128, "two lines");
+
+// Global-memory views of the operands (their addresses arrive through LDS,
+// which would leave generic flat accesses otherwise).
+template <typename V>
+using gptr = __attribute__((address_space(1))) V *;
+
+// Lane t moves words t, t + 256, ... of the widest word the operands'
+// alignment allows.  (A version that issued all of a lane's loads before its
+// first store, unconditional and clamped, was slower: 2.72 against 2.35 us
+// per 16-byte request, 3.70 against 3.56 at 32 KiB; tools/kernel_variants.hip.)
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+template <typename V>
+__device__ __forceinline__ void copy_as(const unsigned char *src, unsigned char *dst, unsigned char *dst2,
+                                        unsigned long long bytes) {
+    const gptr<const V> s = (gptr<const V>)(src);
+    const gptr<V> d = (gptr<V>)(dst);
+    const gptr<V> d2 = (gptr<V>)(dst2);
+    const unsigned long long n = bytes / sizeof(V);
+    for (unsigned long long i = threadIdx.x; i < n; i += kSvcBlock) {
+        const V x = s[i];
+        d[i] = x;
+        if (dst2) d2[i] = x;
+    }
+}
+
+// Wave 0 has one read of the mailbox in flight at a time: a read of host
+// memory takes ~1.2 us, so a request waits for the first read that leaves
+// after it was posted (0 to 1.2 us by the phase of the post; tools/kernel_ab.hip
+// gap sweep, profiles/r06_service_lab.txt).  More reads in flight would hold
+// up the copy's loads and stores behind them: the CU's vector memory path
+// returns in order (measured: 7.3 us per 16-byte request with six in flight).
+__global__ __launch_bounds__(kSvcBlock) void service_kernel(Mailbox *mb, unsigned long long served,
+                                                         unsigned long long idle_ticks) {
+    __shared__ unsigned long long s_seq, s_bytes;
+    __shared__ const unsigned char *s_src;
+    __shared__ unsigned char *s_dst, *s_dst2;
+    unsigned long long last = served;
+    unsigned long long t_last = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        if (threadIdx.x < 64) {
+            // wave 0: lanes 0-6 read the mailbox's first line in one load
+            // instruction, every lane takes the words from them
+            const unsigned long long *line = reinterpret_cast<const unsigned long long *>(mb);
+            const int lane = threadIdx.x;
+            unsigned long long q = 0;
+            for (;;) {
+                const unsigned long long v =
+                    lane < 7 ? __hip_atomic_load(line + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0;
+                q = __shfl(v, 0);
+                const unsigned long long quit = __shfl(v, 1);
+                if (q != last) {
+                    const unsigned long long a = __shfl(v, 2), b = __shfl(v, 3), b2 = __shfl(v, 4),
+                                             n = __shfl(v, 5), c = __shfl(v, 6);
+                    if ((q ^ a ^ b ^ b2 ^ n ^ kMix) == c) {
+                        if (lane == 0) {
+                            // lines of the source another kernel wrote since
+                            // this one started are dropped (system scope)
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                            s_src = reinterpret_cast<const unsigned char *>(a);
+                            s_dst = reinterpret_cast<unsigned char *>(b);
+                            s_dst2 = reinterpret_cast<unsigned char *>(b2);
+                            s_bytes = n;
+                        }
+                        break;
+                    }
+                    continue;   // torn read: the line again
+                }
+                if (quit || __builtin_amdgcn_s_memrealtime() - t_last > idle_ticks) {
+                    q = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (lane == 0) s_seq = q;
+        }
+        __syncthreads();
+        const unsigned long long q = s_seq;
+        if (!q) return;   // idle or told to quit: every wave leaves here
+        const unsigned char *src = s_src;
+        unsigned char *dst = s_dst, *dst2 = s_dst2;
+        const unsigned long long n = s_bytes;
+        const uintptr_t al = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) |
+                             reinterpret_cast<uintptr_t>(dst2) | n;
+        if ((al & 15) == 0) copy_as<v4u>(src, dst, dst2, n);
+        else if ((al & 7) == 0) copy_as<unsigned long long>(src, dst, dst2, n);
+        else if ((al & 3) == 0) copy_as<unsigned>(src, dst, dst2, n);
+        else if ((al & 1) == 0) copy_as<unsigned short>(src, dst, dst2, n);
+        else copy_as<unsigned char>(src, dst, dst2, n);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's stores issued and done
+        __syncthreads();
+        if (threadIdx.x == 0)   // write back, then tell the host
+            __hip_atomic_store(&mb->done, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        last = q;
+        t_last = __builtin_amdgcn_s_memrealtime();
+        __syncthreads();   // the s_* words are read before wave 0 polls again
+    }
+}
+
+}
+namespace B {
+constexpr unsigned long long kMix = 0x9E3779B97F4A7C15ull;
+constexpr unsigned kIdleUs = 200;
+constexpr int kSvcBlock = 1024;
+
+// Written by the host: the first line (seq last, with release); by the
+// device: the second.
+struct alignas(64) Mailbox {
+    unsigned long long seq;
+    unsigned long long quit;
+    const void *src;
+    void *dst;
+    void *dst2;   // a second destination (the mirrored heap's view), or null
+    unsigned long long bytes;
+    unsigned long long check;   // seq ^ src ^ dst ^ dst2 ^ bytes ^ kMix
+    unsigned long long pad;
+    alignas(64) unsigned long long done;
+};
+static_assert(sizeof(Mailbox) == 128, "two lines");
+
+// Global-memory views of the operands (their addresses arrive through LDS,
+// which would leave generic flat accesses otherwise).
+template <typename V>
+using gptr = __attribute__((address_space(1))) V *;
+
+// Lane t moves words t, t + 256, ... of the widest word the operands'
+// alignment allows.  (A version that issued all of a lane's loads before its
+// first store, unconditional and clamped, was slower: 2.72 against 2.35 us
+// per 16-byte request, 3.70 against 3.56 at 32 KiB; tools/kernel_variants.hip.)
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+template <typename V>
+__device__ __forceinline__ void copy_as(const unsigned char *src, unsigned char *dst, unsigned char *dst2,
+                                        unsigned long long bytes) {
+    const gptr<const V> s = (gptr<const V>)(src);
+    const gptr<V> d = (gptr<V>)(dst);
+    const gptr<V> d2 = (gptr<V>)(dst2);
+    const unsigned long long n = bytes / sizeof(V);
+    for (unsigned long long i = threadIdx.x; i < n; i += kSvcBlock) {
+        const V x = s[i];
+        d[i] = x;
+        if (dst2) d2[i] = x;
+    }
+}
+
+// Wave 0 has one read of the mailbox in flight at a time: a read of host
+// memory takes ~1.2 us, so a request waits for the first read that leaves
+// after it was posted (0 to 1.2 us by the phase of the post; tools/kernel_ab.hip
+// gap sweep, profiles/r06_service_lab.txt).  More reads in flight would hold
+// up the copy's loads and stores behind them: the CU's vector memory path
+// returns in order (measured: 7.3 us per 16-byte request with six in flight).
+__global__ __launch_bounds__(kSvcBlock) void service_kernel(Mailbox *mb, unsigned long long served,
+                                                         unsigned long long idle_ticks) {
+    __shared__ unsigned long long s_seq, s_bytes;
+    __shared__ const unsigned char *s_src;
+    __shared__ unsigned char *s_dst, *s_dst2;
+    unsigned long long last = served;
+    unsigned long long t_last = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        if (threadIdx.x < 64) {
+            // wave 0: lanes 0-6 read the mailbox's first line in one load
+            // instruction, every lane takes the words from them
+            const unsigned long long *line = reinterpret_cast<const unsigned long long *>(mb);
+            const int lane = threadIdx.x;
+            unsigned long long q = 0;
+            for (;;) {
+                const unsigned long long v =
+                    lane < 7 ? __hip_atomic_load(line + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0;
+                q = __shfl(v, 0);
+                const unsigned long long quit = __shfl(v, 1);
+                if (q != last) {
+                    const unsigned long long a = __shfl(v, 2), b = __shfl(v, 3), b2 = __shfl(v, 4),
+                                             n = __shfl(v, 5), c = __shfl(v, 6);
+                    if ((q ^ a ^ b ^ b2 ^ n ^ kMix) == c) {
+                        if (lane == 0) {
+                            // lines of the source another kernel wrote since
+                            // this one started are dropped (system scope)
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                            s_src = reinterpret_cast<const unsigned char *>(a);
+                            s_dst = reinterpret_cast<unsigned char *>(b);
+                            s_dst2 = reinterpret_cast<unsigned char *>(b2);
+                            s_bytes = n;
+                        }
+                        break;
+                    }
+                    continue;   // torn read: the line again
+                }
+                if (quit || __builtin_amdgcn_s_memrealtime() - t_last > idle_ticks) {
+                    q = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (lane == 0) s_seq = q;
+        }
+        __syncthreads();
+        const unsigned long long q = s_seq;
+        if (!q) return;   // idle or told to quit: every wave leaves here
+        const unsigned char *src = s_src;
+        unsigned char *dst = s_dst, *dst2 = s_dst2;
+        const unsigned long long n = s_bytes;
+        const uintptr_t al = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) |
+                             reinterpret_cast<uintptr_t>(dst2) | n;
+        if ((al & 15) == 0) copy_as<v4u>(src, dst, dst2, n);
+        else if ((al & 7) == 0) copy_as<unsigned long long>(src, dst, dst2, n);
+        else if ((al & 3) == 0) copy_as<unsigned>(src, dst, dst2, n);
+        else if ((al & 1) == 0) copy_as<unsigned short>(src, dst, dst2, n);
+        else copy_as<unsigned char>(src, dst, dst2, n);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's stores issued and done
+        __syncthreads();
+        if (threadIdx.x == 0)   // write back, then tell the host
+            __hip_atomic_store(&mb->done, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        last = q;
+        t_last = __builtin_amdgcn_s_memrealtime();
+        __syncthreads();   // the s_* words are read before wave 0 polls again
+    }
+}
+
+}
+namespace C {
+constexpr unsigned long long kMix = 0x9E3779B97F4A7C15ull;
+constexpr unsigned kIdleUs = 200;
+constexpr int kSvcBlock = 256;
+
+// Written by the host: the first line (seq last, with release); by the
+// device: the second.
+struct alignas(64) Mailbox {
+    unsigned long long seq;
+    unsigned long long quit;
+    const void *src;
+    void *dst;
+    void *dst2;   // a second destination (the mirrored heap's view), or null
+    unsigned long long bytes;
+    unsigned long long check;   // seq ^ src ^ dst ^ dst2 ^ bytes ^ kMix
+    unsigned long long pad;
+    alignas(64) unsigned long long done;
+};
+static_assert(sizeof(Mailbox) == 128, "two lines");
+
+// Global-memory views of the operands (their addresses arrive through LDS,
+// which would leave generic flat accesses otherwise).
+template <typename V>
+using gptr = __attribute__((address_space(1))) V *;
+
+// One pass: lane t moves words t, t + 256, ... (a 32 KiB copy of 16-byte
+// words is 8 per lane).  Every lane issues all its loads before its first
+// store: within a pass of 64 words its wave needs, the loads are
+// unconditional (an index past the end reads the last word again), only the
+// stores are masked, so no load waits for another.
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+template <typename V>
+__device__ __forceinline__ void copy_as(const unsigned char *src, unsigned char *dst, unsigned char *dst2,
+                                        unsigned long long bytes) {
+    constexpr int U = 8;
+    const gptr<const V> s = (gptr<const V>)(src);
+    const gptr<V> d = (gptr<V>)(dst);
+    const gptr<V> d2 = (gptr<V>)(dst2);
+    const unsigned long long n = bytes / sizeof(V);
+    // (in a scalar register: the test below is a scalar branch)
+    const unsigned long long wave_first = (unsigned)__builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
+    for (unsigned long long base = 0; base < n; base += (unsigned long long)U * kSvcBlock) {
+        V v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (base + wave_first + (unsigned long long)u * kSvcBlock < n) {
+                const unsigned long long i = base + threadIdx.x + (unsigned long long)u * kSvcBlock;
+                v[u] = s[i < n ? i : n - 1];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const unsigned long long i = base + threadIdx.x + (unsigned long long)u * kSvcBlock;
+            if (i < n) {
+                d[i] = v[u];
+                if (dst2) d2[i] = v[u];
+            }
+        }
+    }
+}
+
+// Wave 0 has one read of the mailbox in flight at a time: a read of host
+// memory takes ~1.2 us, so a request waits for the first read that leaves
+// after it was posted (0 to 1.2 us by the phase of the post; tools/kernel_ab.hip
+// gap sweep, profiles/r06_service_lab.txt).  More reads in flight would hold
+// up the copy's loads and stores behind them: the CU's vector memory path
+// returns in order (measured: 7.3 us per 16-byte request with six in flight).
+__global__ __launch_bounds__(kSvcBlock) void service_kernel(Mailbox *mb, unsigned long long served,
+                                                         unsigned long long idle_ticks) {
+    __shared__ unsigned long long s_seq, s_bytes;
+    __shared__ const unsigned char *s_src;
+    __shared__ unsigned char *s_dst, *s_dst2;
+    unsigned long long last = served;
+    unsigned long long t_last = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        if (threadIdx.x < 64) {
+            // wave 0: lanes 0-6 read the mailbox's first line in one load
+            // instruction, every lane takes the words from them
+            const unsigned long long *line = reinterpret_cast<const unsigned long long *>(mb);
+            const int lane = threadIdx.x;
+            unsigned long long q = 0;
+            for (;;) {
+                const unsigned long long v =
+                    lane < 7 ? __hip_atomic_load(line + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0;
+                q = __shfl(v, 0);
+                const unsigned long long quit = __shfl(v, 1);
+                if (q != last) {
+                    const unsigned long long a = __shfl(v, 2), b = __shfl(v, 3), b2 = __shfl(v, 4),
+                                             n = __shfl(v, 5), c = __shfl(v, 6);
+                    if ((q ^ a ^ b ^ b2 ^ n ^ kMix) == c) {
+                        if (lane == 0) {
+                            // lines of the source another kernel wrote since
+                            // this one started are dropped (system scope)
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                            s_src = reinterpret_cast<const unsigned char *>(a);
+                            s_dst = reinterpret_cast<unsigned char *>(b);
+                            s_dst2 = reinterpret_cast<unsigned char *>(b2);
+                            s_bytes = n;
+                        }
+                        break;
+                    }
+                    continue;   // torn read: the line again
+                }
+                if (quit || __builtin_amdgcn_s_memrealtime() - t_last > idle_ticks) {
+                    q = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (lane == 0) s_seq = q;
+        }
+        __syncthreads();
+        const unsigned long long q = s_seq;
+        if (!q) return;   // idle or told to quit: every wave leaves here
+        const unsigned char *src = s_src;
+        unsigned char *dst = s_dst, *dst2 = s_dst2;
+        const unsigned long long n = s_bytes;
+        if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) | n) & 15) == 0) {
+            for (unsigned long long i = threadIdx.x; i < n / 16; i += 256)
+                reinterpret_cast<uint4 *>(dst)[i] = reinterpret_cast<const uint4 *>(src)[i];
+        } else {
+            for (unsigned long long i = threadIdx.x; i < n; i += 256) dst[i] = src[i];
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's stores issued and done
+        __syncthreads();
+        if (threadIdx.x == 0)   // write back, then tell the host
+            __hip_atomic_store(&mb->done, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        last = q;
+        t_last = __builtin_amdgcn_s_memrealtime();
+        __syncthreads();   // the s_* words are read before wave 0 polls again
+    }
+}
+
+}
+namespace D {
+constexpr unsigned long long kMix = 0x9E3779B97F4A7C15ull;
+constexpr int kSvcBlock = 1024;
+constexpr int kPollWaves = 4;
+constexpr int kCopyThreads = kSvcBlock - 64 * kPollWaves;
+constexpr unsigned long long kSlot = 33;   // s_memrealtime ticks: poller w reads in slots w, w + 4, ...
+constexpr unsigned long long kExit = ~0ull;
+struct alignas(64) Mailbox {
+    unsigned long long seq, quit;
+    const void *src;
+    void *dst, *dst2;
+    unsigned long long bytes, check, pad;
+    alignas(64) unsigned long long done;
+};
+typedef unsigned int u16v __attribute__((ext_vector_type(16)));
+template <typename V>
+using gptr = __attribute__((address_space(1))) V *;
+__device__ __forceinline__ unsigned long long w64(const u16v &v, int k) {
+    return (unsigned long long)v[2 * k + 1] << 32 | v[2 * k];
+}
+__device__ __forceinline__ unsigned long long lds_load(const unsigned long long *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_store(unsigned long long *p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__global__ __launch_bounds__(kSvcBlock) void service_kernel(Mailbox *mb, unsigned long long served,
+                                                         unsigned long long idle_ticks) {
+    __shared__ unsigned long long s_claim, s_req, s_go, s_done, s_count, s_leave, s_bytes;
+    __shared__ const unsigned char *s_src;
+    __shared__ unsigned char *s_dst, *s_dst2;
+    if (threadIdx.x == 0) {
+        s_claim = s_req = s_go = s_done = served;
+        s_count = 0;
+        s_leave = 0;
+    }
+    __syncthreads();
+    const int wave = threadIdx.x >> 6;
+    if (wave < kPollWaves) {
+        unsigned long long last = served;
+        unsigned long long t_last = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            // this wave's slot
+            while (((__builtin_amdgcn_s_memrealtime() / kSlot) & (kPollWaves - 1)) != (unsigned)wave)
+                __builtin_amdgcn_s_sleep(1);
+            u16v v;
+            asm volatile("s_load_dwordx16 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(mb) : "memory");
+            const unsigned long long q = w64(v, 0);
+            if (q != last) {
+                const unsigned long long a = w64(v, 2), b = w64(v, 3), b2 = w64(v, 4), n = w64(v, 5), c = w64(v, 6);
+                if ((q ^ a ^ b ^ b2 ^ n ^ kMix) == c) {
+                    last = q;
+                    t_last = __builtin_amdgcn_s_memrealtime();
+                    // the first poller to see it hands it over
+                    unsigned long long expect = lds_load(&s_claim);
+                    if (expect != q && threadIdx.x % 64 == 0 &&
+                        __hip_atomic_compare_exchange_strong(&s_claim, &expect, q, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                        s_src = reinterpret_cast<const unsigned char *>(a);
+                        s_dst = reinterpret_cast<unsigned char *>(b);
+                        s_dst2 = reinterpret_cast<unsigned char *>(b2);
+                        s_bytes = n;
+                        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                        lds_store(&s_req, q);
+                    }
+                    continue;
+                }
+            }
+            if (lds_load(&s_leave)) break;
+            if (wave == 0 && (w64(v, 1) || (__builtin_amdgcn_s_memrealtime() - t_last > idle_ticks &&
+                                             lds_load(&s_claim) == lds_load(&s_done)))) {
+                lds_store(&s_leave, 1);
+                break;
+            }
+            // another poller took a newer request: catch up
+            const unsigned long long cl = lds_load(&s_claim);
+            if (cl != last && cl != served) { last = cl; t_last = __builtin_amdgcn_s_memrealtime(); }
+        }
+        if (wave == 0) {
+            while (lds_load(&s_done) != lds_load(&s_claim)) __builtin_amdgcn_s_sleep(1);
+            lds_store(&s_req, kExit);
+        }
+        return;
+    }
+    const int t = threadIdx.x - 64 * kPollWaves;
+    unsigned long long seen = served;
+    for (;;) {
+        unsigned long long q;
+        if (wave == kPollWaves) {
+            while ((q = lds_load(&s_req)) == seen) __builtin_amdgcn_s_sleep(1);
+            if (q != kExit) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // drop stale lines (system scope)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            lds_store(&s_go, q);
+        } else {
+            while ((q = lds_load(&s_go)) == seen) __builtin_amdgcn_s_sleep(1);
+        }
+        if (q == kExit) return;
+        seen = q;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const unsigned char *src = s_src;
+        unsigned char *dst = s_dst, *dst2 = s_dst2;
+        const unsigned long long n = s_bytes;
+        if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(dst2) | n) & 15) == 0) {
+            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+            const gptr<const v4u> s = (gptr<const v4u>)src;
+            const gptr<v4u> d = (gptr<v4u>)dst;
+            for (unsigned long long i = t; i < n / 16; i += kCopyThreads) d[i] = s[i];
+        } else {
+            for (unsigned long long i = t; i < n; i += kCopyThreads) dst[i] = src[i];
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (threadIdx.x % 64 == 0) {
+            const unsigned long long arrived =
+                __hip_atomic_fetch_add(&s_count, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (arrived == kCopyThreads / 64 - 1) {
+                lds_store(&s_count, 0);
+                __hip_atomic_store(&mb->done, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                lds_store(&s_done, q);
+            }
+        }
+    }
+}
+}
+
+namespace G {
+constexpr unsigned long long kMix = 0x9E3779B97F4A7C15ull;
+constexpr int kSvcBlock = 1024;
+constexpr int kPollWaves = 4;
+constexpr int kCopyThreads = kSvcBlock - 64 * kPollWaves;
+constexpr unsigned long long kSlot = 33;   // s_memrealtime ticks: poller w reads in slots w, w + 4, ...
+constexpr unsigned long long kExit = ~0ull;
+struct alignas(64) Mailbox {
+    unsigned long long seq, quit;
+    const void *src;
+    void *dst, *dst2;
+    unsigned long long bytes, check, pad;
+    alignas(64) unsigned long long done;
+};
+typedef unsigned int u16v __attribute__((ext_vector_type(16)));
+template <typename V>
+using gptr = __attribute__((address_space(1))) V *;
+__device__ __forceinline__ unsigned long long w64(const u16v &v, int k) {
+    return (unsigned long long)v[2 * k + 1] << 32 | v[2 * k];
+}
+__device__ __forceinline__ unsigned long long lds_load(const unsigned long long *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_store(unsigned long long *p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__global__ __launch_bounds__(kSvcBlock) void service_kernel(Mailbox *mb, unsigned long long served,
+                                                         unsigned long long idle_ticks) {
+    __shared__ unsigned long long s_claim, s_req, s_go, s_done, s_count, s_leave, s_bytes;
+    __shared__ const unsigned char *s_src;
+    __shared__ unsigned char *s_dst, *s_dst2;
+    if (threadIdx.x == 0) {
+        s_claim = s_req = s_go = s_done = served;
+        s_count = 0;
+        s_leave = 0;
+    }
+    __syncthreads();
+    const int wave = threadIdx.x >> 6;
+    if (wave < kPollWaves) {
+        unsigned long long last = served;
+        unsigned long long t_last = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            // this wave's slot
+            while (((__builtin_amdgcn_s_memrealtime() / kSlot) & (kPollWaves - 1)) != (unsigned)wave)
+                __builtin_amdgcn_s_sleep(1);
+            u16v v;
+            asm volatile("s_load_dwordx16 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(mb) : "memory");
+            const unsigned long long q = w64(v, 0);
+            if (q != last) {
+                const unsigned long long a = w64(v, 2), b = w64(v, 3), b2 = w64(v, 4), n = w64(v, 5), c = w64(v, 6);
+                if ((q ^ a ^ b ^ b2 ^ n ^ kMix) == c) {
+                    last = q;
+                    t_last = __builtin_amdgcn_s_memrealtime();
+                    // the first poller to see it hands it over
+                    unsigned long long expect = lds_load(&s_claim);
+                    if (expect != q && threadIdx.x % 64 == 0 &&
+                        __hip_atomic_compare_exchange_strong(&s_claim, &expect, q, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                        s_src = reinterpret_cast<const unsigned char *>(a);
+                        s_dst = reinterpret_cast<unsigned char *>(b);
+                        s_dst2 = reinterpret_cast<unsigned char *>(b2);
+                        s_bytes = n;
+                        // drop stale lines here (no vector access of this
+                        // wave is in flight), for the copy waves of this CU
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                        lds_store(&s_req, q);
+                    }
+                    continue;
+                }
+            }
+            if (lds_load(&s_leave)) break;
+            if (wave == 0 && (w64(v, 1) || (__builtin_amdgcn_s_memrealtime() - t_last > idle_ticks &&
+                                             lds_load(&s_claim) == lds_load(&s_done)))) {
+                lds_store(&s_leave, 1);
+                break;
+            }
+            // another poller took a newer request: catch up
+            const unsigned long long cl = lds_load(&s_claim);
+            if (cl != last && cl != served) { last = cl; t_last = __builtin_amdgcn_s_memrealtime(); }
+        }
+        if (wave == 0) {
+            while (lds_load(&s_done) != lds_load(&s_claim)) __builtin_amdgcn_s_sleep(1);
+            lds_store(&s_req, kExit);
+        }
+        return;
+    }
+    const int t = threadIdx.x - 64 * kPollWaves;
+    unsigned long long seen = served;
+    for (;;) {
+        unsigned long long q;
+        while ((q = lds_load(&s_req)) == seen) __builtin_amdgcn_s_sleep(1);
+        if (q == kExit) return;
+        seen = q;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const unsigned char *src = s_src;
+        unsigned char *dst = s_dst, *dst2 = s_dst2;
+        const unsigned long long n = s_bytes;
+        if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(dst2) | n) & 15) == 0) {
+            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+            const gptr<const v4u> s = (gptr<const v4u>)src;
+            const gptr<v4u> d = (gptr<v4u>)dst;
+            for (unsigned long long i = t; i < n / 16; i += kCopyThreads) d[i] = s[i];
+        } else {
+            for (unsigned long long i = t; i < n; i += kCopyThreads) dst[i] = src[i];
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (threadIdx.x % 64 == 0) {
+            const unsigned long long arrived =
+                __hip_atomic_fetch_add(&s_count, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (arrived == kCopyThreads / 64 - 1) {
+                lds_store(&s_count, 0);
+                __hip_atomic_store(&mb->done, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+                lds_store(&s_done, q);
+            }
+        }
+    }
+}
+}
+
+
+struct alignas(64) LabMailbox {
+    // one 64-byte line the device reads; the host writes the fields and
+    // check first, seq last (release)
+    unsigned long long seq;
+    unsigned long long quit;
+    const void *src;
+    void *dst;
+    unsigned long long bytes;
+    unsigned long long check;   // seq ^ src ^ dst ^ bytes ^ kLabMix: a torn read shows
+    unsigned long long pad[2];
+    // the device's line
+    alignas(64) unsigned long long done;   // (system-scope release)
+    unsigned long long polls;   // heartbeat: polls so far (every 1024th)
+};
+constexpr unsigned long long kLabMix = 0x9E3779B97F4A7C15ull;
+
+// LINE: wave 0's lanes 0-5 read the mailbox's first line with one load
+// instruction (the descriptor arrives with the sequence number, no second
+// round trip over PCIe); the check word catches a torn read
+template <bool LINE>
+__global__ __launch_bounds__(256) void service_kernel(LabMailbox *mb, unsigned long long served,
+                                                      unsigned long long idle_ticks) {
+    __shared__ unsigned long long s_seq;
+    __shared__ const unsigned char *s_src;
+    __shared__ unsigned char *s_dst;
+    __shared__ unsigned long long s_bytes;
+    unsigned long long last = served, npoll = 0;
+    unsigned long long t_last = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        if (LINE && threadIdx.x < 64) {
+            const unsigned long long *line = reinterpret_cast<const unsigned long long *>(mb);
+            const int lane = threadIdx.x;
+            unsigned long long q = 0;
+            for (;;) {
+                const unsigned long long v =
+                    lane < 6 ? __hip_atomic_load(line + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0;
+                q = __shfl(v, 0);
+                const unsigned long long quit = __shfl(v, 1);
+                if (q != last) {
+                    const unsigned long long a = __shfl(v, 2), b = __shfl(v, 3), n = __shfl(v, 4),
+                                             c = __shfl(v, 5);
+                    if ((q ^ a ^ b ^ n ^ kLabMix) == c) {
+                        if (lane == 0) {
+                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope: fresh lines
+                            s_src = reinterpret_cast<const unsigned char *>(a);
+                            s_dst = reinterpret_cast<unsigned char *>(b);
+                            s_bytes = n;
+                        }
+                        break;
+                    }
+                    continue;   // torn: read the line again
+                }
+                if (quit || __builtin_amdgcn_s_memrealtime() - t_last > idle_ticks) {
+                    q = 0;
+                    break;
+                }
+                if (lane == 0 && (++npoll & 1023) == 0)
+                    __hip_atomic_store(&mb->polls, npoll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (lane == 0) s_seq = q;
+        } else if (!LINE && threadIdx.x == 0) {
+            unsigned long long q = 0;
+            for (;;) {
+                q = __hip_atomic_load(&mb->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                if (q != last) break;
+                if (__hip_atomic_load(&mb->quit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+                    q = 0;
+                    break;
+                }
+                if (__builtin_amdgcn_s_memrealtime() - t_last > idle_ticks) {
+                    q = 0;
+                    break;
+                }
+                if ((++npoll & 1023) == 0)
+                    __hip_atomic_store(&mb->polls, npoll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (q) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // system scope: fresh lines
+                s_src = static_cast<const unsigned char *>(mb->src);
+                s_dst = static_cast<unsigned char *>(mb->dst);
+                s_bytes = mb->bytes;
+            }
+            s_seq = q;
+        }
+        __syncthreads();
+        const unsigned long long q = s_seq;
+        if (!q) return;   // every wave of the workgroup leaves together
+        const unsigned char *src = s_src;
+        unsigned char *dst = s_dst;
+        const unsigned long long n = s_bytes;
+        if (((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) | n) & 15) == 0) {
+            for (unsigned long long i = threadIdx.x; i < n / 16; i += 256)
+                reinterpret_cast<uint4 *>(dst)[i] = reinterpret_cast<const uint4 *>(src)[i];
+        } else {
+            for (unsigned long long i = threadIdx.x; i < n; i += 256) dst[i] = src[i];
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_store(&mb->done, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        last = q;
+        t_last = __builtin_amdgcn_s_memrealtime();
+        __syncthreads();
+    }
+}
+
+
+
+static double now_us() { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+template <class MB, class Post> static void bench(const char *name, MB *mb, hipStream_t svc, int reps, Post post) {
+    unsigned long long seq = 0;
+    for (double gap : {0.0, 0.4, 0.8, 1.2}) {
+        std::vector<double> rt;
+        for (int r = 0; r < reps + 100; ++r) {
+            { const double t0 = now_us(); while (now_us() - t0 < gap) {} }
+            ++seq; post(mb, seq);
+            const volatile unsigned long long *d = &mb->done; const double t0 = now_us();
+            while (*d != seq) if (now_us() - t0 > 2e6) { std::printf("hung\n"); std::exit(3); }
+            if (r >= 100) rt.push_back(now_us() - t0);
+        }
+        std::sort(rt.begin(), rt.end());
+        std::printf("%-4s gap %.1f: post to done median %.2f p10 %.2f p90 %.2f\n", name, gap, rt[rt.size()/2], rt[rt.size()/10], rt[rt.size()*9/10]);
+    }
+    __atomic_store_n(&mb->quit, 1ull, __ATOMIC_RELEASE); (void)hipStreamSynchronize(svc);
+}
+int main(int argc, char **argv) {
+    std::setvbuf(stdout, nullptr, _IONBF, 0);
+    const int reps = 2000;
+    const unsigned long long bytes = argc > 1 ? std::atoll(argv[1]) : 16;
+    (void)hipSetDevice(0);
+    char *src, *tgt; (void)hipMalloc(&src, 1 << 20); (void)hipMalloc(&tgt, 1 << 20); (void)hipMemset(src, 1, 1 << 20); (void)hipDeviceSynchronize();
+    int lo = 0, hi = 0; (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    hipStream_t svc; (void)hipStreamCreateWithPriority(&svc, hipStreamNonBlocking, hi);
+    for (int round = 0; round < 2; ++round) {
+#define RUN_LIB(NS) { NS::Mailbox *mb; (void)hipHostMalloc((void **)&mb, sizeof *mb, hipHostMallocCoherent); std::memset(mb, 0, sizeof *mb); \
+        hipLaunchKernelGGL(NS::service_kernel, dim3(1), dim3(NS::kSvcBlock), 0, svc, mb, 0ull, 20000000ull); \
+        bench(#NS, mb, svc, reps, [&](NS::Mailbox *m, unsigned long long q) { m->src = src; m->dst = tgt; m->dst2 = nullptr; m->bytes = bytes; \
+            m->check = q ^ (uintptr_t)src ^ (uintptr_t)tgt ^ bytes ^ NS::kMix; __atomic_store_n(&m->seq, q, __ATOMIC_RELEASE); }); }
+        RUN_LIB(A) RUN_LIB(D) RUN_LIB(G)
+        { LabMailbox *mb; (void)hipHostMalloc((void **)&mb, sizeof *mb, hipHostMallocCoherent); std::memset(mb, 0, sizeof *mb);
+          hipLaunchKernelGGL(service_kernel<true>, dim3(1), dim3(256), 0, svc, mb, 0ull, 20000000ull);
+          bench("lab", mb, svc, reps, [&](LabMailbox *m, unsigned long long q) { m->src = src; m->dst = tgt; m->bytes = bytes;
+            m->check = q ^ (uintptr_t)src ^ (uintptr_t)tgt ^ bytes ^ kLabMix; __atomic_store_n(&m->seq, q, __ATOMIC_RELEASE); }); }
+    }
+    std::printf("ok\n");
+}
