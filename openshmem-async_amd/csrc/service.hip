@@ -9,12 +9,12 @@
 // algorithm.  Here one workgroup stays resident on its own
 // non-blocking stream and polls a mailbox in page-locked, host-coherent
 // memory: the host writes the call's descriptor and a sequence number into
-// one 64-byte line, the workgroup's first wave reads that whole line with
-// one load instruction (no second round trip over PCIe for the descriptor;
-// a check word catches a torn read), drops stale lines (system-scope
-// acquire), copies, writes back (system-scope release) and stores the
-// sequence number into a second host-coherent line the host spins on:
-// 2.2-3.8 us per round trip by the phase of the post (below).
+// one 64-byte line, a polling wave reads that whole line with one scalar load
+// (no second round trip over PCIe for the descriptor; a check word catches a
+// torn read), drops stale lines (system-scope acquire) and hands the request
+// to the copy waves, which copy, write back (system-scope release) and store
+// the sequence number into a second host-coherent line the host spins on:
+// 2.5-2.7 us per round trip for 16 bytes, 3.2 at 32 KiB (service_kernel).
 //
 // Ordering.  A blocking call is ordered after the legacy default stream and
 // the library's stream (the buffers a plain HIP program, or PyTorch's
@@ -31,8 +31,8 @@
 // (state.h lib_stream_dirty).
 //
 // Lifetime.  The workgroup leaves by itself after kIdleUs without a request
-// (every wave reaches that exit: the first wave decides, the workgroup
-// barrier releases the others), at once when the host stores the quit word
+// (every wave reaches that exit: poller 0 decides, the LDS claim and request
+// words release the others), at once when the host stores the quit word
 // (service_quiesce: shmem_finalize, an atexit handler, and before the
 // library's own device-wide synchronisations), and is launched again by the
 // next call that finds its stream idle.  A request posted while it was
