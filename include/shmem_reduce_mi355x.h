@@ -340,11 +340,17 @@ int shmemx_rccl_register_heap(int on);
  * stream's earlier work (the host waits for them first when they still have
  * some); it leaves after 200 us without a request (so a
  * program's hipDeviceSynchronize waits that long at most) and at
- * shmem_finalize.  $SHMEMX_SERVICE=0 turns it off.  Stats: out[0] calls
- * served, out[1] launches of the workgroup, out[2] / out[3] calls that found
- * the legacy default stream / the library's stream busy and waited for it,
- * out[4] / out[5] nanoseconds summed over the served calls from the check's
- * start to the post / from the post to the result; returns how many were
+ * shmem_finalize.  A blocking call over several PEs of at most 4 KiB per PE
+ * under SHMEMX_ALGO_AUTO is served the same way: each member leaves its
+ * source in a page-locked exchange shared by the job's PEs, and after the
+ * entry barrier its workgroup folds every member's source into its target
+ * (no kernel launch, no GPU reading another GPU's memory), then the exit
+ * barrier.  $SHMEMX_SERVICE=0 turns both off (every PE alike).  Stats:
+ * out[0] requests served, out[1] launches of the workgroup, out[2] / out[3]
+ * requests that found the legacy default stream / the library's stream busy
+ * and waited for it, out[4] / out[5] nanoseconds summed over the served
+ * requests from the check's start to the post / from the post to the result,
+ * out[6] folds of the exchange (multi-PE calls); returns how many were
  * written. */
 int shmemx_service_stats(unsigned long long *out, int nout, int reset);
 

@@ -49,7 +49,10 @@ struct Mapping {
 
 struct Node {
     Shared *sh = nullptr;
-    std::string name;
+    std::string name, xname;   // the block's and the exchange's /dev/shm names
+    uint64_t hash = 0;
+    char *xchg = nullptr;      // the exchange slots: host mapping, device address
+    char *xchg_dev = nullptr;
     int pe = 0, npes = 0;
     uint64_t entered[kMaxPes] = {};     // barriers entered with each peer
     char *own[kNumRegions] = {};
@@ -122,6 +125,7 @@ bool attach(int pe, int npes, const void *key, size_t keylen) {
     if (p == MAP_FAILED) return false;
     g_node.sh = static_cast<Shared *>(p);
     g_node.name = name;
+    g_node.hash = h;
     g_node.pe = pe;
     g_node.npes = npes;
     std::memset(g_node.entered, 0, sizeof g_node.entered);
@@ -132,10 +136,62 @@ bool attach(int pe, int npes, const void *key, size_t keylen) {
 void unlink_name() {
     if (g_node.sh && !g_node.name.empty()) shm_unlink(g_node.name.c_str());
     g_node.name.clear();
+    if (!g_node.xname.empty()) shm_unlink(g_node.xname.c_str());
+    g_node.xname.clear();
+}
+
+namespace {
+constexpr size_t kXchgBytes = kMaxPes * kXchgSlotBytes;
+void xchg_detach() {
+    if (!g_node.xchg) return;
+    if (g_node.xchg_dev) (void)hipHostUnregister(g_node.xchg);
+    munmap(g_node.xchg, kXchgBytes);
+    g_node.xchg = g_node.xchg_dev = nullptr;
+}
+}  // namespace
+
+bool xchg_attach() {
+    if (g_node.xchg_dev) return true;
+    if (!g_node.sh) return false;
+    char name[64];
+    snprintf(name, sizeof name, "/shmemx_xchg_%016llx", (unsigned long long)g_node.hash);
+    const int fd = shm_open(name, O_RDWR | O_CREAT, 0600);
+    if (fd < 0) return false;
+    g_node.xname = name;
+    if (ftruncate(fd, kXchgBytes) != 0) {
+        close(fd);
+        return false;
+    }
+    void *p = mmap(nullptr, kXchgBytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) return false;
+    g_node.xchg = static_cast<char *>(p);
+    // page-locked and mapped into the GPU's address space: the service
+    // workgroups of every member read and write it over PCIe
+    void *d = nullptr;
+    if (hipHostRegister(p, kXchgBytes, hipHostRegisterMapped) != hipSuccess ||
+        hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        trace(LOG_INIT, "small-call exchange %s: page-locking failed", name);
+        xchg_detach();
+        return false;
+    }
+    g_node.xchg_dev = static_cast<char *>(d);
+    trace(LOG_INIT, "small-call exchange %s (%zu bytes) at %p, device %p", name, kXchgBytes, p, d);
+    return true;
+}
+
+char *xchg_host(int q) {
+    return g_node.xchg_dev && q >= 0 && q < kMaxPes ? g_node.xchg + (size_t)q * kXchgSlotBytes : nullptr;
+}
+
+char *xchg_dev(int q) {
+    return g_node.xchg_dev && q >= 0 && q < kMaxPes ? g_node.xchg_dev + (size_t)q * kXchgSlotBytes : nullptr;
 }
 
 void detach(bool unlink) {
     if (!g_node.sh) return;
+    xchg_detach();
     for (int r = 0; r < kNumRegions; ++r)
         for (int q = 0; q < kMaxPes; ++q) close_peer(static_cast<Region>(r), q);
     if (unlink) unlink_name();

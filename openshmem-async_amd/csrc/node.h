@@ -71,6 +71,17 @@ uint64_t region_gen(Region r, int pe);
 // open) turns into the same error return on all of them instead of a hang.
 bool agree(int start, int step, int P, bool ok);
 
+// The small-call exchange (staging.cpp, service.hip): one slot of
+// kXchgSlotBytes per PE in a second shared-memory block of the job, page-
+// locked and mapped into this GPU (hipHostRegister), where every member of a
+// small blocking call leaves its source for the others' service workgroups.
+// xchg_attach maps and registers it (false on any error; every PE calls it at
+// init and the job agrees); the name goes with unlink_name().
+constexpr size_t kXchgSlotBytes = 4096;
+bool xchg_attach();
+char *xchg_host(int pe);   // a slot's host address (nullptr if not attached)
+char *xchg_dev(int pe);    // the same slot's device address
+
 void put_desc(const Desc &d);
 Desc get_desc(int pe);
 

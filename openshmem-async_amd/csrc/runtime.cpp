@@ -247,6 +247,7 @@ static int init_locked(int pe, int npes, int device, const void *uid) {
     g_state.force_collective = env_int("SHMEMX_FORCE_COLLECTIVE", nullptr, 0) != 0;
     g_state.ipc_only = ipc_transport_env();
     g_state.node_shared = false;
+    g_state.xchg = false;
     if (npes > 1 || g_state.force_collective) {
         ncclUniqueId id;
         if (npes > 1) {
@@ -282,8 +283,10 @@ static int init_locked(int pe, int npes, int device, const void *uid) {
         // then, so a job that dies leaves nothing in /dev/shm.
         if (attached) {
             node::put_gpu_numa(gpu_numa_node(device));   // (staging.cpp's copy threads)
+            const bool xchg = npes > 1 && node::xchg_attach();   // (opened before the names go)
             node::barrier(0, 1, npes);
             if (pe == 0) node::unlink_name();
+            g_state.xchg = npes > 1 && node::agree(0, 1, npes, xchg);
         }
     }
     g_state.pe = pe;
@@ -989,6 +992,7 @@ void pshmem_finalize(void) {
     (void)hipStreamDestroy(g_state.stream);
     g_state.stream = nullptr;
     g_state.node_shared = false;
+    g_state.xchg = false;
     g_state.inited = false;
 }
 

@@ -46,7 +46,9 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "fold_ops.h"
 #include "internal.h"
+#include "node.h"
 #include "shmem_reduce_mi355x.h"
 #include "state.h"
 
@@ -75,8 +77,8 @@ struct alignas(64) Mailbox {
     void *dst;
     void *dst2;   // a second destination (the mirrored heap's view), or null
     unsigned long long bytes;
-    unsigned long long check;   // seq ^ src ^ dst ^ dst2 ^ bytes ^ kMix
-    unsigned long long pad;
+    unsigned long long check;   // seq ^ src ^ dst ^ dst2 ^ bytes ^ cfg ^ kMix
+    unsigned long long cfg;     // 0: a copy; else a fold of the exchange slots (fold_cfg)
     alignas(64) unsigned long long done;
 };
 static_assert(sizeof(Mailbox) == 128, "two lines");
@@ -103,6 +105,100 @@ __device__ __forceinline__ void copy_as(int t, const unsigned char *src, unsigne
         const V x = s[i];
         d[i] = x;
         if (dst2) d2[i] = x;
+    }
+}
+
+// A fold request: bit 0 set; type, op, the calling PE's own order or
+// PE_start's, and the set (PE_start, logPE_stride, PE_size) with the caller.
+struct FoldCfg {
+    int type, op, own, start, logstride, size, me;
+};
+__host__ __device__ inline unsigned long long pack_cfg(const FoldCfg &f) {
+    return 1ull | (unsigned long long)f.type << 1 | (unsigned long long)f.op << 5 |
+           (unsigned long long)f.own << 8 | (unsigned long long)f.start << 9 |
+           (unsigned long long)f.logstride << 16 | (unsigned long long)f.size << 24 |
+           (unsigned long long)f.me << 32;
+}
+__device__ inline FoldCfg unpack_cfg(unsigned long long c) {
+    return FoldCfg{(int)(c >> 1 & 15), (int)(c >> 5 & 7), (int)(c >> 8 & 1), (int)(c >> 9 & 127),
+                   (int)(c >> 16 & 7), (int)(c >> 24 & 127), (int)(c >> 32 & 127)};
+}
+
+// The j-th input of PE me's fold: its own source first, then the other
+// members in ascending order (reduce-op.c:219-248), or PE_start's order
+// (every member the same bits: the DIRECT / A2A convention).
+__device__ __forceinline__ int member_at(const FoldCfg &f, int j) {
+    if (!f.own) return f.start + (j << f.logstride);
+    const int r = (f.me - f.start) >> f.logstride;
+    if (j == 0) return f.me;
+    return f.start + ((j - 1 < r ? j - 1 : j) << f.logstride);
+}
+
+// Element i of the fold, for copy thread t: up to 8 members' words loaded
+// before the first op (the slots are in host memory: one round trip per 8).
+template <typename T, int OP>
+__device__ void fold_slots(int t, const unsigned char *slots, unsigned char *dst, unsigned char *dst2,
+                           unsigned long long bytes, const FoldCfg &f) {
+    const unsigned long long n = bytes / sizeof(T);
+    for (unsigned long long i = t; i < n; i += kCopyThreads) {
+        T acc{};
+        for (int j0 = 0; j0 < f.size; j0 += 8) {
+            T v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (j0 + u < f.size)
+                    v[u] = reinterpret_cast<const T *>(slots + (size_t)member_at(f, j0 + u) * node::kXchgSlotBytes)[i];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (j0 + u < f.size) acc = j0 + u == 0 ? v[u] : Op<T, OP>::ap(acc, v[u]);
+        }
+        reinterpret_cast<T *>(dst)[i] = acc;
+        if (dst2) reinterpret_cast<T *>(dst2)[i] = acc;
+    }
+}
+
+template <typename T>
+__device__ void fold_int(int t, const unsigned char *sl, unsigned char *d, unsigned char *d2, unsigned long long b,
+                         const FoldCfg &f) {
+    switch (f.op) {
+    case SHMEMX_OP_SUM: fold_slots<T, SHMEMX_OP_SUM>(t, sl, d, d2, b, f); break;
+    case SHMEMX_OP_PROD: fold_slots<T, SHMEMX_OP_PROD>(t, sl, d, d2, b, f); break;
+    case SHMEMX_OP_AND: fold_slots<T, SHMEMX_OP_AND>(t, sl, d, d2, b, f); break;
+    case SHMEMX_OP_OR: fold_slots<T, SHMEMX_OP_OR>(t, sl, d, d2, b, f); break;
+    case SHMEMX_OP_XOR: fold_slots<T, SHMEMX_OP_XOR>(t, sl, d, d2, b, f); break;
+    case SHMEMX_OP_MIN: fold_slots<T, SHMEMX_OP_MIN>(t, sl, d, d2, b, f); break;
+    default: fold_slots<T, SHMEMX_OP_MAX>(t, sl, d, d2, b, f); break;
+    }
+}
+template <typename T>
+__device__ void fold_fp(int t, const unsigned char *sl, unsigned char *d, unsigned char *d2, unsigned long long b,
+                        const FoldCfg &f) {
+    switch (f.op) {
+    case SHMEMX_OP_SUM: fold_slots<T, SHMEMX_OP_SUM>(t, sl, d, d2, b, f); break;
+    case SHMEMX_OP_PROD: fold_slots<T, SHMEMX_OP_PROD>(t, sl, d, d2, b, f); break;
+    case SHMEMX_OP_MIN: fold_slots<T, SHMEMX_OP_MIN>(t, sl, d, d2, b, f); break;
+    default: fold_slots<T, SHMEMX_OP_MAX>(t, sl, d, d2, b, f); break;
+    }
+}
+template <typename T>
+__device__ void fold_cplx(int t, const unsigned char *sl, unsigned char *d, unsigned char *d2,
+                          unsigned long long b, const FoldCfg &f) {
+    if (f.op == SHMEMX_OP_SUM) fold_slots<T, SHMEMX_OP_SUM>(t, sl, d, d2, b, f);
+    else fold_slots<T, SHMEMX_OP_PROD>(t, sl, d, d2, b, f);
+}
+__device__ void fold_request(int t, const unsigned char *sl, unsigned char *d, unsigned char *d2,
+                             unsigned long long b, unsigned long long cfg) {
+    const FoldCfg f = unpack_cfg(cfg);
+    switch (f.type) {
+    case SHMEMX_TYPE_SHORT: fold_int<short>(t, sl, d, d2, b, f); break;
+    case SHMEMX_TYPE_INT: fold_int<int>(t, sl, d, d2, b, f); break;
+    case SHMEMX_TYPE_LONG:
+    case SHMEMX_TYPE_LONGLONG: fold_int<long>(t, sl, d, d2, b, f); break;
+    case SHMEMX_TYPE_FLOAT: fold_fp<float>(t, sl, d, d2, b, f); break;
+    case SHMEMX_TYPE_DOUBLE: fold_fp<double>(t, sl, d, d2, b, f); break;
+    case SHMEMX_TYPE_LONGDOUBLE: fold_fp<ld80>(t, sl, d, d2, b, f); break;
+    case SHMEMX_TYPE_COMPLEXD: fold_cplx<cplxd>(t, sl, d, d2, b, f); break;
+    default: fold_cplx<cplxf>(t, sl, d, d2, b, f); break;
     }
 }
 
@@ -142,7 +238,7 @@ __device__ __forceinline__ unsigned long long word(const line_t &v, int k) {
 // relaunch (service_copy).
 __global__ __launch_bounds__(kSvcBlock) void service_kernel(Mailbox *mb, unsigned long long served,
                                                          unsigned long long idle_ticks) {
-    __shared__ unsigned long long s_claim, s_req, s_done, s_count, s_bytes;
+    __shared__ unsigned long long s_claim, s_req, s_done, s_count, s_bytes, s_cfg;
     __shared__ const unsigned char *s_src;
     __shared__ unsigned char *s_dst, *s_dst2;
     if (threadIdx.x == 0) {
@@ -164,8 +260,8 @@ __global__ __launch_bounds__(kSvcBlock) void service_kernel(Mailbox *mb, unsigne
             if (claim == kExit) break;
             if (q != last) {
                 const unsigned long long a = word(v, 2), b = word(v, 3), b2 = word(v, 4), n = word(v, 5),
-                                         c = word(v, 6);
-                if ((q ^ a ^ b ^ b2 ^ n ^ kMix) == c) {   // else a torn read: the next one
+                                         c = word(v, 6), g = word(v, 7);
+                if ((q ^ a ^ b ^ b2 ^ n ^ g ^ kMix) == c) {   // else a torn read: the next one
                     last = q;
                     t_last = __builtin_amdgcn_s_memrealtime();
                     if (claim != q && lds_cas(&s_claim, claim, q)) {
@@ -173,6 +269,7 @@ __global__ __launch_bounds__(kSvcBlock) void service_kernel(Mailbox *mb, unsigne
                         s_dst = reinterpret_cast<unsigned char *>(b);
                         s_dst2 = reinterpret_cast<unsigned char *>(b2);
                         s_bytes = n;
+                        s_cfg = g;
                         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // lines written since: dropped
                         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
                         lds_store(&s_req, q);
@@ -202,10 +299,11 @@ __global__ __launch_bounds__(kSvcBlock) void service_kernel(Mailbox *mb, unsigne
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         const unsigned char *src = s_src;
         unsigned char *dst = s_dst, *dst2 = s_dst2;
-        const unsigned long long n = s_bytes;
+        const unsigned long long n = s_bytes, cfg = s_cfg;
         const uintptr_t al = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) |
                              reinterpret_cast<uintptr_t>(dst2) | n;
-        if ((al & 15) == 0) copy_as<v4u>(t, src, dst, dst2, n);
+        if (cfg) fold_request(t, src, dst, dst2, n, cfg);
+        else if ((al & 15) == 0) copy_as<v4u>(t, src, dst, dst2, n);
         else if ((al & 7) == 0) copy_as<unsigned long long>(t, src, dst, dst2, n);
         else if ((al & 3) == 0) copy_as<unsigned>(t, src, dst, dst2, n);
         else if ((al & 1) == 0) copy_as<unsigned short>(t, src, dst, dst2, n);
@@ -232,7 +330,7 @@ struct Service {
     bool exit_hook = false;
     // shmemx_service_stats: calls served, launches, calls that found the
     // legacy / the library stream busy (and waited for it first)
-    unsigned long long served = 0, launches = 0, busy_null = 0, busy_lib = 0;
+    unsigned long long served = 0, launches = 0, busy_null = 0, busy_lib = 0, folds = 0;
     // nanoseconds summed over the served calls: from entering service_copy
     // to the post, and from the post to seeing the result done
     unsigned long long ns_before_post = 0, ns_round_trip = 0;
@@ -300,10 +398,8 @@ bool stream_idle(hipStream_t s) {
     return false;
 }
 
-}  // namespace
-
-bool service_copy(void *dst, void *dst2, const void *src, size_t bytes) {
-    if (!enabled() || bytes == 0 || bytes > kServiceMaxBytes || !dst || !src) return false;
+// Post one request and wait for it: a copy (cfg 0) or a fold (cfg = pack_cfg).
+bool serve(void *dst, void *dst2, const void *src, size_t bytes, unsigned long long cfg) {
     // ordered after the legacy stream and the library stream: once both have
     // no work left (the resident workgroup's own stream, non-blocking, is
     // not part of the null stream's wait)
@@ -331,8 +427,9 @@ bool service_copy(void *dst, void *dst2, const void *src, size_t bytes) {
     mb->dst = dst;
     mb->dst2 = dst2;
     mb->bytes = bytes;
+    mb->cfg = cfg;
     mb->check = q ^ reinterpret_cast<uintptr_t>(src) ^ reinterpret_cast<uintptr_t>(dst) ^
-                reinterpret_cast<uintptr_t>(dst2) ^ (unsigned long long)bytes ^ kMix;
+                reinterpret_cast<uintptr_t>(dst2) ^ (unsigned long long)bytes ^ cfg ^ kMix;
     __atomic_store_n(&mb->seq, q, __ATOMIC_RELEASE);
     const auto t_post = std::chrono::steady_clock::now();
     const volatile unsigned long long *done = &mb->done;
@@ -347,10 +444,27 @@ bool service_copy(void *dst, void *dst2, const void *src, size_t bytes) {
     }
     g_svc.last_use = std::chrono::steady_clock::now();
     ++g_svc.served;
+    if (cfg) ++g_svc.folds;
     g_svc.ns_before_post += (unsigned long long)std::chrono::duration_cast<std::chrono::nanoseconds>(t_post - t_begin).count();
     g_svc.ns_round_trip +=
         (unsigned long long)std::chrono::duration_cast<std::chrono::nanoseconds>(g_svc.last_use - t_post).count();
     return true;
+}
+
+}  // namespace
+
+bool service_copy(void *dst, void *dst2, const void *src, size_t bytes) {
+    if (!enabled() || bytes == 0 || bytes > kServiceMaxBytes || !dst || !src) return false;
+    return serve(dst, dst2, src, bytes, 0);
+}
+
+bool service_available() { return enabled(); }
+
+void service_fold(int type, int op, bool own_order, int start, int logstride, int size, void *dst, void *dst2,
+                  size_t bytes) {
+    const FoldCfg f{type, op, own_order ? 1 : 0, start, logstride, size, g_state.pe};
+    if (!serve(dst, dst2, node::xchg_dev(0), bytes, pack_cfg(f)))
+        fatal("service workgroup", "a small multi-PE call could not reach the service workgroup");
 }
 
 void service_quiesce() {
@@ -382,10 +496,10 @@ extern "C" int shmemx_service_stats(unsigned long long *out, int nout, int reset
     std::lock_guard<std::recursive_mutex> lk(shmx::g_mu);
     if (!out || nout < 0) return shmx::set_error(SHMEMX_EINVAL), -1;
     shmx::Service &v = shmx::g_svc;
-    const unsigned long long all[6] = {v.served, v.launches, v.busy_null, v.busy_lib, v.ns_before_post,
-                                       v.ns_round_trip};
-    const int k = nout < 6 ? nout : 6;
+    const unsigned long long all[7] = {v.served, v.launches, v.busy_null, v.busy_lib, v.ns_before_post,
+                                       v.ns_round_trip, v.folds};
+    const int k = nout < 7 ? nout : 7;
     for (int i = 0; i < k; ++i) out[i] = all[i];
-    if (reset) v.served = v.launches = v.busy_null = v.busy_lib = v.ns_before_post = v.ns_round_trip = 0;
+    if (reset) v.served = v.launches = v.busy_null = v.busy_lib = v.ns_before_post = v.ns_round_trip = v.folds = 0;
     return k;
 }

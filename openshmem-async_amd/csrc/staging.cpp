@@ -28,6 +28,7 @@
 #include "heap.h"
 #include "internal.h"
 #include "shmem_reduce_mi355x.h"
+#include "node.h"
 #include "state.h"
 #include "stage_plan.h"
 #include "topology.h"
@@ -498,6 +499,38 @@ void reduce_blocking(int type, int op, void *target, const void *source,
 static void reduce_blocking_impl2(int type, int op, void *target, const void *source, int nreduce,
                                   int start, int logstride, int size, bool trace_call);
 
+// A small blocking call over several PEs (<= 4 KiB per PE): the reference's
+// barrier, gets and barrier (reduce-op.c:217-250) with the gets and the fold
+// done by each member's resident service workgroup (service.hip), no kernel
+// launch.  Each member leaves its source in its slot of the job's page-locked
+// exchange (node.h; a device source by a service copy, a host one by the
+// CPU), passes the entry barrier, has its workgroup fold every member's slot
+// (its own order for the pairs where the order decides the answer, else
+// PE_start's, as DIRECT and A2A do) into its target (a host target through
+// the bounce buffer), and passes the exit barrier, after which its slot may
+// be written again.  Host memory is the meeting point, so no GPU reads
+// another GPU's memory and no L2 write-back beyond each workgroup's own
+// system-scope release is needed.
+static void xchg_reduce(int type, int op, void *target, bool tdev, const void *source, bool sdev, size_t bytes,
+                        int start, int logstride, int size) {
+    const int step = 1 << logstride;
+    if (!tdev && !small_bounce_reserve())
+        fatal("small multi-PE call", "no page-locked bounce buffer for a host target");
+    if (sdev) {
+        if (!service_copy(node::xchg_dev(g_state.pe), nullptr, source, bytes))
+            fatal("small multi-PE call", "the service workgroup did not take the source");
+    } else {
+        std::memcpy(node::xchg_host(g_state.pe), source, bytes);
+    }
+    node::barrier(start, step, size);
+    char *bout = static_cast<char *>(g_state.bounce) + kSmallHostBytes;
+    void *dst2 = tdev ? g_state.settle_dst : nullptr;
+    service_fold(type, op, own_order_pair(type, op), start, logstride, size, tdev ? target : bout, dst2, bytes);
+    if (dst2) g_state.settled = true;
+    if (!tdev) std::memcpy(target, bout, bytes);
+    node::barrier(start, step, size);
+}
+
 // A blocking call returns as soon as its work's host signal arrives.
 static void reduce_blocking_impl(int type, int op, void *target, const void *source, int nreduce,
                                  int start, int logstride, int size, bool trace_call) {
@@ -546,6 +579,14 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
         }
     }
     if (trace_call) trace_reference_overlap(target, source, bytes);   // the caller's arrays
+    // A small call over several PEs under auto: through the exchange and the
+    // service workgroups (xchg_reduce).  Every member decides alike: the
+    // same size, set and settings, and g_state.xchg was agreed at init.
+    if (size > 1 && bytes <= node::kXchgSlotBytes && g_state.xchg && g_state.algo == SHMEMX_ALGO_AUTO &&
+        !g_state.force_collective && service_available()) {
+        xchg_reduce(type, op, target, tdev, source, sdev, bytes, start, logstride, size);
+        return;
+    }
     if (tdev && sdev) {
         if (collective && bytes > kSmallHostBytes && !calls_agree(start, logstride, size, 1)) return;
         if (plan.nmembers == 1 && !collective && !overlap(target, source, bytes)) {

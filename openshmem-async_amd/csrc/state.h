@@ -32,6 +32,7 @@ struct State {
     // IPC transport a PE without it is fatal).  AUTO's plan reads this, never
     // per-process state, so every PE plans alike.
     bool node_shared = false;
+    bool xchg = false;   // every PE mapped the small-call exchange (node.h), agreed at init
     // the heap segment registered with the RCCL communicator
     // (shmemx_rccl_register_heap), or nullptr
     void *rccl_reg = nullptr;
@@ -145,6 +146,14 @@ int gpu_numa_node(int device);   // NUMA node of a HIP device's PCI function, or
 // not taken ($SHMEMX_SERVICE=0, or no mailbox): the caller launches.
 constexpr size_t kServiceMaxBytes = size_t(32) << 10;
 bool service_copy(void *dst, void *dst2, const void *src, size_t bytes);
+// Small multi-PE blocking calls (staging.cpp): every member has left its
+// source in its exchange slot (node.h) and passed the entry barrier; the
+// service workgroup folds the members' slots, in the calling PE's own order
+// or PE_start's, into dst (and dst2 if not null).  Aborts if the workgroup
+// cannot be reached (the members decided on this path together).
+bool service_available();   // $SHMEMX_SERVICE is not 0
+void service_fold(int type, int op, bool own_order, int start, int logstride, int size, void *dst, void *dst2,
+                  size_t bytes);
 void service_quiesce();   // the workgroup leaves now, if it is up
 void service_release();   // shmem_finalize (and at exit)
 void device_sync();       // service_quiesce, then hipDeviceSynchronize

@@ -445,7 +445,7 @@ def direct_stats(reset: bool = True) -> dict:
 
 
 SERVICE_STATS = ("served", "launches", "null_stream_busy", "library_stream_busy", "ns_before_post",
-                 "ns_round_trip")
+                 "ns_round_trip", "folds")
 
 
 def service_stats(reset: bool = False) -> dict:

@@ -702,6 +702,29 @@ elif scenario == "ownorder":
     for t in ("float", "double"):
         seed += 1
         run_case(t, "max", 4103, (0, 0, npes), "auto", "host", seed, special=True)
+elif scenario == "xchg":
+    # Small blocking calls over several PEs under auto (<= 4 KiB per PE):
+    # each member's resident service workgroup folds the members' exchange
+    # slots (staging.cpp xchg_reduce), no kernel launch.  Every reference
+    # pair at 1 element, at the 4 KiB limit and one element past it (DIRECT /
+    # RCCL again), every active set, heap operands; host and in-place host
+    # operands for a few pairs; the own-order pairs on NaN / +-0 sources.
+    shm.service_stats(reset=True)
+    for (t, op) in shm.REFERENCE_PAIRS:
+        sz = oracle.NP_DTYPE[t]().itemsize
+        for n in (1, 4096 // sz, 4096 // sz + 1):
+            for st in active_sets():
+                seed += 1
+                run_case(t, op, n, st, "auto", "heap", seed, special=(t, op) in OWN_ORDER)
+    for (t, op) in (("int", "sum"), ("double", "max"), ("longdouble", "sum"), ("complexf", "prod")):
+        for mode in ("host", "hostinplace"):
+            for st in active_sets():
+                seed += 1
+                run_case(t, op, 4096 // oracle.NP_DTYPE[t]().itemsize, st, "auto", mode, seed,
+                         special=(t, op) in OWN_ORDER)
+    extra["folds"] = shm.service_stats(reset=True)["folds"]
+    if npes > 1 and not extra["folds"]:
+        fails.append("no small multi-PE call was folded by the service workgroup")
 elif scenario == "config0":
     # BASELINE.json configs[0]: shmem_int_sum_to_all, nreduce = 1024, on 2 PEs
     # (the reference's "oshrun loopback"), through the C entry point itself

@@ -165,6 +165,29 @@ def test_own_order_min_max_on_nan_and_signed_zeros(tmp_path, transport, npes):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("transport,npes,heap", [("ipc", 2, "device"), ("ipc", 3, "mirrored"), ("ipc", 8, "device"),
+                                                 ("rccl", 3, "device")])
+def test_small_multi_pe_calls_through_the_service_exchange(tmp_path, transport, npes, heap):
+    """Blocking calls of at most 4 KiB per PE over several PEs under auto:
+    each member leaves its source in the job's page-locked exchange, passes
+    the entry barrier, its resident service workgroup folds every member's
+    slot into its target, then the exit barrier (reduce-op.c:217-250's
+    barrier, gets, barrier, with no kernel launch).  Every reference pair at
+    1 element, at the limit and one past it, every active set, heap / host /
+    in-place operands, own-order pairs on NaN / +-0 sources; every PE against
+    the oracle (its own order where that decides the answer, else
+    PE_start's), and the folds are counted, so the path is the one that ran."""
+    env = {"SHMEMX_TRANSPORT": transport, "SHMEMX_HEAP_MEMORY": heap}
+    if transport == "rccl":
+        env["FAKE_RCCL"] = os.path.join(HERE, "native", "libfake_rccl.so")
+    reports = run_pes(tmp_path, npes, "xchg", env, timeout=300)
+    for r in reports:
+        assert r["ncases"] > 0
+        assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
+        assert r["folds"] > 0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("transport,heap", [("ipc", "device"), ("ipc", "mirrored"), ("rccl", "device")])
 def test_baseline_config0_int_sum_1024_two_pes(tmp_path, transport, heap):
     """BASELINE.json configs[0]: shmem_int_sum_to_all, nreduce = 1024, 2 PEs,
