@@ -514,6 +514,9 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
 static void xchg_reduce(int type, int op, void *target, bool tdev, const void *source, bool sdev, size_t bytes,
                         int start, int logstride, int size) {
     const int step = 1 << logstride;
+    if (log_enabled(LOG_REDUCTION))
+        trace(LOG_REDUCTION, "type %d op %d nreduce %zu set (%d,%d,%d) algo service exchange%s", type, op,
+              bytes / type_size(type), start, logstride, size, own_order_pair(type, op) ? " (own order)" : "");
     if (!tdev && !small_bounce_reserve())
         fatal("small multi-PE call", "no page-locked bounce buffer for a host target");
     if (sdev) {
