@@ -1,6 +1,7 @@
 // Lab: variants of the service kernel against the lab's line-read kernel,
 // same host code (what the library kernel's extra 0.4 us is):
-//   A  the library's kernel (csrc/service.hip, extracted when this file was made)
+//   A  the library's kernel (csrc/service.hip, extracted when this file was made;
+//      with the exchange fold)
 //   B  A with 1024 threads (earlier: each lane's loads all issued before
 //      its stores, unconditional and clamped: 2.89 vs 2.63 us at 8 KiB)
 //   C  the kernel before that with the lab's plain copy loops
@@ -18,129 +19,20 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
-namespace A {
+#include "fold_ops.h"
+#include "node.h"
+namespace shmx { namespace A {
 constexpr unsigned long long kMix = 0x9E3779B97F4A7C15ull;
 constexpr unsigned kIdleUs = 200;
-constexpr int kSvcBlock = 256;
-
-// Written by the host: the first line (seq last, with release); by the
-// device: the second.
-struct alignas(64) Mailbox {
-    unsigned long long seq;
-    unsigned long long quit;
-    const void *src;
-    void *dst;
-    void *dst2;   // a second destination (the mirrored heap's view), or null
-    unsigned long long bytes;
-    unsigned long long check;   // seq ^ src ^ dst ^ dst2 ^ bytes ^ kMix
-    unsigned long long pad;
-    alignas(64) unsigned long long done;
-};
-static_assert(sizeof(Mailbox) == 128, "two lines");
-
-// Global-memory views of the operands (their addresses arrive through LDS,
-// which would leave generic flat accesses otherwise).
-template <typename V>
-using gptr = __attribute__((address_space(1))) V *;
-
-// Lane t moves words t, t + 256, ... of the widest word the operands'
-// alignment allows.  (A version that issued all of a lane's loads before its
-// first store, unconditional and clamped, was slower: 2.72 against 2.35 us
-// per 16-byte request, 3.70 against 3.56 at 32 KiB; tools/kernel_variants.hip.)
-typedef unsigned int v4u __attribute__((ext_vector_type(4)));
-
-template <typename V>
-__device__ __forceinline__ void copy_as(const unsigned char *src, unsigned char *dst, unsigned char *dst2,
-                                        unsigned long long bytes) {
-    const gptr<const V> s = (gptr<const V>)(src);
-    const gptr<V> d = (gptr<V>)(dst);
-    const gptr<V> d2 = (gptr<V>)(dst2);
-    const unsigned long long n = bytes / sizeof(V);
-    for (unsigned long long i = threadIdx.x; i < n; i += kSvcBlock) {
-        const V x = s[i];
-        d[i] = x;
-        if (dst2) d2[i] = x;
-    }
-}
-
-// Wave 0 has one read of the mailbox in flight at a time: a read of host
-// memory takes ~1.2 us, so a request waits for the first read that leaves
-// after it was posted (0 to 1.2 us by the phase of the post; tools/kernel_ab.hip
-// gap sweep, profiles/r06_service_lab.txt).  More reads in flight would hold
-// up the copy's loads and stores behind them: the CU's vector memory path
-// returns in order (measured: 7.3 us per 16-byte request with six in flight).
-__global__ __launch_bounds__(kSvcBlock) void service_kernel(Mailbox *mb, unsigned long long served,
-                                                         unsigned long long idle_ticks) {
-    __shared__ unsigned long long s_seq, s_bytes;
-    __shared__ const unsigned char *s_src;
-    __shared__ unsigned char *s_dst, *s_dst2;
-    unsigned long long last = served;
-    unsigned long long t_last = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
-        if (threadIdx.x < 64) {
-            // wave 0: lanes 0-6 read the mailbox's first line in one load
-            // instruction, every lane takes the words from them
-            const unsigned long long *line = reinterpret_cast<const unsigned long long *>(mb);
-            const int lane = threadIdx.x;
-            unsigned long long q = 0;
-            for (;;) {
-                const unsigned long long v =
-                    lane < 7 ? __hip_atomic_load(line + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0;
-                q = __shfl(v, 0);
-                const unsigned long long quit = __shfl(v, 1);
-                if (q != last) {
-                    const unsigned long long a = __shfl(v, 2), b = __shfl(v, 3), b2 = __shfl(v, 4),
-                                             n = __shfl(v, 5), c = __shfl(v, 6);
-                    if ((q ^ a ^ b ^ b2 ^ n ^ kMix) == c) {
-                        if (lane == 0) {
-                            // lines of the source another kernel wrote since
-                            // this one started are dropped (system scope)
-                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-                            s_src = reinterpret_cast<const unsigned char *>(a);
-                            s_dst = reinterpret_cast<unsigned char *>(b);
-                            s_dst2 = reinterpret_cast<unsigned char *>(b2);
-                            s_bytes = n;
-                        }
-                        break;
-                    }
-                    continue;   // torn read: the line again
-                }
-                if (quit || __builtin_amdgcn_s_memrealtime() - t_last > idle_ticks) {
-                    q = 0;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            if (lane == 0) s_seq = q;
-        }
-        __syncthreads();
-        const unsigned long long q = s_seq;
-        if (!q) return;   // idle or told to quit: every wave leaves here
-        const unsigned char *src = s_src;
-        unsigned char *dst = s_dst, *dst2 = s_dst2;
-        const unsigned long long n = s_bytes;
-        const uintptr_t al = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) |
-                             reinterpret_cast<uintptr_t>(dst2) | n;
-        if ((al & 15) == 0) copy_as<v4u>(src, dst, dst2, n);
-        else if ((al & 7) == 0) copy_as<unsigned long long>(src, dst, dst2, n);
-        else if ((al & 3) == 0) copy_as<unsigned>(src, dst, dst2, n);
-        else if ((al & 1) == 0) copy_as<unsigned short>(src, dst, dst2, n);
-        else copy_as<unsigned char>(src, dst, dst2, n);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's stores issued and done
-        __syncthreads();
-        if (threadIdx.x == 0)   // write back, then tell the host
-            __hip_atomic_store(&mb->done, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        last = q;
-        t_last = __builtin_amdgcn_s_memrealtime();
-        __syncthreads();   // the s_* words are read before wave 0 polls again
-    }
-}
-
-}
-namespace B {
-constexpr unsigned long long kMix = 0x9E3779B97F4A7C15ull;
-constexpr unsigned kIdleUs = 200;
+// Waves 0-3 poll the mailbox, waves 4-15 copy.
 constexpr int kSvcBlock = 1024;
+constexpr int kPollWaves = 4;
+constexpr int kCopyThreads = kSvcBlock - 64 * kPollWaves;
+// Poller w reads the mailbox in the time slots w, w + 4, w + 8, ... of
+// kSlot s_memrealtime ticks (10 ns each): a read of host memory takes ~1.2 us,
+// so the four together read it every 0.33 us and stay that far apart.
+constexpr unsigned long long kSlot = 33;
+constexpr unsigned long long kExit = ~0ull;
 
 // Written by the host: the first line (seq last, with release); by the
 // device: the second.
@@ -151,8 +43,8 @@ struct alignas(64) Mailbox {
     void *dst;
     void *dst2;   // a second destination (the mirrored heap's view), or null
     unsigned long long bytes;
-    unsigned long long check;   // seq ^ src ^ dst ^ dst2 ^ bytes ^ kMix
-    unsigned long long pad;
+    unsigned long long check;   // seq ^ src ^ dst ^ dst2 ^ bytes ^ cfg ^ kMix
+    unsigned long long cfg;     // 0: a copy; else a fold of the exchange slots (fold_cfg)
     alignas(64) unsigned long long done;
 };
 static_assert(sizeof(Mailbox) == 128, "two lines");
@@ -162,100 +54,505 @@ static_assert(sizeof(Mailbox) == 128, "two lines");
 template <typename V>
 using gptr = __attribute__((address_space(1))) V *;
 
-// Lane t moves words t, t + 256, ... of the widest word the operands'
+// Copy thread t moves words t, t + 768, ... of the widest word the operands'
 // alignment allows.  (A version that issued all of a lane's loads before its
 // first store, unconditional and clamped, was slower: 2.72 against 2.35 us
 // per 16-byte request, 3.70 against 3.56 at 32 KiB; tools/kernel_variants.hip.)
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
 template <typename V>
-__device__ __forceinline__ void copy_as(const unsigned char *src, unsigned char *dst, unsigned char *dst2,
+__device__ __forceinline__ void copy_as(int t, const unsigned char *src, unsigned char *dst, unsigned char *dst2,
                                         unsigned long long bytes) {
     const gptr<const V> s = (gptr<const V>)(src);
     const gptr<V> d = (gptr<V>)(dst);
     const gptr<V> d2 = (gptr<V>)(dst2);
     const unsigned long long n = bytes / sizeof(V);
-    for (unsigned long long i = threadIdx.x; i < n; i += kSvcBlock) {
+    for (unsigned long long i = t; i < n; i += kCopyThreads) {
         const V x = s[i];
         d[i] = x;
         if (dst2) d2[i] = x;
     }
 }
 
-// Wave 0 has one read of the mailbox in flight at a time: a read of host
-// memory takes ~1.2 us, so a request waits for the first read that leaves
-// after it was posted (0 to 1.2 us by the phase of the post; tools/kernel_ab.hip
-// gap sweep, profiles/r06_service_lab.txt).  More reads in flight would hold
-// up the copy's loads and stores behind them: the CU's vector memory path
-// returns in order (measured: 7.3 us per 16-byte request with six in flight).
-__global__ __launch_bounds__(kSvcBlock) void service_kernel(Mailbox *mb, unsigned long long served,
-                                                         unsigned long long idle_ticks) {
-    __shared__ unsigned long long s_seq, s_bytes;
-    __shared__ const unsigned char *s_src;
-    __shared__ unsigned char *s_dst, *s_dst2;
-    unsigned long long last = served;
-    unsigned long long t_last = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
-        if (threadIdx.x < 64) {
-            // wave 0: lanes 0-6 read the mailbox's first line in one load
-            // instruction, every lane takes the words from them
-            const unsigned long long *line = reinterpret_cast<const unsigned long long *>(mb);
-            const int lane = threadIdx.x;
-            unsigned long long q = 0;
-            for (;;) {
-                const unsigned long long v =
-                    lane < 7 ? __hip_atomic_load(line + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0;
-                q = __shfl(v, 0);
-                const unsigned long long quit = __shfl(v, 1);
-                if (q != last) {
-                    const unsigned long long a = __shfl(v, 2), b = __shfl(v, 3), b2 = __shfl(v, 4),
-                                             n = __shfl(v, 5), c = __shfl(v, 6);
-                    if ((q ^ a ^ b ^ b2 ^ n ^ kMix) == c) {
-                        if (lane == 0) {
-                            // lines of the source another kernel wrote since
-                            // this one started are dropped (system scope)
-                            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-                            s_src = reinterpret_cast<const unsigned char *>(a);
-                            s_dst = reinterpret_cast<unsigned char *>(b);
-                            s_dst2 = reinterpret_cast<unsigned char *>(b2);
-                            s_bytes = n;
-                        }
-                        break;
-                    }
-                    continue;   // torn read: the line again
-                }
-                if (quit || __builtin_amdgcn_s_memrealtime() - t_last > idle_ticks) {
-                    q = 0;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            if (lane == 0) s_seq = q;
+// A fold request: bit 0 set; type, op, the calling PE's own order or
+// PE_start's, and the set (PE_start, logPE_stride, PE_size) with the caller.
+struct FoldCfg {
+    int type, op, own, start, logstride, size, me;
+};
+__host__ __device__ inline unsigned long long pack_cfg(const FoldCfg &f) {
+    return 1ull | (unsigned long long)f.type << 1 | (unsigned long long)f.op << 5 |
+           (unsigned long long)f.own << 8 | (unsigned long long)f.start << 9 |
+           (unsigned long long)f.logstride << 16 | (unsigned long long)f.size << 24 |
+           (unsigned long long)f.me << 32;
+}
+__device__ inline FoldCfg unpack_cfg(unsigned long long c) {
+    return FoldCfg{(int)(c >> 1 & 15), (int)(c >> 5 & 7), (int)(c >> 8 & 1), (int)(c >> 9 & 127),
+                   (int)(c >> 16 & 7), (int)(c >> 24 & 127), (int)(c >> 32 & 127)};
+}
+
+// The j-th input of PE me's fold: its own source first, then the other
+// members in ascending order (reduce-op.c:219-248), or PE_start's order
+// (every member the same bits: the DIRECT / A2A convention).
+__device__ __forceinline__ int member_at(const FoldCfg &f, int j) {
+    if (!f.own) return f.start + (j << f.logstride);
+    const int r = (f.me - f.start) >> f.logstride;
+    if (j == 0) return f.me;
+    return f.start + ((j - 1 < r ? j - 1 : j) << f.logstride);
+}
+
+// Element i of the fold, for copy thread t: up to 8 members' words loaded
+// before the first op (the slots are in host memory: one round trip per 8).
+template <typename T, int OP>
+__device__ void fold_slots(int t, const unsigned char *slots, unsigned char *dst, unsigned char *dst2,
+                           unsigned long long bytes, const FoldCfg &f) {
+    const unsigned long long n = bytes / sizeof(T);
+    for (unsigned long long i = t; i < n; i += kCopyThreads) {
+        T acc{};
+        for (int j0 = 0; j0 < f.size; j0 += 8) {
+            T v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (j0 + u < f.size)
+                    v[u] = reinterpret_cast<const T *>(slots + (size_t)member_at(f, j0 + u) * node::kXchgSlotBytes)[i];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (j0 + u < f.size) acc = j0 + u == 0 ? v[u] : Op<T, OP>::ap(acc, v[u]);
         }
-        __syncthreads();
-        const unsigned long long q = s_seq;
-        if (!q) return;   // idle or told to quit: every wave leaves here
-        const unsigned char *src = s_src;
-        unsigned char *dst = s_dst, *dst2 = s_dst2;
-        const unsigned long long n = s_bytes;
-        const uintptr_t al = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) |
-                             reinterpret_cast<uintptr_t>(dst2) | n;
-        if ((al & 15) == 0) copy_as<v4u>(src, dst, dst2, n);
-        else if ((al & 7) == 0) copy_as<unsigned long long>(src, dst, dst2, n);
-        else if ((al & 3) == 0) copy_as<unsigned>(src, dst, dst2, n);
-        else if ((al & 1) == 0) copy_as<unsigned short>(src, dst, dst2, n);
-        else copy_as<unsigned char>(src, dst, dst2, n);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's stores issued and done
-        __syncthreads();
-        if (threadIdx.x == 0)   // write back, then tell the host
-            __hip_atomic_store(&mb->done, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-        last = q;
-        t_last = __builtin_amdgcn_s_memrealtime();
-        __syncthreads();   // the s_* words are read before wave 0 polls again
+        reinterpret_cast<T *>(dst)[i] = acc;
+        if (dst2) reinterpret_cast<T *>(dst2)[i] = acc;
     }
 }
 
+template <typename T>
+__device__ void fold_int(int t, const unsigned char *sl, unsigned char *d, unsigned char *d2, unsigned long long b,
+                         const FoldCfg &f) {
+    switch (f.op) {
+    case SHMEMX_OP_SUM: fold_slots<T, SHMEMX_OP_SUM>(t, sl, d, d2, b, f); break;
+    case SHMEMX_OP_PROD: fold_slots<T, SHMEMX_OP_PROD>(t, sl, d, d2, b, f); break;
+    case SHMEMX_OP_AND: fold_slots<T, SHMEMX_OP_AND>(t, sl, d, d2, b, f); break;
+    case SHMEMX_OP_OR: fold_slots<T, SHMEMX_OP_OR>(t, sl, d, d2, b, f); break;
+    case SHMEMX_OP_XOR: fold_slots<T, SHMEMX_OP_XOR>(t, sl, d, d2, b, f); break;
+    case SHMEMX_OP_MIN: fold_slots<T, SHMEMX_OP_MIN>(t, sl, d, d2, b, f); break;
+    default: fold_slots<T, SHMEMX_OP_MAX>(t, sl, d, d2, b, f); break;
+    }
 }
+template <typename T>
+__device__ void fold_fp(int t, const unsigned char *sl, unsigned char *d, unsigned char *d2, unsigned long long b,
+                        const FoldCfg &f) {
+    switch (f.op) {
+    case SHMEMX_OP_SUM: fold_slots<T, SHMEMX_OP_SUM>(t, sl, d, d2, b, f); break;
+    case SHMEMX_OP_PROD: fold_slots<T, SHMEMX_OP_PROD>(t, sl, d, d2, b, f); break;
+    case SHMEMX_OP_MIN: fold_slots<T, SHMEMX_OP_MIN>(t, sl, d, d2, b, f); break;
+    default: fold_slots<T, SHMEMX_OP_MAX>(t, sl, d, d2, b, f); break;
+    }
+}
+template <typename T>
+__device__ void fold_cplx(int t, const unsigned char *sl, unsigned char *d, unsigned char *d2,
+                          unsigned long long b, const FoldCfg &f) {
+    if (f.op == SHMEMX_OP_SUM) fold_slots<T, SHMEMX_OP_SUM>(t, sl, d, d2, b, f);
+    else fold_slots<T, SHMEMX_OP_PROD>(t, sl, d, d2, b, f);
+}
+__device__ void fold_request(int t, const unsigned char *sl, unsigned char *d, unsigned char *d2,
+                             unsigned long long b, unsigned long long cfg) {
+    const FoldCfg f = unpack_cfg(cfg);
+    switch (f.type) {
+    case SHMEMX_TYPE_SHORT: fold_int<short>(t, sl, d, d2, b, f); break;
+    case SHMEMX_TYPE_INT: fold_int<int>(t, sl, d, d2, b, f); break;
+    case SHMEMX_TYPE_LONG:
+    case SHMEMX_TYPE_LONGLONG: fold_int<long>(t, sl, d, d2, b, f); break;
+    case SHMEMX_TYPE_FLOAT: fold_fp<float>(t, sl, d, d2, b, f); break;
+    case SHMEMX_TYPE_DOUBLE: fold_fp<double>(t, sl, d, d2, b, f); break;
+    case SHMEMX_TYPE_LONGDOUBLE: fold_fp<ld80>(t, sl, d, d2, b, f); break;
+    case SHMEMX_TYPE_COMPLEXD: fold_cplx<cplxd>(t, sl, d, d2, b, f); break;
+    default: fold_cplx<cplxf>(t, sl, d, d2, b, f); break;
+    }
+}
+
+__device__ __forceinline__ unsigned long long lds_load(const unsigned long long *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_store(unsigned long long *p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ bool lds_cas(unsigned long long *p, unsigned long long expect, unsigned long long v) {
+    return __hip_atomic_compare_exchange_strong(p, &expect, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+typedef unsigned int line_t __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ unsigned long long word(const line_t &v, int k) {
+    return (unsigned long long)v[2 * k + 1] << 32 | v[2 * k];
+}
+
+// The mailbox is read with a scalar load (the whole 64-byte line, past the
+// scalar cache: glc), not a vector one.  A vector read of host memory in
+// flight holds up every later vector access of the CU (its vector memory path
+// returns in order: six reads in flight made a 16-byte request take 7.3 us),
+// so with vector reads one poller could have only one in flight and a
+// request waited up to a whole read for the next one (2.3-3.4 us by the
+// phase of the post, sawtooth).  Scalar reads do not stand in the copy's way:
+// four polling waves, a read each, a quarter of a read apart, take 2.5-2.7 us
+// whatever the phase (tools/kernel_variants.hip, profiles/r06_service_phase.txt).
+// A poller that sees a new request claims it in LDS (compare-and-swap: the
+// others see the same request), drops stale lines (system-scope acquire: it
+// has no vector access in flight, so the wait is free) and hands it to the
+// copy waves; the last copy wave to finish writes back (system-scope release)
+// and stores the sequence number into the host's done line.  Leaving: poller
+// 0 swaps the claim word to kExit once no copy is pending (a claim and the
+// exit cannot both win), every poller then leaves, and the copy waves on
+// s_req = kExit.  A request that lost to the exit is served by the host's
+// relaunch (service_copy).
+__global__ __launch_bounds__(kSvcBlock) void service_kernel(Mailbox *mb, unsigned long long served,
+                                                         unsigned long long idle_ticks) {
+    __shared__ unsigned long long s_claim, s_req, s_done, s_count, s_bytes, s_cfg;
+    __shared__ const unsigned char *s_src;
+    __shared__ unsigned char *s_dst, *s_dst2;
+    if (threadIdx.x == 0) {
+        s_claim = s_req = s_done = served;
+        s_count = 0;
+    }
+    __syncthreads();
+    const int wave = threadIdx.x >> 6;
+    if (wave < kPollWaves) {
+        unsigned long long last = served;
+        unsigned long long t_last = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            while (((__builtin_amdgcn_s_memrealtime() / kSlot) & (kPollWaves - 1)) != (unsigned)wave)
+                __builtin_amdgcn_s_sleep(1);
+            line_t v;
+            asm volatile("s_load_dwordx16 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(mb) : "memory");
+            const unsigned long long q = word(v, 0);
+            const unsigned long long claim = lds_load(&s_claim);
+            if (claim == kExit) break;
+            if (q != last) {
+                const unsigned long long a = word(v, 2), b = word(v, 3), b2 = word(v, 4), n = word(v, 5),
+                                         c = word(v, 6), g = word(v, 7);
+                if ((q ^ a ^ b ^ b2 ^ n ^ g ^ kMix) == c) {   // else a torn read: the next one
+                    last = q;
+                    t_last = __builtin_amdgcn_s_memrealtime();
+                    if (claim != q && lds_cas(&s_claim, claim, q)) {
+                        s_src = reinterpret_cast<const unsigned char *>(a);
+                        s_dst = reinterpret_cast<unsigned char *>(b);
+                        s_dst2 = reinterpret_cast<unsigned char *>(b2);
+                        s_bytes = n;
+                        s_cfg = g;
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // lines written since: dropped
+                        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                        lds_store(&s_req, q);
+                    }
+                    continue;
+                }
+            }
+            if (claim != last) {   // another poller's request
+                last = claim;
+                t_last = __builtin_amdgcn_s_memrealtime();
+            }
+            if (wave == 0 && (word(v, 1) || __builtin_amdgcn_s_memrealtime() - t_last > idle_ticks) &&
+                lds_load(&s_done) == claim && lds_cas(&s_claim, claim, kExit)) {
+                lds_store(&s_req, kExit);
+                break;
+            }
+        }
+        return;
+    }
+    const int t = threadIdx.x - 64 * kPollWaves;
+    unsigned long long seen = served;
+    for (;;) {
+        unsigned long long q;
+        while ((q = lds_load(&s_req)) == seen) __builtin_amdgcn_s_sleep(1);
+        if (q == kExit) return;
+        seen = q;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const unsigned char *src = s_src;
+        unsigned char *dst = s_dst, *dst2 = s_dst2;
+        const unsigned long long n = s_bytes, cfg = s_cfg;
+        const uintptr_t al = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) |
+                             reinterpret_cast<uintptr_t>(dst2) | n;
+        if (cfg) fold_request(t, src, dst, dst2, n, cfg);
+        else if ((al & 15) == 0) copy_as<v4u>(t, src, dst, dst2, n);
+        else if ((al & 7) == 0) copy_as<unsigned long long>(t, src, dst, dst2, n);
+        else if ((al & 3) == 0) copy_as<unsigned>(t, src, dst, dst2, n);
+        else if ((al & 1) == 0) copy_as<unsigned short>(t, src, dst, dst2, n);
+        else copy_as<unsigned char>(t, src, dst, dst2, n);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores have landed
+        if (threadIdx.x % 64 == 0 &&
+            __hip_atomic_fetch_add(&s_count, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ==
+                kCopyThreads / 64 - 1) {
+            // the last copy wave: write back, then tell the host
+            lds_store(&s_count, 0);
+            __hip_atomic_store(&mb->done, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            lds_store(&s_done, q);
+        }
+    }
+}
+
+} }
+namespace shmx { namespace B {
+constexpr unsigned long long kMix = 0x9E3779B97F4A7C15ull;
+constexpr unsigned kIdleUs = 200;
+// Waves 0-3 poll the mailbox, waves 4-15 copy.
+constexpr int kSvcBlock = 1024;
+constexpr int kPollWaves = 4;
+constexpr int kCopyThreads = kSvcBlock - 64 * kPollWaves;
+// Poller w reads the mailbox in the time slots w, w + 4, w + 8, ... of
+// kSlot s_memrealtime ticks (10 ns each): a read of host memory takes ~1.2 us,
+// so the four together read it every 0.33 us and stay that far apart.
+constexpr unsigned long long kSlot = 33;
+constexpr unsigned long long kExit = ~0ull;
+
+// Written by the host: the first line (seq last, with release); by the
+// device: the second.
+struct alignas(64) Mailbox {
+    unsigned long long seq;
+    unsigned long long quit;
+    const void *src;
+    void *dst;
+    void *dst2;   // a second destination (the mirrored heap's view), or null
+    unsigned long long bytes;
+    unsigned long long check;   // seq ^ src ^ dst ^ dst2 ^ bytes ^ cfg ^ kMix
+    unsigned long long cfg;     // 0: a copy; else a fold of the exchange slots (fold_cfg)
+    alignas(64) unsigned long long done;
+};
+static_assert(sizeof(Mailbox) == 128, "two lines");
+
+// Global-memory views of the operands (their addresses arrive through LDS,
+// which would leave generic flat accesses otherwise).
+template <typename V>
+using gptr = __attribute__((address_space(1))) V *;
+
+// Copy thread t moves words t, t + 768, ... of the widest word the operands'
+// alignment allows.  (A version that issued all of a lane's loads before its
+// first store, unconditional and clamped, was slower: 2.72 against 2.35 us
+// per 16-byte request, 3.70 against 3.56 at 32 KiB; tools/kernel_variants.hip.)
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+template <typename V>
+__device__ __forceinline__ void copy_as(int t, const unsigned char *src, unsigned char *dst, unsigned char *dst2,
+                                        unsigned long long bytes) {
+    const gptr<const V> s = (gptr<const V>)(src);
+    const gptr<V> d = (gptr<V>)(dst);
+    const gptr<V> d2 = (gptr<V>)(dst2);
+    const unsigned long long n = bytes / sizeof(V);
+    for (unsigned long long i = t; i < n; i += kCopyThreads) {
+        const V x = s[i];
+        d[i] = x;
+        if (dst2) d2[i] = x;
+    }
+}
+
+// A fold request: bit 0 set; type, op, the calling PE's own order or
+// PE_start's, and the set (PE_start, logPE_stride, PE_size) with the caller.
+struct FoldCfg {
+    int type, op, own, start, logstride, size, me;
+};
+__host__ __device__ inline unsigned long long pack_cfg(const FoldCfg &f) {
+    return 1ull | (unsigned long long)f.type << 1 | (unsigned long long)f.op << 5 |
+           (unsigned long long)f.own << 8 | (unsigned long long)f.start << 9 |
+           (unsigned long long)f.logstride << 16 | (unsigned long long)f.size << 24 |
+           (unsigned long long)f.me << 32;
+}
+__device__ inline FoldCfg unpack_cfg(unsigned long long c) {
+    return FoldCfg{(int)(c >> 1 & 15), (int)(c >> 5 & 7), (int)(c >> 8 & 1), (int)(c >> 9 & 127),
+                   (int)(c >> 16 & 7), (int)(c >> 24 & 127), (int)(c >> 32 & 127)};
+}
+
+// The j-th input of PE me's fold: its own source first, then the other
+// members in ascending order (reduce-op.c:219-248), or PE_start's order
+// (every member the same bits: the DIRECT / A2A convention).
+__device__ __forceinline__ int member_at(const FoldCfg &f, int j) {
+    if (!f.own) return f.start + (j << f.logstride);
+    const int r = (f.me - f.start) >> f.logstride;
+    if (j == 0) return f.me;
+    return f.start + ((j - 1 < r ? j - 1 : j) << f.logstride);
+}
+
+// Element i of the fold, for copy thread t: up to 8 members' words loaded
+// before the first op (the slots are in host memory: one round trip per 8).
+template <typename T, int OP>
+__device__ void fold_slots(int t, const unsigned char *slots, unsigned char *dst, unsigned char *dst2,
+                           unsigned long long bytes, const FoldCfg &f) {
+    const unsigned long long n = bytes / sizeof(T);
+    for (unsigned long long i = t; i < n; i += kCopyThreads) {
+        T acc{};
+        for (int j0 = 0; j0 < f.size; j0 += 8) {
+            T v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (j0 + u < f.size)
+                    v[u] = reinterpret_cast<const T *>(slots + (size_t)member_at(f, j0 + u) * node::kXchgSlotBytes)[i];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (j0 + u < f.size) acc = j0 + u == 0 ? v[u] : Op<T, OP>::ap(acc, v[u]);
+        }
+        reinterpret_cast<T *>(dst)[i] = acc;
+        if (dst2) reinterpret_cast<T *>(dst2)[i] = acc;
+    }
+}
+
+template <typename T>
+__device__ void fold_int(int t, const unsigned char *sl, unsigned char *d, unsigned char *d2, unsigned long long b,
+                         const FoldCfg &f) {
+    switch (f.op) {
+    case SHMEMX_OP_SUM: fold_slots<T, SHMEMX_OP_SUM>(t, sl, d, d2, b, f); break;
+    case SHMEMX_OP_PROD: fold_slots<T, SHMEMX_OP_PROD>(t, sl, d, d2, b, f); break;
+    case SHMEMX_OP_AND: fold_slots<T, SHMEMX_OP_AND>(t, sl, d, d2, b, f); break;
+    case SHMEMX_OP_OR: fold_slots<T, SHMEMX_OP_OR>(t, sl, d, d2, b, f); break;
+    case SHMEMX_OP_XOR: fold_slots<T, SHMEMX_OP_XOR>(t, sl, d, d2, b, f); break;
+    case SHMEMX_OP_MIN: fold_slots<T, SHMEMX_OP_MIN>(t, sl, d, d2, b, f); break;
+    default: fold_slots<T, SHMEMX_OP_MAX>(t, sl, d, d2, b, f); break;
+    }
+}
+template <typename T>
+__device__ void fold_fp(int t, const unsigned char *sl, unsigned char *d, unsigned char *d2, unsigned long long b,
+                        const FoldCfg &f) {
+    switch (f.op) {
+    case SHMEMX_OP_SUM: fold_slots<T, SHMEMX_OP_SUM>(t, sl, d, d2, b, f); break;
+    case SHMEMX_OP_PROD: fold_slots<T, SHMEMX_OP_PROD>(t, sl, d, d2, b, f); break;
+    case SHMEMX_OP_MIN: fold_slots<T, SHMEMX_OP_MIN>(t, sl, d, d2, b, f); break;
+    default: fold_slots<T, SHMEMX_OP_MAX>(t, sl, d, d2, b, f); break;
+    }
+}
+template <typename T>
+__device__ void fold_cplx(int t, const unsigned char *sl, unsigned char *d, unsigned char *d2,
+                          unsigned long long b, const FoldCfg &f) {
+    if (f.op == SHMEMX_OP_SUM) fold_slots<T, SHMEMX_OP_SUM>(t, sl, d, d2, b, f);
+    else fold_slots<T, SHMEMX_OP_PROD>(t, sl, d, d2, b, f);
+}
+__device__ __attribute__((noinline)) void fold_request(int t, const unsigned char *sl, unsigned char *d, unsigned char *d2,
+                             unsigned long long b, unsigned long long cfg) {
+    const FoldCfg f = unpack_cfg(cfg);
+    switch (f.type) {
+    case SHMEMX_TYPE_SHORT: fold_int<short>(t, sl, d, d2, b, f); break;
+    case SHMEMX_TYPE_INT: fold_int<int>(t, sl, d, d2, b, f); break;
+    case SHMEMX_TYPE_LONG:
+    case SHMEMX_TYPE_LONGLONG: fold_int<long>(t, sl, d, d2, b, f); break;
+    case SHMEMX_TYPE_FLOAT: fold_fp<float>(t, sl, d, d2, b, f); break;
+    case SHMEMX_TYPE_DOUBLE: fold_fp<double>(t, sl, d, d2, b, f); break;
+    case SHMEMX_TYPE_LONGDOUBLE: fold_fp<ld80>(t, sl, d, d2, b, f); break;
+    case SHMEMX_TYPE_COMPLEXD: fold_cplx<cplxd>(t, sl, d, d2, b, f); break;
+    default: fold_cplx<cplxf>(t, sl, d, d2, b, f); break;
+    }
+}
+
+__device__ __forceinline__ unsigned long long lds_load(const unsigned long long *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_store(unsigned long long *p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ bool lds_cas(unsigned long long *p, unsigned long long expect, unsigned long long v) {
+    return __hip_atomic_compare_exchange_strong(p, &expect, v, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+typedef unsigned int line_t __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ unsigned long long word(const line_t &v, int k) {
+    return (unsigned long long)v[2 * k + 1] << 32 | v[2 * k];
+}
+
+// The mailbox is read with a scalar load (the whole 64-byte line, past the
+// scalar cache: glc), not a vector one.  A vector read of host memory in
+// flight holds up every later vector access of the CU (its vector memory path
+// returns in order: six reads in flight made a 16-byte request take 7.3 us),
+// so with vector reads one poller could have only one in flight and a
+// request waited up to a whole read for the next one (2.3-3.4 us by the
+// phase of the post, sawtooth).  Scalar reads do not stand in the copy's way:
+// four polling waves, a read each, a quarter of a read apart, take 2.5-2.7 us
+// whatever the phase (tools/kernel_variants.hip, profiles/r06_service_phase.txt).
+// A poller that sees a new request claims it in LDS (compare-and-swap: the
+// others see the same request), drops stale lines (system-scope acquire: it
+// has no vector access in flight, so the wait is free) and hands it to the
+// copy waves; the last copy wave to finish writes back (system-scope release)
+// and stores the sequence number into the host's done line.  Leaving: poller
+// 0 swaps the claim word to kExit once no copy is pending (a claim and the
+// exit cannot both win), every poller then leaves, and the copy waves on
+// s_req = kExit.  A request that lost to the exit is served by the host's
+// relaunch (service_copy).
+__global__ __launch_bounds__(kSvcBlock) void service_kernel(Mailbox *mb, unsigned long long served,
+                                                         unsigned long long idle_ticks) {
+    __shared__ unsigned long long s_claim, s_req, s_done, s_count, s_bytes, s_cfg;
+    __shared__ const unsigned char *s_src;
+    __shared__ unsigned char *s_dst, *s_dst2;
+    if (threadIdx.x == 0) {
+        s_claim = s_req = s_done = served;
+        s_count = 0;
+    }
+    __syncthreads();
+    const int wave = threadIdx.x >> 6;
+    if (wave < kPollWaves) {
+        unsigned long long last = served;
+        unsigned long long t_last = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            while (((__builtin_amdgcn_s_memrealtime() / kSlot) & (kPollWaves - 1)) != (unsigned)wave)
+                __builtin_amdgcn_s_sleep(1);
+            line_t v;
+            asm volatile("s_load_dwordx16 %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(mb) : "memory");
+            const unsigned long long q = word(v, 0);
+            const unsigned long long claim = lds_load(&s_claim);
+            if (claim == kExit) break;
+            if (q != last) {
+                const unsigned long long a = word(v, 2), b = word(v, 3), b2 = word(v, 4), n = word(v, 5),
+                                         c = word(v, 6), g = word(v, 7);
+                if ((q ^ a ^ b ^ b2 ^ n ^ g ^ kMix) == c) {   // else a torn read: the next one
+                    last = q;
+                    t_last = __builtin_amdgcn_s_memrealtime();
+                    if (claim != q && lds_cas(&s_claim, claim, q)) {
+                        s_src = reinterpret_cast<const unsigned char *>(a);
+                        s_dst = reinterpret_cast<unsigned char *>(b);
+                        s_dst2 = reinterpret_cast<unsigned char *>(b2);
+                        s_bytes = n;
+                        s_cfg = g;
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // lines written since: dropped
+                        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                        lds_store(&s_req, q);
+                    }
+                    continue;
+                }
+            }
+            if (claim != last) {   // another poller's request
+                last = claim;
+                t_last = __builtin_amdgcn_s_memrealtime();
+            }
+            if (wave == 0 && (word(v, 1) || __builtin_amdgcn_s_memrealtime() - t_last > idle_ticks) &&
+                lds_load(&s_done) == claim && lds_cas(&s_claim, claim, kExit)) {
+                lds_store(&s_req, kExit);
+                break;
+            }
+        }
+        return;
+    }
+    const int t = threadIdx.x - 64 * kPollWaves;
+    unsigned long long seen = served;
+    for (;;) {
+        unsigned long long q;
+        while ((q = lds_load(&s_req)) == seen) __builtin_amdgcn_s_sleep(1);
+        if (q == kExit) return;
+        seen = q;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const unsigned char *src = s_src;
+        unsigned char *dst = s_dst, *dst2 = s_dst2;
+        const unsigned long long n = s_bytes, cfg = s_cfg;
+        const uintptr_t al = reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst) |
+                             reinterpret_cast<uintptr_t>(dst2) | n;
+        if (cfg) fold_request(t, src, dst, dst2, n, cfg);
+        else if ((al & 15) == 0) copy_as<v4u>(t, src, dst, dst2, n);
+        else if ((al & 7) == 0) copy_as<unsigned long long>(t, src, dst, dst2, n);
+        else if ((al & 3) == 0) copy_as<unsigned>(t, src, dst, dst2, n);
+        else if ((al & 1) == 0) copy_as<unsigned short>(t, src, dst, dst2, n);
+        else copy_as<unsigned char>(t, src, dst, dst2, n);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's stores have landed
+        if (threadIdx.x % 64 == 0 &&
+            __hip_atomic_fetch_add(&s_count, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ==
+                kCopyThreads / 64 - 1) {
+            // the last copy wave: write back, then tell the host
+            lds_store(&s_count, 0);
+            __hip_atomic_store(&mb->done, q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            lds_store(&s_done, q);
+        }
+    }
+}
+
+} }
 namespace C {
 constexpr unsigned long long kMix = 0x9E3779B97F4A7C15ull;
 constexpr unsigned kIdleUs = 200;
@@ -778,7 +1075,7 @@ int main(int argc, char **argv) {
         hipLaunchKernelGGL(NS::service_kernel, dim3(1), dim3(NS::kSvcBlock), 0, svc, mb, 0ull, 20000000ull); \
         bench(#NS, mb, svc, reps, [&](NS::Mailbox *m, unsigned long long q) { m->src = src; m->dst = tgt; m->dst2 = nullptr; m->bytes = bytes; \
             m->check = q ^ (uintptr_t)src ^ (uintptr_t)tgt ^ bytes ^ NS::kMix; __atomic_store_n(&m->seq, q, __ATOMIC_RELEASE); }); }
-        RUN_LIB(A) RUN_LIB(D) RUN_LIB(G)
+        RUN_LIB(shmx::A) RUN_LIB(shmx::B) RUN_LIB(G)
         { LabMailbox *mb; (void)hipHostMalloc((void **)&mb, sizeof *mb, hipHostMallocCoherent); std::memset(mb, 0, sizeof *mb);
           hipLaunchKernelGGL(service_kernel<true>, dim3(1), dim3(256), 0, svc, mb, 0ull, 20000000ull);
           bench("lab", mb, svc, reps, [&](LabMailbox *m, unsigned long long q) { m->src = src; m->dst = tgt; m->bytes = bytes;
