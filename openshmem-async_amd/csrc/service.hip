@@ -134,26 +134,42 @@ __device__ __forceinline__ int member_at(const FoldCfg &f, int j) {
     return f.start + ((j - 1 < r ? j - 1 : j) << f.logstride);
 }
 
-// Element i of the fold, for copy thread t: up to 8 members' words loaded
-// before the first op (the slots are in host memory: one round trip per 8).
+// The fold, for copy thread t: 16-byte word w of every member's slot (the
+// slots are 4 KiB-aligned, in host memory), up to 8 members' words loaded
+// before the first op, so a 4 KiB slot is one round trip over PCIe (768
+// threads, 256 words); the word's elements folded in the member order, then
+// stored element by element (the target's alignment is the caller's).
 template <typename T, int OP>
 __device__ void fold_slots(int t, const unsigned char *slots, unsigned char *dst, unsigned char *dst2,
                            unsigned long long bytes, const FoldCfg &f) {
-    const unsigned long long n = bytes / sizeof(T);
-    for (unsigned long long i = t; i < n; i += kCopyThreads) {
-        T acc{};
+    constexpr int E = 16 / sizeof(T);
+    static_assert(E >= 1 && E * sizeof(T) == 16, "whole elements per 16-byte word");
+    const unsigned long long n = bytes / sizeof(T), nw = (n + E - 1) / E;
+    for (unsigned long long w = t; w < nw; w += kCopyThreads) {
+        T acc[E];
         for (int j0 = 0; j0 < f.size; j0 += 8) {
-            T v[8];
+            v4u v[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u)
                 if (j0 + u < f.size)
-                    v[u] = reinterpret_cast<const T *>(slots + (size_t)member_at(f, j0 + u) * node::kXchgSlotBytes)[i];
+                    v[u] = reinterpret_cast<const v4u *>(slots + (size_t)member_at(f, j0 + u) * node::kXchgSlotBytes)[w];
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (j0 + u < f.size) acc = j0 + u == 0 ? v[u] : Op<T, OP>::ap(acc, v[u]);
+            for (int u = 0; u < 8; ++u) {
+                if (j0 + u >= f.size) break;
+                T x[E];
+                __builtin_memcpy(x, &v[u], 16);
+#pragma unroll
+                for (int e = 0; e < E; ++e) acc[e] = j0 + u == 0 ? x[e] : Op<T, OP>::ap(acc[e], x[e]);
+            }
         }
-        reinterpret_cast<T *>(dst)[i] = acc;
-        if (dst2) reinterpret_cast<T *>(dst2)[i] = acc;
+        const unsigned long long e0 = w * E;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            if (e0 + e < n) {
+                reinterpret_cast<T *>(dst)[e0 + e] = acc[e];
+                if (dst2) reinterpret_cast<T *>(dst2)[e0 + e] = acc[e];
+            }
+        }
     }
 }
 
