@@ -414,6 +414,14 @@ static void reduce_blocking_impl(int type, int op, void *target, const void *sou
 // 0.26 us: profiles/r04_isx_mirror.txt).
 static size_t mirror_settle_limit() { return kSmallHostBytes; }
 
+// Whether a blocking call of `bytes` per PE over several PEs takes the
+// exchange: every member decides alike (the same size and settings;
+// g_state.xchg was agreed at init).
+static bool xchg_eligible(size_t bytes) {
+    return bytes <= node::kXchgSlotBytes && g_state.xchg && g_state.algo == SHMEMX_ALGO_AUTO &&
+           !g_state.force_collective && service_available();
+}
+
 // The blocking entry point body: host- or device-resident arrays.  Operands
 // in the mirrored heap's host view run on their HBM twins (heap.h).
 void reduce_blocking(int type, int op, void *target, const void *source,
@@ -445,12 +453,20 @@ void reduce_blocking(int type, int op, void *target, const void *source,
             // twin first (its blocks keep their state: a HOST_NEWER block is
             // flushed whole by the next call that needs it in HBM).  ISx's
             // nreduce = 1 round: profiles/r05_isx_mirror.txt.
-            const void *cur = light && size == 1 && !g_state.force_collective && bytes <= kSmallHostBytes
+            // A small call over several PEs through the exchange (xchg_reduce)
+            // on the same terms: the view's current bytes go into this PE's
+            // exchange slot by a CPU copy, and the source's HBM twin, neither
+            // flushed nor read, keeps its blocks' state.
+            const bool xchg = size > 1 && xchg_eligible(bytes);
+            const void *cur = light && (size == 1 || xchg) && !g_state.force_collective && bytes <= kSmallHostBytes
                                   ? heap::current_host_bytes(source, bytes) : nullptr;
             const void *s = nullptr;
-            if (cur && small_bounce_reserve()) {
+            if (cur && size == 1 && small_bounce_reserve()) {
                 std::memcpy(g_state.bounce, cur, bytes);
                 s = g_state.bounce;
+            } else if (cur && xchg) {
+                g_state.xchg_src_host = cur;
+                s = heap::twin(source);
             } else {
                 s = light ? heap::device_operand_bytes(source, bytes) : heap::device_operand(source, bytes);
             }
@@ -468,6 +484,7 @@ void reduce_blocking(int type, int op, void *target, const void *source,
             g_state.settle_dst = dst;
             g_state.settled = false;
             reduce_blocking_impl(type, op, t.ptr(), s, nreduce, start, logstride, size, false);
+            g_state.xchg_src_host = nullptr;
             const bool copied = g_state.settled;
             g_state.settle_dst = nullptr;
             g_state.settled = false;
@@ -519,7 +536,9 @@ static void xchg_reduce(int type, int op, void *target, bool tdev, const void *s
               bytes / type_size(type), start, logstride, size, own_order_pair(type, op) ? " (own order)" : "");
     if (!tdev && !small_bounce_reserve())
         fatal("small multi-PE call", "no page-locked bounce buffer for a host target");
-    if (sdev) {
+    if (g_state.xchg_src_host) {   // a mirrored-heap source's current view bytes
+        std::memcpy(node::xchg_host(g_state.pe), g_state.xchg_src_host, bytes);
+    } else if (sdev) {
         if (!service_copy(node::xchg_dev(g_state.pe), nullptr, source, bytes))
             fatal("small multi-PE call", "the service workgroup did not take the source");
     } else {
@@ -585,8 +604,7 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
     // A small call over several PEs under auto: through the exchange and the
     // service workgroups (xchg_reduce).  Every member decides alike: the
     // same size, set and settings, and g_state.xchg was agreed at init.
-    if (size > 1 && bytes <= node::kXchgSlotBytes && g_state.xchg && g_state.algo == SHMEMX_ALGO_AUTO &&
-        !g_state.force_collective && service_available()) {
+    if (size > 1 && xchg_eligible(bytes)) {
         xchg_reduce(type, op, target, tdev, source, sdev, bytes, start, logstride, size);
         return;
     }

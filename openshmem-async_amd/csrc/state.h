@@ -33,6 +33,9 @@ struct State {
     // per-process state, so every PE plans alike.
     bool node_shared = false;
     bool xchg = false;   // every PE mapped the small-call exchange (node.h), agreed at init
+    // a mirrored-heap source's current host-view bytes, for the exchange
+    // (staging.cpp reduce_blocking; its HBM twin is not flushed)
+    const void *xchg_src_host = nullptr;
     // the heap segment registered with the RCCL communicator
     // (shmemx_rccl_register_heap), or nullptr
     void *rccl_reg = nullptr;

@@ -725,6 +725,19 @@ elif scenario == "xchg":
     extra["folds"] = shm.service_stats(reset=True)["folds"]
     if npes > 1 and not extra["folds"]:
         fails.append("no small multi-PE call was folded by the service workgroup")
+    # configs[0]'s call (int sum, n = 1024, PEs 0-1) timed from C on this
+    # heap (on the mirrored heap: host-written view addresses), for the log
+    if npes >= 2 and pe < 2:
+        sys.path.insert(0, os.path.dirname(HERE))
+        import bench  # noqa: E402  (call_times_us: the C call timer)
+        vals = (np.arange(1024, dtype=np.int32) * 3 + pe).astype(np.int32)
+        if MIRRORED:
+            host_view(HEAP_SRC, np.int32, 1024)[:] = vals
+        else:
+            heap_write(HEAP_SRC, vals, vals.nbytes)
+        ts = bench.call_times_us("int", "sum", HEAP_TGT, HEAP_SRC, 1024, 0, 0, 2, np.full(128, -1, np.int64), 20, 300)
+        if ts:
+            extra["config0_c_us"] = round(float(np.median(ts)), 2)
 elif scenario == "config0":
     # BASELINE.json configs[0]: shmem_int_sum_to_all, nreduce = 1024, on 2 PEs
     # (the reference's "oshrun loopback"), through the C entry point itself

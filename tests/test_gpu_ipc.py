@@ -185,6 +185,7 @@ def test_small_multi_pe_calls_through_the_service_exchange(tmp_path, transport, 
         assert r["ncases"] > 0
         assert not r["fails"], f"PE {r['pe']}: {r['fails'][:10]}"
         assert r["folds"] > 0
+    print("configs[0] call from C, us per PE:", [r.get("config0_c_us") for r in reports if r["pe"] < 2])
 
 
 @pytest.mark.gpu
