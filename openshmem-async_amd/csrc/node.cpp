@@ -32,6 +32,7 @@ struct PeSlot {
     Desc desc;
     std::atomic<int> vote;       // agree()
     std::atomic<int> gpu_numa;   // the GPU's NUMA node + 1 (0 = unknown)
+    std::atomic<uint64_t> gpu_id;   // a hash of the GPU's PCI bus id (0 = unknown)
 };
 
 struct Shared {
@@ -318,6 +319,19 @@ Desc get_desc(int q) {
 
 void put_gpu_numa(int nd) {
     if (g_node.sh) g_node.sh->pe[g_node.pe].gpu_numa.store(nd < 0 ? 0 : nd + 1, std::memory_order_release);
+}
+
+void put_gpu_id(uint64_t id) {
+    if (g_node.sh) g_node.sh->pe[g_node.pe].gpu_id.store(id, std::memory_order_release);
+}
+
+bool gpu_shared() {
+    if (!g_node.sh) return false;
+    const uint64_t mine = g_node.sh->pe[g_node.pe].gpu_id.load(std::memory_order_acquire);
+    if (!mine) return false;
+    for (int q = 0; q < g_node.npes; ++q)
+        if (q != g_node.pe && g_node.sh->pe[q].gpu_id.load(std::memory_order_acquire) == mine) return true;
+    return false;
 }
 
 int gpu_numa(int q) {

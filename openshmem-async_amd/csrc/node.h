@@ -90,6 +90,11 @@ Desc get_desc(int pe);
 // a NUMA node take different cache domains (staging.cpp).
 void put_gpu_numa(int node);
 int gpu_numa(int pe);
+// A hash of this PE's GPU's PCI bus id, published with the NUMA node; after
+// init's barrier gpu_shared() says whether another PE process of the job
+// uses the same GPU (tests and rehearsals put several on one).
+void put_gpu_id(uint64_t id);
+bool gpu_shared();
 int npes();   // PEs attached to the block (0 if it is down)
 
 }  // namespace node

@@ -248,6 +248,7 @@ static int init_locked(int pe, int npes, int device, const void *uid) {
     g_state.ipc_only = ipc_transport_env();
     g_state.node_shared = false;
     g_state.xchg = false;
+    g_state.gpu_shared = false;
     if (npes > 1 || g_state.force_collective) {
         ncclUniqueId id;
         if (npes > 1) {
@@ -283,10 +284,22 @@ static int init_locked(int pe, int npes, int device, const void *uid) {
         // then, so a job that dies leaves nothing in /dev/shm.
         if (attached) {
             node::put_gpu_numa(gpu_numa_node(device));   // (staging.cpp's copy threads)
+            {
+                char bus[64] = {0};
+                uint64_t id = 0;
+                if (hipDeviceGetPCIBusId(bus, sizeof bus, device) == hipSuccess) {
+                    id = 1469598103934665603ull;   // FNV-1a, never 0 for a real id
+                    for (const char *c = bus; *c; ++c) id = (id ^ (unsigned char)*c) * 1099511628211ull;
+                } else {
+                    (void)hipGetLastError();
+                }
+                node::put_gpu_id(id);
+            }
             const bool xchg = npes > 1 && node::xchg_attach();   // (opened before the names go)
             node::barrier(0, 1, npes);
             if (pe == 0) node::unlink_name();
             g_state.xchg = npes > 1 && node::agree(0, 1, npes, xchg);
+            g_state.gpu_shared = node::gpu_shared();
         }
     }
     g_state.pe = pe;
@@ -993,6 +1006,7 @@ void pshmem_finalize(void) {
     g_state.stream = nullptr;
     g_state.node_shared = false;
     g_state.xchg = false;
+    g_state.gpu_shared = false;
     g_state.inited = false;
 }
 

@@ -352,12 +352,21 @@ struct Service {
     unsigned long long ns_before_post = 0, ns_round_trip = 0;
 } g_svc;
 
+// $SHMEMX_SERVICE: 0 off, 1 on; unset: on unless another PE process of the
+// job shares this GPU.  Several PE processes' resident workgroups on one GPU
+// made every other kernel and copy of those processes several times slower
+// (8 ranks on one MI355X: the host-resident call 91 -> 672 ms, the small-call
+// timings minutes long; profiles/r06_bench_rehearsal_ipc_n8_b.json against
+// SHMEMX_SERVICE=0), most likely because the GPU time-slices the processes'
+// queues and a queue whose kernel never ends is switched out and back with
+// its waves saved and restored.  One PE per GPU, the deployment this path is
+// for, showed nothing of the kind.
 bool enabled() {
-    static const bool on = [] {
+    static const int env = [] {
         const char *e = std::getenv("SHMEMX_SERVICE");
-        return !(e && *e == '0');
+        return e && *e == '0' ? 0 : e && *e == '1' ? 1 : -1;
     }();
-    return on;
+    return env == 1 || (env < 0 && !g_state.gpu_shared);
 }
 
 void at_exit() { service_release(); }

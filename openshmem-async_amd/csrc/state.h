@@ -33,6 +33,9 @@ struct State {
     // per-process state, so every PE plans alike.
     bool node_shared = false;
     bool xchg = false;   // every PE mapped the small-call exchange (node.h), agreed at init
+    // another PE process of the job uses this GPU (node::gpu_shared): the
+    // service workgroup stays off unless $SHMEMX_SERVICE=1 (service.hip)
+    bool gpu_shared = false;
     // a mirrored-heap source's current host-view bytes, for the exchange
     // (staging.cpp reduce_blocking; its HBM twin is not flushed)
     const void *xchg_src_host = nullptr;

@@ -1008,6 +1008,7 @@ elif scenario == "mirrored":
     # into the view by the call, on every PE
     s8, t8 = shm.malloc(8), shm.malloc(8)
     sv, tv = host_view(s8, np.int64, 1), host_view(t8, np.int64, 1)
+    shm.service_stats(reset=True)
     for r in range(21):
         if r == 1:
             shm.mirror_stats(reset=True)
@@ -1022,9 +1023,10 @@ elif scenario == "mirrored":
     # (one PE: PE_size 1, a copy: the source goes through the coherent bounce
     # buffer; several PEs: through the exchange, by a CPU copy from the view
     # into the PE's slot; either way nothing is flushed and the source's block
-    # stays HOST_NEWER.  Without the service workgroup the source's bytes are
+    # stays HOST_NEWER.  Without the service workgroup — off by default when,
+    # as here, several PE processes share the GPU — the source's bytes are
     # flushed to its HBM twin every round.)
-    no_flush = npes == 1 or os.environ.get("SHMEMX_SERVICE") != "0"
+    no_flush = npes == 1 or shm.service_stats(reset=True)["folds"] > 0
     flushed_ok = st["blocks_flushed"] == 0 if no_flush else st["blocks_flushed"] >= 20
     if (st["write_faults"] or st["read_faults"] or st["blocks_device_newer"] or st["blocks_fetched"]
             or st["blocks_settled"] < 20 or not flushed_ok):

@@ -177,7 +177,9 @@ def test_small_multi_pe_calls_through_the_service_exchange(tmp_path, transport, 
     in-place operands, own-order pairs on NaN / +-0 sources; every PE against
     the oracle (its own order where that decides the answer, else
     PE_start's), and the folds are counted, so the path is the one that ran."""
-    env = {"SHMEMX_TRANSPORT": transport, "SHMEMX_HEAP_MEMORY": heap}
+    # (SHMEMX_SERVICE=1: the PE processes share the one GPU here, where the
+    # service workgroup is otherwise off)
+    env = {"SHMEMX_TRANSPORT": transport, "SHMEMX_HEAP_MEMORY": heap, "SHMEMX_SERVICE": "1"}
     if transport == "rccl":
         env["FAKE_RCCL"] = os.path.join(HERE, "native", "libfake_rccl.so")
     reports = run_pes(tmp_path, npes, "xchg", env, timeout=300)
