@@ -52,8 +52,14 @@ struct Node {
     Shared *sh = nullptr;
     std::string name, xname;   // the block's and the exchange's /dev/shm names
     uint64_t hash = 0;
-    char *xchg = nullptr;      // the exchange slots: host mapping, device address
+    char *xchg = nullptr;      // the exchange block: host mapping, device address
     char *xchg_dev = nullptr;
+    // exchange calls so far with each PE, and the readers of this PE's
+    // previous call with the pair counts of that call
+    uint64_t xcount[kMaxPes] = {};
+    int xlast_n = 0;
+    int xlast_pe[kMaxPes] = {};
+    uint64_t xlast_count[kMaxPes] = {};
     int pe = 0, npes = 0;
     uint64_t entered[kMaxPes] = {};     // barriers entered with each peer
     char *own[kNumRegions] = {};
@@ -142,7 +148,12 @@ void unlink_name() {
 }
 
 namespace {
-constexpr size_t kXchgBytes = kMaxPes * kXchgSlotBytes;
+// the slots, then done[reader][writer]
+constexpr size_t kXchgDoneOff = kMaxPes * kXchgSlotBytes;
+constexpr size_t kXchgBytes = kXchgDoneOff + kMaxPes * kMaxPes * sizeof(uint64_t);
+std::atomic<uint64_t> &xchg_word(size_t off, int a, int b) {
+    return reinterpret_cast<std::atomic<uint64_t> *>(g_node.xchg + off)[(size_t)a * kMaxPes + b];
+}
 void xchg_detach() {
     if (!g_node.xchg) return;
     if (g_node.xchg_dev) (void)hipHostUnregister(g_node.xchg);
@@ -188,6 +199,39 @@ char *xchg_host(int q) {
 
 char *xchg_dev(int q) {
     return g_node.xchg_dev && q >= 0 && q < kMaxPes ? g_node.xchg_dev + (size_t)q * kXchgSlotBytes : nullptr;
+}
+
+void xchg_claim(int start, int step, int P, uint64_t *counts) {
+    const int me = g_node.pe;
+    Backoff bo;
+    for (int i = 0; i < g_node.xlast_n; ++i) {
+        const int r = g_node.xlast_pe[i];
+        while (xchg_word(kXchgDoneOff, r, me).load(std::memory_order_acquire) < g_node.xlast_count[i]) {
+            bo.step();
+            if (bo.waited_s > barrier_timeout_s()) {
+                char why[96];
+                snprintf(why, sizeof why, "PE %d never finished reading this PE's exchange slot", r);
+                fatal("node exchange", why);
+            }
+        }
+    }
+    int n = 0;
+    for (int i = 0; i < P; ++i) {
+        const int q = start + i * step;
+        counts[i] = q == me ? 0 : ++g_node.xcount[q];
+        if (q != me) {
+            g_node.xlast_pe[n] = q;
+            g_node.xlast_count[n++] = counts[i];
+        }
+    }
+    g_node.xlast_n = n;
+}
+
+void xchg_finish(int start, int step, int P, const uint64_t *counts) {
+    for (int i = 0; i < P; ++i) {
+        const int q = start + i * step;
+        if (q != g_node.pe) xchg_word(kXchgDoneOff, g_node.pe, q).store(counts[i], std::memory_order_release);
+    }
 }
 
 void detach(bool unlink) {

@@ -71,16 +71,26 @@ uint64_t region_gen(Region r, int pe);
 // open) turns into the same error return on all of them instead of a hang.
 bool agree(int start, int step, int P, bool ok);
 
-// The small-call exchange (staging.cpp, service.hip): one slot of
-// kXchgSlotBytes per PE in a second shared-memory block of the job, page-
-// locked and mapped into this GPU (hipHostRegister), where every member of a
-// small blocking call leaves its source for the others' service workgroups.
-// xchg_attach maps and registers it (false on any error; every PE calls it at
-// init and the job agrees); the name goes with unlink_name().
+// The small-call exchange (staging.cpp, service.hip): a second shared-memory
+// block of the job, page-locked and mapped into this GPU (hipHostRegister),
+// with one slot of kXchgSlotBytes per PE (its source for the others' service
+// workgroups) and, per pair of PEs, how many of their calls together the
+// reader has finished reading the writer's slot for.  A PE writes its slot
+// again only once every reader of its previous call is done with it (host
+// side, at the start of its next call; normally at once), so a call needs no
+// exit barrier.  xchg_attach maps and registers the block (false on any
+// error; every PE calls it at init and the job agrees); the name goes with
+// unlink_name().
 constexpr size_t kXchgSlotBytes = 4096;
 bool xchg_attach();
 char *xchg_host(int pe);   // a slot's host address (nullptr if not attached)
 char *xchg_dev(int pe);    // the same slot's device address
+// Start this PE's part of a call over the members start + i * step, i < P:
+// wait until the readers of its previous call are done with its slot, and
+// count the call with every other member (counts[i] for member i).
+void xchg_claim(int start, int step, int P, uint64_t *counts);
+// After this PE's fold: it is done reading every member's slot of this call.
+void xchg_finish(int start, int step, int P, const uint64_t *counts);
 
 void put_desc(const Desc &d);
 Desc get_desc(int pe);

@@ -524,8 +524,10 @@ static void reduce_blocking_impl2(int type, int op, void *target, const void *so
 // CPU), passes the entry barrier, has its workgroup fold every member's slot
 // (its own order for the pairs where the order decides the answer, else
 // PE_start's, as DIRECT and A2A do) into its target (a host target through
-// the bounce buffer), and passes the exit barrier, after which its slot may
-// be written again.  Host memory is the meeting point, so no GPU reads
+// the bounce buffer), and marks itself done with every member's slot; a
+// member writes its slot again only once the readers of its previous call
+// are done (node::xchg_claim), which takes the place of the reference's exit
+// barrier.  Host memory is the meeting point, so no GPU reads
 // another GPU's memory and no L2 write-back beyond each workgroup's own
 // system-scope release is needed.
 static void xchg_reduce(int type, int op, void *target, bool tdev, const void *source, bool sdev, size_t bytes,
@@ -536,6 +538,8 @@ static void xchg_reduce(int type, int op, void *target, bool tdev, const void *s
               bytes / type_size(type), start, logstride, size, own_order_pair(type, op) ? " (own order)" : "");
     if (!tdev && !small_bounce_reserve())
         fatal("small multi-PE call", "no page-locked bounce buffer for a host target");
+    uint64_t counts[node::kMaxPes];
+    node::xchg_claim(start, step, size, counts);   // the slot is free again
     if (g_state.xchg_src_host) {   // a mirrored-heap source's current view bytes
         std::memcpy(node::xchg_host(g_state.pe), g_state.xchg_src_host, bytes);
     } else if (sdev) {
@@ -548,9 +552,9 @@ static void xchg_reduce(int type, int op, void *target, bool tdev, const void *s
     char *bout = static_cast<char *>(g_state.bounce) + kSmallHostBytes;
     void *dst2 = tdev ? g_state.settle_dst : nullptr;
     service_fold(type, op, own_order_pair(type, op), start, logstride, size, tdev ? target : bout, dst2, bytes);
+    node::xchg_finish(start, step, size, counts);   // (no exit barrier: xchg_claim)
     if (dst2) g_state.settled = true;
     if (!tdev) std::memcpy(target, bout, bytes);
-    node::barrier(start, step, size);
 }
 
 // A blocking call returns as soon as its work's host signal arrives.
