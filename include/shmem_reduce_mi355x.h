@@ -344,8 +344,9 @@ int shmemx_rccl_register_heap(int on);
  * under SHMEMX_ALGO_AUTO is served the same way: each member leaves its
  * source in a page-locked exchange shared by the job's PEs, and after the
  * entry barrier its workgroup folds every member's source into its target
- * (no kernel launch, no GPU reading another GPU's memory), then the exit
- * barrier.  $SHMEMX_SERVICE=0 turns both off (every PE alike); they are also
+ * (no kernel launch, no GPU reading another GPU's memory); a member writes
+ * its part of the exchange again only once the readers of its previous call
+ * are done with it.  $SHMEMX_SERVICE=0 turns both off (every PE alike); they are also
  * off when several PE processes of the job share one GPU, unless
  * $SHMEMX_SERVICE=1.  Stats:
  * out[0] requests served, out[1] launches of the workgroup, out[2] / out[3]
